@@ -1,0 +1,269 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: "RS encode/decode GB/s per GPU and whole node; % of HBM
+roofline", on the CESS segment -> fragment codec (libcessec, HIP kernels for gfx950).
+
+Default workload = BASELINE.json configs[1]: batched encode of 1 GiB of synthetic 16 MiB
+segments per GPU, RS(k=2, m=1), 8 MiB fragments, device-resident (inputs already in HBM when
+the timed region starts). A "step" is one batched encode launch over the rank's 64 segments.
+Bytes counted per segment = (k+m) * F (k fragments read, m written).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4|5]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, weak scaling)
+
+Rank 0 prints one JSON line. `roofline` is the dominant kernel's algorithmic bytes per launch /
+its average launch time (HIP events on the launch stream); `cpu_baseline` times the C oracle
+(oracle/rs_oracle.c, kind "port": the reference ships no codec) on a bounded sample on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MiB = 1 << 20
+GB = 1e9
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+METRIC = "RS encode/decode GB/s per GPU and whole node; % of HBM roofline"
+SEED0 = 0xCE550000
+
+CONFIGS = {
+    # id: (k, m, fragment bytes, segments per GPU, description)
+    2: (2, 1, 8 * MiB, 64, "batched RS(2,1) encode of 1 GiB of 16 MiB segments per GPU"),
+    3: (2, 1, 8 * MiB, 64, "degraded reconstruct RS(2,1), erased fragment = seg mod 3, 1 GiB"),
+    4: (2, 1, 8 * MiB, 4096, "64 GiB file (4096 x 16 MiB segments) encoded, sharded over GPUs"),
+    5: (32, 32, 512 * 1024, 64, "RS(32,32) encode of 1 GiB + SHA-256 of all 64 fragments"),
+}
+
+
+def cpu_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))  # a GPU box gives one GPU a 16-CPU share
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(k: int, m: int, F: int, target_s: float) -> dict:
+    """Time the C oracle (oracle/rs_oracle.c) on a bounded sample of the same workload."""
+    from oracle.c_oracle import load_c_oracle
+    orc = load_c_oracle()
+    simd = orc.orc_set_simd(-1)
+    nseg = 8 if k * F >= 8 * MiB else 64
+    data = np.empty(nseg * k * F, np.uint8)
+    par = np.empty(nseg * m * F, np.uint8)
+    orc.orc_fill_synthetic(data.ctypes.data, k * F, nseg, 0, SEED0 + 2)
+    threads = cpu_threads()
+    orc.orc_encode_batch(k, m, data.ctypes.data, par.ctypes.data, nseg, F, threads, 1)  # touch
+    t1 = orc.orc_encode_batch(k, m, data.ctypes.data, par.ctypes.data, nseg, F, threads, 1)
+    reps = max(1, int(target_s / max(t1, 1e-6)))
+    t = orc.orc_encode_batch(k, m, data.ctypes.data, par.ctypes.data, nseg, F, threads, reps)
+    st = orc.orc_encode_batch(k, m, data.ctypes.data, par.ctypes.data, 1, F, 1, 1)
+    per_seg = (k + m) * F
+    return {
+        "value": round(reps * nseg * per_seg / t / GB, 3),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{reps} x {nseg} segments of {k * F // MiB} MiB, RS({k},{m}), "
+                  f"{'AVX2 split-nibble' if simd == 1 else 'scalar table'} C oracle, "
+                  f"{threads} threads, {t:.1f} s",
+        "value_1thread": round(per_seg / st / GB, 3),
+        "cpu_model": cpu_model(),
+    }
+
+
+def load_traffic(tag: str):
+    """Per-launch HBM bytes from the PMC pass (profiles/traffic_<tag>.json), if collected."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--variant", type=int, default=-1, help="CT kernel variant (tuning)")
+    ap.add_argument("--generic", action="store_true", help="force run-time-coefficient kernel")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import cess_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    k, m, F, nseg_cfg, desc = CONFIGS[args.config]
+    nseg = nseg_cfg // world if args.config == 4 else nseg_cfg
+    seg0 = rank * nseg
+    stream = torch.cuda.current_stream(dev)
+
+    d_data = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
+    d_par = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
+    cess_amd.fill_synthetic(d_data, k * F, nseg, seg0, SEED0 + args.config, stream=stream)
+    enc = cess_amd.New(k, m, device=local)
+    if args.generic:
+        enc.set_option(1, 1)
+    enc.set_option(2, args.variant)
+    enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)  # valid parity for config 3
+
+    present = None
+    if args.config == 3:
+        present = np.ones((nseg, k + m), np.uint8)
+        present[np.arange(nseg), (seg0 + np.arange(nseg)) % (k + m)] = 0
+    d_hex = None
+    if args.config == 5:
+        d_hex = torch.empty((nseg, k + m, 64), dtype=torch.uint8, device=dev)
+
+    def step():
+        if args.config == 3:
+            enc.ReconstructBatch(d_data, d_par, nseg, F, present, stream=stream)
+        else:
+            enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
+            if d_hex is not None:
+                enc.Sha256Batch(d_data, d_par, nseg, F, d_hex, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+
+    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, launch_ms = float(t[0]), float(t[1])
+
+    per_seg = (k + m) * F  # algorithmic bytes per segment (read k*F, write m*F)
+    bytes_step_gpu = nseg * per_seg
+    value = world * bytes_step_gpu * args.steps / elapsed / GB
+    achieved = bytes_step_gpu / (launch_ms * 1e-3) / GB
+
+    sha_note = None
+    if args.config == 5:
+        # the step holds encode + SHA-256; time each kernel alone for the roofline
+        def timed(fn, reps=5):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for _ in range(reps):
+                fn()
+            b.record(stream)
+            torch.cuda.synchronize(dev)
+            return a.elapsed_time(b) / reps
+        enc_ms = timed(lambda: enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream), 20)
+        sha_ms = timed(lambda: enc.Sha256Batch(d_data, d_par, nseg, F, d_hex, stream=stream), 3)
+        achieved = bytes_step_gpu / (enc_ms * 1e-3) / GB
+        sha_note = {"sha256_ms": round(sha_ms, 3), "encode_ms": round(enc_ms, 4),
+                    "sha256_GBps": round(bytes_step_gpu / (sha_ms * 1e-3) / GB, 2),
+                    "streams": nseg * (k + m),
+                    "note": "SHA-256 is one sequential chain per fragment: bounded by streams x "
+                            "per-lane issue rate, reported apart from the HBM roofline"}
+
+    tag = f"c{args.config}"
+    traffic = load_traffic(tag)
+    kernel_name = {2: "k_ct<EncCT<2,1>>", 3: "k_ct<Dec1CT<2,1,*>> / k_ct<EncCT<2,1>>",
+                   4: "k_ct<EncCT<2,1>>", 5: "k_ct<EncCT<32,32>>"}[args.config]
+    if args.generic:
+        kernel_name = "k_rt"
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak" if args.config != 4 else "strong",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 counter generator, generated in HBM)",
+        "config": {"workload": desc, "baseline_config": args.config, "k": k, "m": m,
+                   "fragment_bytes": F, "segments_per_gpu": nseg,
+                   "bytes_per_step_per_gpu": bytes_step_gpu, "parallelism": f"shard{world}",
+                   "kernel": kernel_name},
+        "per_gpu_GBps": round(value / world, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": traffic, "launch_ms": round(launch_ms, 4),
+                     "algorithmic_bytes_per_launch": bytes_step_gpu},
+    }
+    if sha_note:
+        out["sha256"] = sha_note
+
+    if not args.no_extra and args.config == 2:
+        # decode rate in the same process (BASELINE config 3 workload, same bytes)
+        pres = np.ones((nseg, k + m), np.uint8)
+        pres[np.arange(nseg), (seg0 + np.arange(nseg)) % (k + m)] = 0
+        for _ in range(3):
+            enc.ReconstructBatch(d_data, d_par, nseg, F, pres, stream=stream)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(20):
+            enc.ReconstructBatch(d_data, d_par, nseg, F, pres, stream=stream)
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        dms = a.elapsed_time(b) / 20
+        out["extra"] = {"reconstruct_GBps_per_gpu": round(bytes_step_gpu / (dms * 1e-3) / GB, 2),
+                        "reconstruct_ms": round(dms, 4)}
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(k, m, F, args.cpu_seconds)
+
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

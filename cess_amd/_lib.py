@@ -1,0 +1,66 @@
+"""ctypes binding of libcessec (include/cess_ec.h). No fallback: a missing or unloadable library
+raises, so nothing silently runs on the CPU."""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CESS_EC_LIB", os.path.join(_HERE, "libcessec.so"))
+
+# exported symbols and their (restype, argtypes); tests check this against include/cess_ec.h
+SIGNATURES = {
+    "cec_version": (c_char_p, []),
+    "cec_strerror": (c_char_p, [c_int]),
+    "cec_last_error": (c_char_p, []),
+    "cec_device_count": (c_int, []),
+    "cec_create": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),
+    "cec_destroy": (None, [c_void_p]),
+    "cec_matrix": (c_int, [c_void_p, POINTER(c_uint8)]),
+    "cec_encode": (c_int, [c_void_p, POINTER(c_void_p), c_size_t]),
+    "cec_reconstruct": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint8), c_size_t, c_int]),
+    "cec_verify": (c_int, [c_void_p, POINTER(c_void_p), c_size_t, POINTER(c_int)]),
+    "cec_encode_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]),
+    "cec_reconstruct_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t,
+                                      POINTER(c_uint8), c_int, c_int, c_void_p]),
+    "cec_sha256_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p,
+                                 c_void_p]),
+    "cec_sha256_hex": (c_int, [POINTER(c_void_p), c_size_t, c_size_t, POINTER(c_uint8),
+                               c_void_p]),
+    "cec_split_segment": (c_int, [c_void_p, c_size_t, c_int, POINTER(c_void_p), c_size_t]),
+    "cec_fill_synthetic": (c_int, [c_void_p, c_size_t, c_size_t, c_uint64, c_uint64, c_void_p]),
+    "cec_set_option": (c_int, [c_void_p, c_int, c_int]),
+}
+
+CEC_OK = 0
+CEC_EINVAL = -1
+CEC_ETOOFEW = -2
+CEC_ESHARDLEN = -3
+CEC_EHIP = -4
+CEC_ENOMEM = -5
+CEC_ENCCL = -6
+CEC_ESHORTDATA = -7
+CEC_ENODEV = -8
+
+CEC_OPT_FORCE_GENERIC = 1
+CEC_OPT_CT_VARIANT = 2
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libcessec once; raises OSError with a build hint when it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"libcessec not found at {LIB_PATH}: build it with "
+                          "`python -c 'import __graft_entry__ as g; g.build()'` "
+                          "or `make -C cess_amd/csrc`")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib

@@ -1,0 +1,175 @@
+// GF(2^8) field and coding-matrix construction for the CESS segment -> fragment codec.
+//
+// Product code (host + compile-time). The oracle under oracle/ is an independent restatement
+// and is never included from here.
+//
+// Convention: the systematic Vandermonde code used by the
+// off-chain CESS tools (klauspost/reedsolomon `New(k, m)` default matrix, the same as
+// Backblaze JavaReedSolomon):
+//   * field GF(2^8), reduction polynomial x^8+x^4+x^3+x^2+1 (0x11D), generator 2;
+//   * V[r][c] = r^c (0^0 = 1) for r in [0, k+m), c in [0, k);
+//   * E = V * inv(V[0:k, :]) so E[0:k] = I (data shards pass through) and E[k+i] is the
+//     coefficient row of parity shard i;
+//   * reconstruct: take the first k present rows S of E (in index order), D = inv(E[S]);
+//     a missing data shard d is row d of D applied to the survivors; a missing parity shard
+//     p is E[p] * D applied to the survivors (bit-identical to klauspost's two-pass
+//     "data first, then re-encode parity", since GF arithmetic is exact).
+//
+// Geometry that fixes k and m for CESS: SEGMENT_SIZE = 16 MiB and FRAGMENT_SIZE = 8 MiB
+// (reference primitives/common/src/lib.rs:60-61) give k = 2; FRAGMENT_COUNT = 3
+// (reference runtime/src/lib.rs:1027) gives m = 1.
+#pragma once
+#include <stdint.h>
+
+namespace cec {
+
+constexpr unsigned kPoly = 0x11D;
+constexpr int kMaxShards = 256;
+
+struct GfTables {
+  uint8_t exp[512];  // exp[i] = 2^i, doubled so exp[log a + log b] needs no modulo
+  uint8_t log[256];  // log[0] unused
+};
+
+constexpr GfTables make_gf_tables() {
+  GfTables t{};
+  unsigned x = 1;
+  for (int i = 0; i < 255; ++i) {
+    t.exp[i] = (uint8_t)x;
+    t.log[x] = (uint8_t)i;
+    x <<= 1;
+    if (x & 0x100) x ^= kPoly;
+  }
+  for (int i = 255; i < 512; ++i) t.exp[i] = t.exp[i - 255];
+  return t;
+}
+
+inline constexpr GfTables kGf = make_gf_tables();
+
+constexpr uint8_t gf_mul(uint8_t a, uint8_t b) {
+  if (a == 0 || b == 0) return 0;
+  return kGf.exp[kGf.log[a] + kGf.log[b]];
+}
+
+constexpr uint8_t gf_inv(uint8_t a) {  // a != 0
+  return kGf.exp[255 - kGf.log[a]];
+}
+
+// a^n with 0^0 = 1 (klauspost galExp semantics).
+constexpr uint8_t gf_pow(uint8_t a, int n) {
+  if (n == 0) return 1;
+  if (a == 0) return 0;
+  return kGf.exp[(kGf.log[a] * n) % 255];
+}
+
+// Fixed-capacity row-major matrix usable both in constant evaluation (small R, C) and at run
+// time (heap-allocated with R = C = kMaxShards).
+template <int R, int C>
+struct Mat {
+  int rows = 0, cols = 0;
+  uint8_t v[R][C] = {};
+};
+
+// Gauss-Jordan inverse of the n x n matrix `a` (read from a.v[0..n)[0..n)). Returns false when
+// singular. `work` must have room for n x 2n.
+template <int R, int C, int R2, int C2>
+constexpr bool gf_invert(const Mat<R, C>& a, int n, Mat<R, C>& out, Mat<R2, C2>& work) {
+  work.rows = n;
+  work.cols = 2 * n;
+  for (int r = 0; r < n; ++r)
+    for (int c = 0; c < 2 * n; ++c)
+      work.v[r][c] = c < n ? a.v[r][c] : (uint8_t)(c - n == r ? 1 : 0);
+  for (int col = 0; col < n; ++col) {
+    int piv = -1;
+    for (int r = col; r < n; ++r)
+      if (work.v[r][col] != 0) { piv = r; break; }
+    if (piv < 0) return false;
+    if (piv != col)
+      for (int c = 0; c < 2 * n; ++c) {
+        uint8_t t = work.v[col][c];
+        work.v[col][c] = work.v[piv][c];
+        work.v[piv][c] = t;
+      }
+    const uint8_t s = gf_inv(work.v[col][col]);
+    for (int c = 0; c < 2 * n; ++c) work.v[col][c] = gf_mul(work.v[col][c], s);
+    for (int r = 0; r < n; ++r) {
+      if (r == col || work.v[r][col] == 0) continue;
+      const uint8_t f = work.v[r][col];
+      for (int c = 0; c < 2 * n; ++c) work.v[r][c] ^= gf_mul(f, work.v[col][c]);
+    }
+  }
+  out.rows = out.cols = n;
+  for (int r = 0; r < n; ++r)
+    for (int c = 0; c < n; ++c) out.v[r][c] = work.v[r][n + c];
+  return true;
+}
+
+// Full (k+m) x k systematic encode matrix E into `e`. `tmp*` are scratch of the same type.
+template <int R, int C, int R2, int C2>
+constexpr bool gf_encode_matrix(int k, int m, Mat<R, C>& e, Mat<R, C>& top, Mat<R, C>& topinv,
+                                Mat<R2, C2>& work) {
+  const int n = k + m;
+  // V[r][c] = r^c, only its top k x k block is needed for the inverse.
+  top.rows = top.cols = k;
+  for (int r = 0; r < k; ++r)
+    for (int c = 0; c < k; ++c) top.v[r][c] = gf_pow((uint8_t)r, c);
+  if (!gf_invert(top, k, topinv, work)) return false;
+  e.rows = n;
+  e.cols = k;
+  for (int r = 0; r < n; ++r)
+    for (int c = 0; c < k; ++c) {
+      uint8_t acc = 0;
+      for (int t = 0; t < k; ++t) acc ^= gf_mul(gf_pow((uint8_t)r, t), topinv.v[t][c]);
+      e.v[r][c] = acc;
+    }
+  return true;
+}
+
+// Reconstruction plan for one erasure pattern: which k survivors are read, which missing shards
+// are written, and the nout x k coefficient matrix mapping survivors to outputs.
+template <int R, int C>
+struct Plan {
+  int k = 0, nout = 0;
+  uint8_t in_idx[R] = {};   // survivor shard indices (first k present, ascending)
+  uint8_t out_idx[R] = {};  // shard indices written
+  Mat<R, C> coef;           // nout x k
+};
+
+// Build the decode plan. `present[i]` != 0 marks shard i as available. With data_only, only
+// missing data shards are produced. Returns 0 on success, -1 if fewer than k shards survive.
+template <int R, int C, int R2, int C2>
+constexpr int gf_decode_plan(int k, int m, const uint8_t* present, bool data_only,
+                             const Mat<R, C>& e, Plan<R, C>& plan, Mat<R, C>& sub,
+                             Mat<R, C>& inv, Mat<R2, C2>& work) {
+  const int n = k + m;
+  plan.k = k;
+  int got = 0;
+  for (int i = 0; i < n && got < k; ++i)
+    if (present[i]) plan.in_idx[got++] = (uint8_t)i;
+  if (got < k) return -1;
+  sub.rows = sub.cols = k;
+  for (int r = 0; r < k; ++r)
+    for (int c = 0; c < k; ++c) sub.v[r][c] = e.v[plan.in_idx[r]][c];
+  if (!gf_invert(sub, k, inv, work)) return -1;  // cannot happen for this code (MDS)
+  plan.nout = 0;
+  for (int i = 0; i < n; ++i) {
+    if (present[i]) continue;
+    if (data_only && i >= k) continue;
+    const int o = plan.nout++;
+    plan.out_idx[o] = (uint8_t)i;
+    for (int c = 0; c < k; ++c) {
+      if (i < k) {
+        plan.coef.v[o][c] = inv.v[i][c];
+      } else {
+        uint8_t acc = 0;
+        for (int t = 0; t < k; ++t) acc ^= gf_mul(e.v[i][t], inv.v[t][c]);
+        plan.coef.v[o][c] = acc;
+      }
+    }
+  }
+  plan.coef.rows = plan.nout;
+  plan.coef.cols = k;
+  return 0;
+}
+
+}  // namespace cec

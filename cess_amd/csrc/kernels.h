@@ -1,0 +1,61 @@
+// Host-side launch interface of the HIP kernels in kernels.hip (internal to libcessec).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cec {
+
+// Where shard `i` of segment `s` lives in HBM. The batched device layout of the C ABI is
+// [seg][shard][len] for data and for parity, i.e. for i < k:
+//   data   + s * data_seg_stride + i * shard_stride
+// and for i >= k:
+//   parity + s * par_seg_stride + (i - k) * shard_stride.
+struct Layout {
+  uint8_t* data;
+  uint8_t* parity;
+  uint64_t len;              // bytes per shard
+  uint64_t shard_stride;     // bytes between consecutive shards of one segment
+  uint64_t data_seg_stride;  // bytes between consecutive segments in `data`
+  uint64_t par_seg_stride;   // bytes between consecutive segments in `parity`
+  int k;
+};
+
+// Survivor / output shard indices for the run-time-coefficient kernel (passed by value).
+struct RtSel {
+  uint8_t in[256];
+  uint8_t out[256];
+};
+
+// True when every shard start and the shard length allow 16-byte vector access.
+bool layout_vec16_ok(const Layout& L);
+
+// Compile-time-coefficient kernels. Return false if no specialised kernel exists for the
+// request (caller then uses the run-time kernel).
+bool launch_encode_ct(int k, int m, const Layout& L, const uint32_t* seg_list, uint32_t nseg,
+                      hipStream_t st);
+// Decode for a single erasure of RS(k, m) codes that have a specialised plan; `missing` is the
+// erased shard index and `data_only` drops a parity output.
+bool launch_decode_ct(int k, int m, int missing, const Layout& L, const uint32_t* seg_list,
+                      uint32_t nseg, hipStream_t st);
+
+// Largest output count one run-time launch handles; more outputs are split over launches.
+constexpr int kRtMaxOut = 32;
+// Bucketed output count the run-time kernel is instantiated for (>= nout).
+int rt_bucket(int nout);
+// Run-time coefficient GF matvec: out[r] = XOR_j coef[j][r] * in[j]. `dcoef` is a device array
+// laid out [nin][rt_bucket(nout)] of uint32 (one coefficient byte per word, zero padded).
+void launch_matvec_rt(const Layout& L, const RtSel& sel, int nin, int nout, const uint32_t* dcoef,
+                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
+
+// SHA-256 of `n` equal-length buffers, written as 64 lowercase hex characters each into
+// `hex_out` (device, n * 64 bytes). If `ptrs` is null, buffer i is shard (i % nshards) of
+// segment (i / nshards) in layout L.
+void launch_sha256_hex(const uint8_t* const* ptrs, const Layout* L, int nshards, uint64_t n,
+                       uint64_t len, uint8_t* hex_out, hipStream_t st);
+
+// Synthetic segment bytes: 64-bit word w of segment s = splitmix64(seed ^ (s << 32) ^ w),
+// little-endian; segments are seg_bytes long and contiguous from `out`.
+void launch_fill_splitmix(uint8_t* out, uint64_t seg_bytes, uint64_t nseg, uint64_t seg0,
+                          uint64_t seed, hipStream_t st);
+
+}  // namespace cec

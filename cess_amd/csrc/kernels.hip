@@ -1,0 +1,675 @@
+// HIP kernels for the CESS segment -> fragment Reed-Solomon codec on MI355X (gfx950, CDNA4).
+//
+// Everything here is HBM-streaming integer work: a GF(2^8) matrix-vector product over byte
+// columns ("out[r] = XOR_j c[r][j] * in[j]") for encode and reconstruct, a per-fragment SHA-256,
+// and a counter-based synthetic-data generator. There is no MFMA: GF(2^8) multiply-accumulate
+// is not a float contraction.
+//
+// GF multiply by a constant is done without tables: 2*x on four packed bytes is one "xtime"
+// (shift, mask, conditional reduction by 0x1D = 6 VALU ops per dword), and c*x is the XOR of
+// the xtime powers 2^b*x selected by the set bits of c.
+//  * Compile-time coefficient kernels (k_ct): the coefficient matrix is a constexpr of the
+//    template, so after unrolling only the XORs for set bits are emitted (about 0.5 VALU op per
+//    byte per coefficient). Small input counts use a Horner form per output row
+//    (y = 2*y ^ XOR_{j: bit b of c[r][j]} x_j, b = 7..0), large ones stream the inputs and keep
+//    one accumulator per output.
+//  * Run-time coefficient kernel (k_rt): coefficients arrive through scalar loads and are
+//    expanded to per-bit masks on the SALU; each (input, output, bit) is one v_bitop3
+//    (acc ^= pow_b & mask_b).
+// Each lane owns 16-byte columns (global_load_dwordx4) of every shard; blockIdx.y is the
+// segment. A shard length that is not a multiple of 16 is finished byte-wise by the last block.
+#include <utility>
+
+#include "gf256.h"
+#include "kernels.h"
+
+namespace cec {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Every lambda on the compile-time path is force-inlined: an outlined body turns into a call
+// with the Layout spilled to scratch.
+#define CEC_AI __attribute__((always_inline))
+
+template <class T>
+__device__ __forceinline__ T xt(T x) {
+  const T hi = x & 0x80808080u;
+  return ((x << 1) & 0xfefefefeu) ^ ((hi - (hi >> 7)) & 0x1d1d1d1du);
+}
+
+__device__ __forceinline__ uint8_t* shard_ptr(const Layout& L, int idx, uint32_t seg) {
+  return idx < L.k ? L.data + seg * L.data_seg_stride + (uint64_t)idx * L.shard_stride
+                   : L.parity + seg * L.par_seg_stride + (uint64_t)(idx - L.k) * L.shard_stride;
+}
+
+// Shard pointer with the data/parity split known at compile time (K = data shard count).
+template <int K, int IDX>
+__device__ __forceinline__ uint8_t* shard_ptr_ct(const Layout& L, uint32_t seg) {
+  if constexpr (IDX < K) return L.data + seg * L.data_seg_stride + (uint64_t)IDX * L.shard_stride;
+  else return L.parity + seg * L.par_seg_stride + (uint64_t)(IDX - K) * L.shard_stride;
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  else return *reinterpret_cast<const u32x4*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  else *reinterpret_cast<u32x4*>(p) = v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Compile-time plans
+// ---------------------------------------------------------------------------------------------
+template <int NI, int NO>
+struct CoefCT {
+  uint8_t c[NO][NI];
+  uint8_t in[NI];
+  uint8_t out[NO];
+  int8_t hb_col[NI];  // highest set bit over column j (-1 if the column is zero)
+  int8_t hb_row[NO];  // highest set bit over row r
+};
+
+constexpr int hibit(unsigned c) {
+  int h = -1;
+  for (int b = 0; b < 8; ++b)
+    if (c >> b & 1) h = b;
+  return h;
+}
+
+template <int NI, int NO>
+constexpr void finish_ct(CoefCT<NI, NO>& r) {
+  for (int j = 0; j < NI; ++j) {
+    int h = -1;
+    for (int o = 0; o < NO; ++o) h = hibit(r.c[o][j]) > h ? hibit(r.c[o][j]) : h;
+    r.hb_col[j] = (int8_t)h;
+  }
+  for (int o = 0; o < NO; ++o) {
+    int h = -1;
+    for (int j = 0; j < NI; ++j) h = hibit(r.c[o][j]) > h ? hibit(r.c[o][j]) : h;
+    r.hb_row[o] = (int8_t)h;
+  }
+}
+
+template <int K, int M>
+constexpr CoefCT<K, M> make_encode_ct() {
+  Mat<64, 64> e, top, topinv;
+  Mat<64, 128> work;
+  gf_encode_matrix(K, M, e, top, topinv, work);
+  CoefCT<K, M> r{};
+  for (int o = 0; o < M; ++o)
+    for (int j = 0; j < K; ++j) r.c[o][j] = e.v[K + o][j];
+  for (int j = 0; j < K; ++j) r.in[j] = (uint8_t)j;
+  for (int o = 0; o < M; ++o) r.out[o] = (uint8_t)(K + o);
+  finish_ct(r);
+  return r;
+}
+
+// Single-erasure decode of RS(K, M): survivors are the first K present shards.
+template <int K, int M, int MISSING>
+constexpr CoefCT<K, 1> make_decode1_ct() {
+  Mat<64, 64> e, top, topinv, sub, inv;
+  Mat<64, 128> work;
+  gf_encode_matrix(K, M, e, top, topinv, work);
+  uint8_t present[64] = {};
+  for (int i = 0; i < K + M; ++i) present[i] = i != MISSING;
+  Plan<64, 64> p;
+  gf_decode_plan(K, M, present, false, e, p, sub, inv, work);
+  CoefCT<K, 1> r{};
+  for (int j = 0; j < K; ++j) r.c[0][j] = p.coef.v[0][j];
+  for (int j = 0; j < K; ++j) r.in[j] = p.in_idx[j];
+  r.out[0] = p.out_idx[0];
+  finish_ct(r);
+  return r;
+}
+
+template <int K_, int M>
+struct EncCT {
+  static constexpr int K = K_;
+  static constexpr int NI = K_, NO = M;
+  static constexpr CoefCT<K_, M> v = make_encode_ct<K_, M>();
+};
+template <int K_, int M, int MISSING>
+struct Dec1CT {
+  static constexpr int K = K_;
+  static constexpr int NI = K_, NO = 1;
+  static constexpr CoefCT<K, 1> v = make_decode1_ct<K_, M, MISSING>();
+};
+
+// Horner form pays one xtime per bit of the largest row coefficient; the streaming form one per
+// bit of the largest column coefficient. Horner needs every input column resident.
+template <class P>
+constexpr bool use_horner(int u) {
+  int ch = 0, cp = 0;
+  for (int o = 0; o < P::NO; ++o) ch += P::v.hb_row[o] > 0 ? P::v.hb_row[o] : 0;
+  for (int j = 0; j < P::NI; ++j) cp += P::v.hb_col[j] > 0 ? P::v.hb_col[j] : 0;
+  return P::NI <= 8 && P::NI * u * 4 <= 64 && ch <= cp;
+}
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1, fully expanded, so the
+// coefficient reads below are constant expressions and only the XORs of set bits are emitted.
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  [&]<int... I>(std::integer_sequence<int, I...>) CEC_AI {
+    (f(std::integral_constant<int, I>{}), ...);
+  }(std::make_integer_sequence<int, N>{});
+}
+
+// XOR helpers on v_bitop3 (truth table 0x96 = a ^ b ^ c). The intrinsic is opaque to LLVM's
+// reassociation, which would otherwise rebuild the per-output XOR chains as trees over every
+// input power and keep them all live (hundreds of VGPRs, scratch spills on wide codes).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ u32x4 xor3(u32x4 a, u32x4 b, u32x4 c) {
+  return u32x4{xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y), xor3(a.z, b.z, c.z),
+               xor3(a.w, b.w, c.w)};
+}
+template <class T>
+__device__ __forceinline__ T xor2(T a, T b) {
+  return xor3(a, b, T(0));
+}
+
+struct BitList {
+  int n;
+  int b[8];
+};
+constexpr BitList set_bits(unsigned c) {
+  BitList r{};
+  for (int b = 0; b < 8; ++b)
+    if (c >> b & 1) r.b[r.n++] = b;
+  return r;
+}
+
+// acc ^= XOR of p[b] over the set bits b of constant C, two terms per v_bitop3.
+template <unsigned C, class T>
+__device__ __forceinline__ T mul_acc(T acc, const T (&p)[8]) {
+  constexpr BitList bl = set_bits(C);
+  static_for<(bl.n + 1) / 2>([&](auto Q) CEC_AI {
+    constexpr int q = Q;
+    if constexpr (2 * q + 1 < bl.n) acc = xor3(acc, p[bl.b[2 * q]], p[bl.b[2 * q + 1]]);
+    else acc = xor2(acc, p[bl.b[2 * q]]);
+  });
+  return acc;
+}
+
+// out = C * x for one column element of type T (u32x4 for the vector body, uint32_t bytes for
+// the tail). `ld(J)` returns input column J, `st(O, y)` stores output O (J, O integral
+// constants).
+template <class P, class T, class LD, class ST>
+__device__ __forceinline__ void ct_column_horner(LD ld, ST st) {
+  T x[P::NI];
+  static_for<P::NI>([&](auto J) CEC_AI { x[J] = ld(J); });
+  static_for<P::NO>([&](auto O) CEC_AI {
+    constexpr int o = O;
+    T y = T(0);
+    static_for<8>([&](auto B) CEC_AI {
+      constexpr int b = 7 - B;
+      if constexpr (b < P::v.hb_row[o]) y = xt(y);
+      // inputs whose coefficient has bit b set, XORed two at a time
+      constexpr auto sel = [] {
+        BitList r{};  // reuse as an index list (NI <= 8 here)
+        int n = 0;
+        int idx[P::NI] = {};
+        for (int j = 0; j < P::NI; ++j)
+          if ((P::v.c[o][j] >> b) & 1) idx[n++] = j;
+        r.n = n;
+        for (int t = 0; t < n && t < 8; ++t) r.b[t] = idx[t];
+        return r;
+      }();
+      static_assert(sel.n <= 8, "Horner form is for narrow codes");
+      static_for<(sel.n + 1) / 2>([&](auto Q) CEC_AI {
+        constexpr int q = Q;
+        if constexpr (2 * q + 1 < sel.n) y = xor3(y, x[sel.b[2 * q]], x[sel.b[2 * q + 1]]);
+        else y = xor2(y, x[sel.b[2 * q]]);
+      });
+    });
+    st(O, y);
+  });
+}
+
+template <class P, class T, class LD, class ST>
+__device__ __forceinline__ void ct_column_stream(LD ld, ST st) {
+  T acc[P::NO];
+  static_for<P::NO>([&](auto O) CEC_AI { acc[O] = T(0); });
+  static_for<P::NI>([&](auto J) CEC_AI {
+    constexpr int j = J;
+    T p[8];
+    p[0] = ld(J);
+    static_for<7>([&](auto B) CEC_AI {
+      constexpr int b = B + 1;
+      if constexpr (b <= P::v.hb_col[j]) p[b] = xt(p[b - 1]);
+    });
+    static_for<P::NO>([&](auto O) CEC_AI {
+      constexpr int o = O;
+      acc[o] = mul_acc<P::v.c[o][j]>(acc[o], p);
+    });
+    // Keep one input column live at a time.
+    if constexpr (P::NO > 8) __builtin_amdgcn_sched_barrier(0);
+  });
+  static_for<P::NO>([&](auto O) CEC_AI { st(O, acc[O]); });
+}
+
+// Byte-wise finish of the last (len % 16) bytes, run by the last block of each segment.
+template <class P>
+__device__ __forceinline__ void ct_tail(const Layout& L, uint32_t seg) {
+  const uint64_t t0 = L.len & ~uint64_t(15);
+  const uint64_t i = t0 + threadIdx.x;
+  if (i >= L.len) return;
+  auto ld = [&](auto J) CEC_AI -> uint32_t {
+    return shard_ptr_ct<P::K, P::v.in[J]>(L, seg)[i];
+  };
+  auto st = [&](auto O, uint32_t y) CEC_AI {
+    shard_ptr_ct<P::K, P::v.out[O]>(L, seg)[i] = (uint8_t)y;
+  };
+  if constexpr (use_horner<P>(1)) ct_column_horner<P, uint32_t>(ld, st);
+  else ct_column_stream<P, uint32_t>(ld, st);
+}
+
+template <class P, int U, bool NT>
+__global__ __launch_bounds__(256) void k_ct(Layout L, const uint32_t* __restrict__ seg_list,
+                                            uint32_t seg0) {
+  const uint32_t seg = seg_list ? seg_list[seg0 + blockIdx.y] : seg0 + blockIdx.y;
+  const uint64_t nvec = L.len >> 4;
+  const uint64_t base = (uint64_t)blockIdx.x * (256 * U) + threadIdx.x;
+  // Shard pointers are recomputed per use (scalar base + index * stride): holding 2 * (NI + NO)
+  // SGPRs of pointers live across the body overflows the SGPR file for wide codes.
+  auto column = [&](uint64_t v) CEC_AI {
+    const uint64_t off = v << 4;
+    auto ld = [&](auto J) CEC_AI {
+      return ld16<NT>(shard_ptr_ct<P::K, P::v.in[J]>(L, seg) + off);
+    };
+    auto st = [&](auto O, u32x4 y) CEC_AI {
+      st16<NT>(shard_ptr_ct<P::K, P::v.out[O]>(L, seg) + off, y);
+    };
+    if constexpr (use_horner<P>(U)) ct_column_horner<P, u32x4>(ld, st);
+    else ct_column_stream<P, u32x4>(ld, st);
+  };
+  if (base + (U - 1) * 256 < nvec) {  // full tile: no per-element predicate
+    static_for<U>([&](auto u) CEC_AI { column(base + u * 256); });
+  } else {
+    static_for<U>([&](auto u) CEC_AI {
+      if (base + u * 256 < nvec) column(base + u * 256);
+    });
+  }
+  if ((L.len & 15) && blockIdx.x == gridDim.x - 1) ct_tail<P>(L, seg);
+}
+
+// Byte-granular variant for layouts whose shard starts are not 16-byte aligned.
+template <class P>
+__global__ __launch_bounds__(256) void k_ct_bytes(Layout L, const uint32_t* __restrict__ seg_list,
+                                                  uint32_t seg0) {
+  const uint32_t seg = seg_list ? seg_list[seg0 + blockIdx.y] : seg0 + blockIdx.y;
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= L.len) return;
+  auto ld = [&](auto J) CEC_AI -> uint32_t {
+    return shard_ptr_ct<P::K, P::v.in[J]>(L, seg)[i];
+  };
+  auto st = [&](auto O, uint32_t y) CEC_AI {
+    shard_ptr_ct<P::K, P::v.out[O]>(L, seg)[i] = (uint8_t)y;
+  };
+  if constexpr (use_horner<P>(1)) ct_column_horner<P, uint32_t>(ld, st);
+  else ct_column_stream<P, uint32_t>(ld, st);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Run-time coefficients
+// ---------------------------------------------------------------------------------------------
+template <class T>
+__device__ __forceinline__ T sel_mask(T p, uint32_t m) {
+  return p & m;
+}
+
+// coef layout: [nin][NOB] uint32, one coefficient per word.
+template <int NOB, int U, class T, class LD>
+__device__ __forceinline__ void rt_accumulate(T (&acc)[NOB][U], int nin,
+                                              const uint32_t* __restrict__ coef, LD ld) {
+  for (int j = 0; j < nin; ++j) {
+    T p[8][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) p[0][u] = ld(j, u);
+#pragma unroll
+    for (int b = 1; b < 8; ++b)
+#pragma unroll
+      for (int u = 0; u < U; ++u) p[b][u] = xt(p[b - 1][u]);
+#pragma unroll
+    for (int o = 0; o < NOB; ++o) {
+      const uint32_t c = coef[j * NOB + o];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint32_t m = (uint32_t)(-(int32_t)((c >> b) & 1u));
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[o][u] ^= p[b][u] & m;
+      }
+    }
+  }
+}
+
+template <int NOB, int U>
+__global__ __launch_bounds__(256) void k_rt(Layout L, RtSel sel, int nin, int nout,
+                                            const uint32_t* __restrict__ coef,
+                                            const uint32_t* __restrict__ seg_list, uint32_t seg0,
+                                            int vec_ok) {
+  const uint32_t seg = seg_list ? seg_list[seg0 + blockIdx.y] : seg0 + blockIdx.y;
+  if (vec_ok) {
+    const uint64_t nvec = L.len >> 4;
+    const uint64_t base = (uint64_t)blockIdx.x * (256 * U) + threadIdx.x;
+    u32x4 acc[NOB][U];
+#pragma unroll
+    for (int o = 0; o < NOB; ++o)
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[o][u] = u32x4(0);
+    auto ld = [&](int j, int u) CEC_AI -> u32x4 {
+      const uint64_t v = base + u * 256;
+      if (v >= nvec) return u32x4(0);
+      return ld16<false>(shard_ptr(L, sel.in[j], seg) + (v << 4));
+    };
+    rt_accumulate<NOB, U, u32x4>(acc, nin, coef, ld);
+#pragma unroll
+    for (int o = 0; o < NOB; ++o) {
+      if (o < nout) {
+        uint8_t* dst = shard_ptr(L, sel.out[o], seg);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint64_t v = base + u * 256;
+          if (v < nvec) st16<false>(dst + (v << 4), acc[o][u]);
+        }
+      }
+    }
+    if (!(L.len & 15) || blockIdx.x != gridDim.x - 1) return;
+  }
+  // byte path: whole shard (vec_ok == 0, grid covers len) or the tail (last block)
+  const uint64_t i = vec_ok ? (L.len & ~uint64_t(15)) + threadIdx.x
+                            : (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= L.len) return;
+  uint32_t acc[NOB][1];
+#pragma unroll
+  for (int o = 0; o < NOB; ++o) acc[o][0] = 0;
+  auto ld = [&](int j, int) CEC_AI -> uint32_t { return shard_ptr(L, sel.in[j], seg)[i]; };
+  rt_accumulate<NOB, 1, uint32_t>(acc, nin, coef, ld);
+#pragma unroll
+  for (int o = 0; o < NOB; ++o)
+    if (o < nout) shard_ptr(L, sel.out[o], seg)[i] = (uint8_t)acc[o][0];
+}
+
+// ---------------------------------------------------------------------------------------------
+// SHA-256 (FIPS 180-4), one lane per buffer.
+// ---------------------------------------------------------------------------------------------
+__constant__ uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) {
+  return __builtin_amdgcn_alignbit(x, x, n);
+}
+
+__device__ __forceinline__ void sha256_block(uint32_t (&h)[8], uint32_t (&w)[16]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+      const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
+      const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+      wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
+      w[t & 15] = wt;
+    }
+    const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = hh + S1 + ch + kSha256K[t] + wt;
+    const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+    const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t t2 = S0 + maj;
+    hh = g; g = f; f = e; e = d + t1;
+    d = c; c = b; b = a; a = t1 + t2;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+__global__ __launch_bounds__(64) void k_sha256(const uint8_t* const* __restrict__ ptrs, Layout L,
+                                               int nshards, uint64_t n, uint64_t len,
+                                               uint8_t* __restrict__ hex_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* src =
+      ptrs ? ptrs[i] : shard_ptr(L, (int)(i % nshards), (uint32_t)(i / nshards));
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint32_t w[16];
+  const uint64_t nfull = len >> 6;
+  const bool al16 = ((uintptr_t)src & 15) == 0;
+  for (uint64_t blk = 0; blk < nfull; ++blk) {
+    const uint8_t* p = src + (blk << 6);
+    if (al16) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(p + 16 * q);
+        w[4 * q + 0] = __builtin_bswap32(v.x);
+        w[4 * q + 1] = __builtin_bswap32(v.y);
+        w[4 * q + 2] = __builtin_bswap32(v.z);
+        w[4 * q + 3] = __builtin_bswap32(v.w);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        w[q] = (uint32_t)p[4 * q] << 24 | (uint32_t)p[4 * q + 1] << 16 |
+               (uint32_t)p[4 * q + 2] << 8 | (uint32_t)p[4 * q + 3];
+    }
+    sha256_block(h, w);
+  }
+  // Padding: remaining r bytes, 0x80, zeros, 64-bit big-endian bit length.
+  const uint32_t r = (uint32_t)(len & 63);
+  const uint8_t* p = src + (nfull << 6);
+  const uint64_t bits = len << 3;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t pos = 4 * q + s;
+      const uint32_t byte = pos < r ? p[pos] : (pos == r ? 0x80u : 0u);
+      word |= byte << (24 - 8 * s);
+    }
+    w[q] = word;
+  }
+  if (r >= 56) {
+    sha256_block(h, w);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) w[q] = 0;
+  }
+  w[14] = (uint32_t)(bits >> 32);
+  w[15] = (uint32_t)bits;
+  sha256_block(h, w);
+  uint8_t* o = hex_out + i * 64;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    uint32_t word = h[q];
+    uint32_t lo = 0, hi = 0;  // 8 hex chars of this word, packed little-endian for 2 stores
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const uint32_t nib = (word >> (28 - 4 * s)) & 15u;
+      const uint32_t ch = nib < 10 ? '0' + nib : 'a' + nib - 10;
+      if (s < 4) lo |= ch << (8 * s);
+      else hi |= ch << (8 * (s - 4));
+    }
+    *reinterpret_cast<uint32_t*>(o + 8 * q) = lo;
+    *reinterpret_cast<uint32_t*>(o + 8 * q + 4) = hi;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Synthetic segments
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_fill(uint8_t* __restrict__ out, uint64_t seg_bytes,
+                                              uint64_t nseg, uint64_t seg0, uint64_t seed) {
+  const uint64_t words_per_seg = seg_bytes >> 3;
+  const uint64_t total = words_per_seg * nseg;
+  uint64_t* o = reinterpret_cast<uint64_t*>(out);
+  for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 2; i < total;
+       i += (uint64_t)gridDim.x * 512) {
+    const uint64_t s = i / words_per_seg, w = i - s * words_per_seg;
+    const uint64_t a = splitmix64(seed ^ ((seg0 + s) << 32) ^ w);
+    uint64_t b;
+    if (w + 1 < words_per_seg) b = splitmix64(seed ^ ((seg0 + s) << 32) ^ (w + 1));
+    else b = splitmix64(seed ^ ((seg0 + s + 1) << 32) ^ 0);
+    if (i + 1 < total) {
+      u32x4 v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+      *reinterpret_cast<u32x4*>(o + i) = v;
+    } else {
+      o[i] = a;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------------------------
+bool layout_vec16_ok(const Layout& L) {
+  const uintptr_t bits = (uintptr_t)L.data | (uintptr_t)L.parity | L.shard_stride |
+                         L.data_seg_stride | L.par_seg_stride;
+  return (bits & 15) == 0;
+}
+
+namespace {
+
+constexpr uint32_t kMaxGridY = 65535;
+
+template <class F>
+void for_seg_chunks(uint32_t nseg, F f) {
+  for (uint32_t s0 = 0; s0 < nseg; s0 += kMaxGridY) f(s0, nseg - s0 < kMaxGridY ? nseg - s0 : kMaxGridY);
+}
+
+template <class P, int U, bool NT>
+void run_ct(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  if (layout_vec16_ok(L)) {
+    const uint64_t nvec = L.len >> 4;
+    uint64_t gx = (nvec + 256 * U - 1) / (256 * U);
+    if (gx == 0) gx = 1;  // tail-only shard
+    for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {
+      hipLaunchKernelGGL((k_ct<P, U, NT>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, seg_list,
+                         s0);
+    });
+  } else {
+    const uint64_t gx = (L.len + 255) / 256;
+    for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {
+      hipLaunchKernelGGL((k_ct_bytes<P>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, seg_list,
+                         s0);
+    });
+  }
+}
+
+int g_ct_variant = -1;  // -1: default; set by cec_set_option(CEC_OPT_CT_VARIANT)
+
+template <class P>
+void run_ct_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  switch (g_ct_variant) {
+    case 0: run_ct<P, 1, false>(L, seg_list, nseg, st); break;
+    case 1: run_ct<P, 2, false>(L, seg_list, nseg, st); break;
+    case 2: run_ct<P, 4, false>(L, seg_list, nseg, st); break;
+    case 3: run_ct<P, 1, true>(L, seg_list, nseg, st); break;
+    case 4: run_ct<P, 2, true>(L, seg_list, nseg, st); break;
+    case 5: run_ct<P, 4, true>(L, seg_list, nseg, st); break;
+    default: run_ct<P, 2, true>(L, seg_list, nseg, st); break;
+  }
+}
+
+}  // namespace
+
+void set_ct_variant(int v) { g_ct_variant = v; }
+
+bool launch_encode_ct(int k, int m, const Layout& L, const uint32_t* seg_list, uint32_t nseg,
+                      hipStream_t st) {
+  if (k == 2 && m == 1) { run_ct_variant<EncCT<2, 1>>(L, seg_list, nseg, st); return true; }
+  if (k == 32 && m == 32) { run_ct<EncCT<32, 32>, 1, false>(L, seg_list, nseg, st); return true; }
+  return false;
+}
+
+bool launch_decode_ct(int k, int m, int missing, const Layout& L, const uint32_t* seg_list,
+                      uint32_t nseg, hipStream_t st) {
+  if (k == 2 && m == 1) {
+    switch (missing) {
+      case 0: run_ct_variant<Dec1CT<2, 1, 0>>(L, seg_list, nseg, st); return true;
+      case 1: run_ct_variant<Dec1CT<2, 1, 1>>(L, seg_list, nseg, st); return true;
+      case 2: run_ct_variant<EncCT<2, 1>>(L, seg_list, nseg, st); return true;
+    }
+  }
+  return false;
+}
+
+int rt_bucket(int nout) {
+  static const int b[] = {1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 24, 32};
+  for (int x : b)
+    if (x >= nout) return x;
+  return kRtMaxOut;
+}
+
+namespace {
+template <int NOB, int U>
+void run_rt(const Layout& L, const RtSel& sel, int nin, int nout, const uint32_t* dcoef,
+            const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  const int vec_ok = layout_vec16_ok(L) ? 1 : 0;
+  uint64_t gx = vec_ok ? (L.len / 16 + 256 * U - 1) / (256 * U) : (L.len + 255) / 256;
+  if (gx == 0) gx = 1;
+  for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {
+    hipLaunchKernelGGL((k_rt<NOB, U>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, sel, nin,
+                       nout, dcoef, seg_list, s0, vec_ok);
+  });
+}
+}  // namespace
+
+void launch_matvec_rt(const Layout& L, const RtSel& sel, int nin, int nout, const uint32_t* dcoef,
+                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  switch (rt_bucket(nout)) {
+    case 1: run_rt<1, 2>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+    case 2: run_rt<2, 2>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+    case 3: run_rt<3, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+    case 4: run_rt<4, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+    case 5: run_rt<5, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+    case 6: run_rt<6, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+    case 7: run_rt<7, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+    case 8: run_rt<8, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+    case 12: run_rt<12, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+    case 16: run_rt<16, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+    case 24: run_rt<24, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+    default: run_rt<32, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+  }
+}
+
+void launch_sha256_hex(const uint8_t* const* ptrs, const Layout* L, int nshards, uint64_t n,
+                       uint64_t len, uint8_t* hex_out, hipStream_t st) {
+  if (n == 0) return;
+  Layout dummy{};
+  const unsigned g = (unsigned)((n + 63) / 64);
+  hipLaunchKernelGGL(k_sha256, dim3(g), dim3(64), 0, st, ptrs, L ? *L : dummy, nshards, n, len,
+                     hex_out);
+}
+
+void launch_fill_splitmix(uint8_t* out, uint64_t seg_bytes, uint64_t nseg, uint64_t seg0,
+                          uint64_t seed, hipStream_t st) {
+  const uint64_t words = (seg_bytes >> 3) * nseg;
+  uint64_t blocks = (words / 2 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(256), 0, st, out, seg_bytes, nseg, seg0,
+                     seed);
+}
+
+}  // namespace cec

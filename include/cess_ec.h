@@ -1,0 +1,115 @@
+/*
+ * cess_ec.h — C ABI of libcessec, the MI355X (gfx950) Reed-Solomon codec for CESS's
+ * segment -> fragment path.
+ *
+ * Reference interfaces replaced (see SURVEY.md §8b and INTEGRATION.md):
+ *   The reference chain (/root/reference) holds no codec: it fixes the geometry and records the
+ *   codec's outputs. Its interface for this path is the on-chain record
+ *     FileBank::upload_declaration(file_hash, deal_info: BoundedVec<SegmentList>, user_brief)
+ *       c-pallets/file-bank/src/lib.rs:423-428
+ *     SegmentList { hash: Hash, fragment_list: BoundedVec<Hash, FragmentCount> }
+ *       c-pallets/file-bank/src/types.rs:13-16
+ *     Hash([u8; 64])                          primitives/common/src/lib.rs:16
+ *     SEGMENT_SIZE = 16 MiB, FRAGMENT_SIZE = 8 MiB   primitives/common/src/lib.rs:60-61
+ *     FRAGMENT_COUNT = 3                      runtime/src/lib.rs:1027
+ *   and the restoral (repair) flow whose off-chain step is a single-fragment reconstruct
+ *     generate_restoral_order / restoral_order_complete   c-pallets/file-bank/src/lib.rs:943-1122
+ *   The entry points below mirror the off-chain codec API those records come from
+ *   (klauspost/reedsolomon Encoder: New / Encode / Reconstruct / ReconstructData / Verify /
+ *   Split — not vendored in the reference), one function per operation,
+ *   plus batched device-resident forms for HBM-resident segment batches.
+ *
+ * Conventions: GF(2^8), polynomial 0x11D, systematic Vandermonde matrix.
+ * Shard i < k is data, i >= k parity. All functions return 0 or a negative CEC_E* code; no
+ * exceptions cross the ABI. A codec is bound to one device and is not re-entrant; distinct
+ * codecs are independent. Caller owns every shard / segment / hash buffer.
+ */
+#ifndef CESS_EC_H
+#define CESS_EC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CEC_OK 0
+#define CEC_EINVAL (-1)     /* bad k/m (k<1, m<1, k+m>256), null pointer, bad option */
+#define CEC_ETOOFEW (-2)    /* fewer than k shards present (klauspost ErrTooFewShards) */
+#define CEC_ESHARDLEN (-3)  /* zero or mismatched shard length (ErrShardSize / ErrShardNoData) */
+#define CEC_EHIP (-4)       /* HIP runtime error (see cec_last_error) */
+#define CEC_ENOMEM (-5)     /* device or host allocation failed */
+#define CEC_ENCCL (-6)      /* RCCL error (multi-GPU paths) */
+#define CEC_ESHORTDATA (-7) /* split of an empty segment (klauspost ErrShortData) */
+#define CEC_ENODEV (-8)     /* no usable GPU */
+
+typedef struct cec_codec cec_codec;
+
+/* Library identity: "cessec <version> gfx950". */
+const char* cec_version(void);
+const char* cec_strerror(int code);
+/* Detail text of the last error on this thread (HIP error string etc.). */
+const char* cec_last_error(void);
+/* Number of visible HIP devices (0 when none). */
+int cec_device_count(void);
+
+/* New(k, m): codec bound to `device`. Builds the (k+m) x k matrix; k >= 1, m >= 1, k+m <= 256. */
+int cec_create(int k, int m, int device, cec_codec** out);
+void cec_destroy(cec_codec* codec);
+/* Copy the (k+m) x k encode matrix, row-major, into `out`. Host only, no GPU work. */
+int cec_matrix(const cec_codec* codec, uint8_t* out);
+
+/* Host-buffer API (klauspost-shaped). `shards` holds k+m host pointers of shard_len bytes each.
+ * The data is staged through HBM; calls are synchronous. */
+int cec_encode(cec_codec* codec, uint8_t* const* shards, size_t shard_len);
+/* present[i] != 0: shard i is valid. Missing shards are written in place; with data_only only
+ * missing data shards are produced (ReconstructData). All present: no-op. */
+int cec_reconstruct(cec_codec* codec, uint8_t* const* shards, const uint8_t* present,
+                    size_t shard_len, int data_only);
+/* *ok = 1 when every parity shard equals the encode of the data shards. */
+int cec_verify(cec_codec* codec, uint8_t* const* shards, size_t shard_len, int* ok);
+
+/* Batched device-resident API. d_data: [nseg][k][shard_len], d_parity: [nseg][m][shard_len],
+ * both in HBM. Work is enqueued on `hip_stream` (NULL = the codec's own stream) and the call
+ * returns without waiting. */
+int cec_encode_batch(cec_codec* codec, const uint8_t* d_data, uint8_t* d_parity, size_t nseg,
+                     size_t shard_len, void* hip_stream);
+/* Rebuild missing shards in place in the same layout. `present` is a host array of k+m flags
+ * (per_segment = 0: one pattern for every segment) or nseg*(k+m) flags (per_segment = 1).
+ * Segments are grouped by erasure pattern; decode matrices are inverted on the host once per
+ * pattern and cached. */
+int cec_reconstruct_batch(cec_codec* codec, uint8_t* d_data, uint8_t* d_parity, size_t nseg,
+                          size_t shard_len, const uint8_t* present, int per_segment,
+                          int data_only, void* hip_stream);
+/* SHA-256 of every shard of every segment in the batch layout, as 64 lowercase hex chars:
+ * d_hex[(seg*(k+m) + shard)*64 ...]. d_parity may be NULL to hash the k data shards only, in
+ * which case the index is seg*k + shard. */
+int cec_sha256_batch(cec_codec* codec, const uint8_t* d_data, const uint8_t* d_parity,
+                     size_t nseg, size_t shard_len, uint8_t* d_hex, void* hip_stream);
+
+/* SHA-256 hex of n device buffers of `len` bytes: `d_bufs` is a host array of device pointers;
+ * `hex` is host memory of n*64 bytes. Synchronous. */
+int cec_sha256_hex(const uint8_t* const* d_bufs, size_t n, size_t len, uint8_t* hex,
+                   void* hip_stream);
+
+/* klauspost Split for one segment (host memory): shard i = seg[i*shard_len, (i+1)*shard_len),
+ * zero-padded past seg_len. Requires k*shard_len >= seg_len > 0. */
+int cec_split_segment(const uint8_t* seg, size_t seg_len, int k, uint8_t* const* shards,
+                      size_t shard_len);
+
+/* Synthetic segments in HBM: little-endian 64-bit word w of segment s is
+ * splitmix64(seed ^ ((seg0 + s) << 32) ^ w). seg_bytes must be a multiple of 8. */
+int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t seg0,
+                       uint64_t seed, void* hip_stream);
+
+/* Options (tuning / testing). */
+#define CEC_OPT_FORCE_GENERIC 1 /* 1: always use the run-time-coefficient kernel */
+#define CEC_OPT_CT_VARIANT 2    /* compile-time kernel unroll/cache variant, -1 = default */
+int cec_set_option(cec_codec* codec, int option, int value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CESS_EC_H */

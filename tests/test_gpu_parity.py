@@ -1,0 +1,270 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle, bit-exact.
+
+Small sizes compare with the golden fixtures and the C oracle; the full BASELINE geometries
+(64 x 16 MiB RS(2,1) segments, 64 x RS(32,32) segments of 512 KiB fragments) compare with the
+multi-threaded C oracle and with size-independent properties (encode -> erase -> reconstruct
+round trips).
+"""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+from tests.conftest import case_data, parse_shavs
+from tests.oracle_c import c_encode, ptrs
+
+pytestmark = pytest.mark.gpu
+
+MiB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need a GPU"
+    t.cuda.init()
+    return t
+
+
+@pytest.fixture(scope="module")
+def cess(torch):
+    import cess_amd
+    return cess_amd
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def to_dev(torch, arr):
+    return torch.from_numpy(np.ascontiguousarray(arr)).cuda()
+
+
+@pytest.mark.parametrize("generic", [0, 1])
+def test_golden_encode_host_api(cess, golden, generic):
+    encs = {}
+    for case in golden["cases"]:
+        k, m = case["k"], case["m"]
+        enc = encs.get((k, m))
+        if enc is None:
+            enc = encs[(k, m)] = cess.New(k, m)
+            enc.set_option(1, generic)
+        data = case_data(case)
+        shards = data + [np.zeros(case["len"], np.uint8) for _ in range(m)]
+        enc.Encode(shards)
+        assert [sha(p) for p in shards[k:]] == case["parity_sha256"], (k, m, case["len"])
+        if "parity_hex" in case:
+            assert [p.tobytes().hex() for p in shards[k:]] == case["parity_hex"]
+        assert enc.Verify(shards)
+        shards[-1][0] ^= 1
+        assert not enc.Verify(shards)
+
+
+@pytest.mark.parametrize("generic", [0, 1])
+def test_golden_encode_batch(torch, cess, golden, corc, generic):
+    """Batch layout [nseg][k][len]: 3 segments per case (seg s = case data XOR s)."""
+    encs = {}
+    for case in golden["cases"]:
+        k, m, ln = case["k"], case["m"], case["len"]
+        enc = encs.get((k, m))
+        if enc is None:
+            enc = encs[(k, m)] = cess.New(k, m)
+            enc.set_option(1, generic)
+        base = case_data(case)
+        segs = [[(d ^ np.uint8(s)) for d in base] for s in range(3)]
+        host = np.stack([np.stack(sg) for sg in segs])  # [3][k][len]
+        d_data = to_dev(torch, host)
+        d_par = torch.zeros((3, m, ln), dtype=torch.uint8, device="cuda")
+        enc.EncodeBatch(d_data, d_par, 3, ln)
+        torch.cuda.synchronize()
+        got = d_par.cpu().numpy()
+        assert [sha(p) for p in got[0]] == case["parity_sha256"]
+        for s in range(3):
+            want = c_encode(corc, k, m, segs[s])
+            for o in range(m):
+                assert np.array_equal(got[s, o], want[o]), (k, m, ln, s, o)
+
+
+@pytest.mark.parametrize("generic", [0, 1])
+def test_golden_reconstruct_host_api(cess, golden, corc, generic):
+    encs = {}
+    for case in golden["cases"]:
+        if case["len"] > 1000:
+            continue
+        k, m = case["k"], case["m"]
+        enc = encs.get((k, m))
+        if enc is None:
+            enc = encs[(k, m)] = cess.New(k, m)
+            enc.set_option(1, generic)
+        data = case_data(case)
+        full = data + c_encode(corc, k, m, data)
+        for rec in case["reconstruct"]:
+            shards = [None if i in rec["erased"] else full[i].copy() for i in range(k + m)]
+            if rec["data_only"]:
+                enc.ReconstructData(shards)
+            else:
+                enc.Reconstruct(shards)
+            for i in range(k + m):
+                if rec["data_only"] and i >= k and i in rec["erased"]:
+                    assert shards[i] is None
+                else:
+                    assert np.array_equal(shards[i], full[i]), (k, m, rec, i)
+
+
+def test_reconstruct_too_few(cess):
+    enc = cess.New(4, 2)
+    sh = [np.ones(8, np.uint8)] * 6
+    with pytest.raises(cess.ErrTooFewShards):
+        enc.Reconstruct([None, None, None] + sh[3:])
+
+
+@pytest.mark.parametrize("k,m,ln,nseg", [(2, 1, 4096, 9), (4, 2, 1000, 7), (32, 32, 4096, 5),
+                                         (10, 4, 4099, 6), (2, 1, 1, 3)])
+@pytest.mark.parametrize("generic", [0, 1])
+def test_reconstruct_batch_per_segment(torch, cess, corc, k, m, ln, nseg, generic):
+    rng = np.random.default_rng(k * 1000 + ln)
+    n = k + m
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    par = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = np.ones((nseg, n), np.uint8)
+    for s in range(nseg):
+        if (k, m) == (2, 1):
+            present[s, s % 3] = 0  # BASELINE config 3: erased index = seg mod 3
+        else:
+            e = int(rng.integers(1, m + 1))
+            present[s, rng.choice(n, size=e, replace=False)] = 0
+    d_data = to_dev(torch, data * present[:, :k, None])
+    d_par = to_dev(torch, par * present[:, k:, None])
+    enc = cess.New(k, m)
+    enc.set_option(1, generic)
+    enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_data.cpu().numpy(), data)
+    assert np.array_equal(d_par.cpu().numpy(), par)
+    # data_only leaves erased parity untouched (still zero)
+    d_data = to_dev(torch, data * present[:, :k, None])
+    d_par = to_dev(torch, par * present[:, k:, None])
+    enc.ReconstructBatch(d_data, d_par, nseg, ln, present, data_only=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_data.cpu().numpy(), data)
+    assert np.array_equal(d_par.cpu().numpy(), par * present[:, k:, None])
+
+
+def test_ct_variants_identical(torch, cess, corc):
+    k, m, ln, nseg = 2, 1, (1 << 16) + 48, 4
+    rng = np.random.default_rng(7)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    d_data = to_dev(torch, data)
+    enc = cess.New(k, m)
+    for v in range(-1, 6):
+        enc.set_option(2, v)
+        d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
+        enc.EncodeBatch(d_data, d_par, nseg, ln)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_par.cpu().numpy(), want), v
+    enc.set_option(2, -1)
+
+
+def test_misaligned_layout_byte_path(torch, cess, corc):
+    """shard_len % 16 != 0 with nseg > 1 makes shard starts unaligned -> byte kernels."""
+    for (k, m) in [(2, 1), (32, 32), (5, 3)]:
+        ln, nseg = 1003, 3
+        rng = np.random.default_rng(ln + k)
+        data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+        want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+        enc = cess.New(k, m)
+        d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
+        enc.EncodeBatch(to_dev(torch, data), d_par, nseg, ln)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_par.cpu().numpy(), want)
+
+
+def test_fill_synthetic_matches_oracle(torch, cess, orc):
+    seg_bytes, nseg, seed = 1 << 16, 5, 0xCE550002
+    d = torch.empty(nseg * seg_bytes, dtype=torch.uint8, device="cuda")
+    cess.fill_synthetic(d, seg_bytes, nseg, 11, seed)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy().reshape(nseg, seg_bytes)
+    for s in range(nseg):
+        assert np.array_equal(got[s], orc.synthetic_segment(seed, 11 + s, seg_bytes))
+
+
+def _full_geometry(torch, cess, corc, k, m, F, nseg, seed):
+    seg = k * F
+    d_data = torch.empty((nseg, k, F), dtype=torch.uint8, device="cuda")
+    d_par = torch.empty((nseg, m, F), dtype=torch.uint8, device="cuda")
+    cess.fill_synthetic(d_data, seg, nseg, 0, seed)
+    enc = cess.New(k, m)
+    enc.EncodeBatch(d_data, d_par, nseg, F)
+    torch.cuda.synchronize()
+    host = d_data.cpu().numpy()
+    gpu_par = d_par.cpu().numpy()
+    # CPU oracle on the same bytes (all host threads, bounded by 16)
+    want = np.zeros_like(gpu_par)
+    import os
+    corc.orc_encode_batch(k, m, host.ctypes.data, want.ctypes.data, nseg, F,
+                          min(16, os.cpu_count() or 1), 1)
+    assert np.array_equal(gpu_par, want)
+    return enc, d_data, d_par, host, gpu_par
+
+
+def test_full_geometry_rs21_1gib(torch, cess, corc):
+    """BASELINE config 2 + 3 at full size: 64 x 16 MiB segments, then every single erasure."""
+    k, m, F, nseg = 2, 1, 8 * MiB, 64
+    enc, d_data, d_par, host, par = _full_geometry(torch, cess, corc, k, m, F, nseg, 0xCE550002)
+    ref_d, ref_p = d_data.clone(), d_par.clone()
+    present = np.ones((nseg, 3), np.uint8)
+    present[np.arange(nseg), np.arange(nseg) % 3] = 0
+    for s in range(nseg):
+        e = s % 3
+        if e < k:
+            d_data[s, e].zero_()
+        else:
+            d_par[s, e - k].zero_()
+    enc.ReconstructBatch(d_data, d_par, nseg, F, present)
+    torch.cuda.synchronize()
+    assert torch.equal(d_data, ref_d) and torch.equal(d_par, ref_p)
+
+
+def test_full_geometry_rs3232(torch, cess, corc):
+    """BASELINE config 5 geometry: 64 segments x 32 fragments of 512 KiB, 32 parity each."""
+    k, m, F, nseg = 32, 32, 512 * 1024, 64
+    enc, d_data, d_par, host, par = _full_geometry(torch, cess, corc, k, m, F, nseg, 0xCE550005)
+    ref_d, ref_p = d_data.clone(), d_par.clone()
+    rng = np.random.default_rng(3)
+    present = np.ones((nseg, k + m), np.uint8)
+    for s in range(nseg):
+        present[s, rng.choice(k + m, size=m, replace=False)] = 0
+    pres_t = torch.from_numpy(present).cuda().bool()
+    d_data.mul_(pres_t[:, :k, None])
+    d_par.mul_(pres_t[:, k:, None])
+    enc.ReconstructBatch(d_data, d_par, nseg, F, present)
+    torch.cuda.synchronize()
+    assert torch.equal(d_data, ref_d) and torch.equal(d_par, ref_p)
+
+
+def test_sha256_shavs_on_gpu(torch, cess):
+    vecs = parse_shavs("SHA256ShortMsg.rsp") + parse_shavs("SHA256LongMsg.rsp")
+    bufs = [torch.from_numpy(np.frombuffer(msg, np.uint8).copy() if msg else
+                             np.zeros(1, np.uint8)).cuda() for msg, _ in vecs]
+    for (msg, md), b in zip(vecs, bufs):
+        got = cess.sha256_hex_device([b.data_ptr()], len(msg))[0]
+        assert got.decode() == md, len(msg)
+
+
+def test_sha256_batch_matches_hashlib(torch, cess):
+    for (k, m, F, nseg) in [(2, 1, 4096 + 7, 3), (32, 32, 65536, 2), (2, 1, 1 << 20, 4)]:
+        rng = np.random.default_rng(F)
+        data = rng.integers(0, 256, (nseg, k, F), dtype=np.uint8)
+        par = rng.integers(0, 256, (nseg, m, F), dtype=np.uint8)
+        enc = cess.New(k, m)
+        d_hex = torch.zeros((nseg, k + m, 64), dtype=torch.uint8, device="cuda")
+        enc.Sha256Batch(to_dev(torch, data), to_dev(torch, par), nseg, F, d_hex)
+        torch.cuda.synchronize()
+        hx = d_hex.cpu().numpy()
+        for s in range(nseg):
+            for i in range(k + m):
+                buf = data[s, i] if i < k else par[s, i - k]
+                assert hx[s, i].tobytes().decode() == sha(buf)

@@ -1,0 +1,151 @@
+"""CPU-side checks of the product: the C ABI library loads and exports what include/cess_ec.h
+declares, host-only entry points behave, the Python mirror raises klauspost's errors, and the
+product's host matrix / decode-plan builder (gf256.h) agrees with the oracle."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "cess_ec.h")
+
+
+def header_symbols():
+    with open(HEADER) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"\b(cec_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from cess_amd import _lib
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 17
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_lib.SIGNATURES), "ctypes table and header disagree"
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                        text=True, check=True).stdout
+    for s in syms:
+        assert re.search(rf"\bT {s}$", nm, re.M), s
+
+
+def test_library_is_gfx950_code_object():
+    """The embedded offload bundle targets gfx950 only (no other GPU arch, no CUDA)."""
+    from cess_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100", b"sm_"):
+        assert other not in blob
+
+
+def test_host_only_entry_points():
+    from cess_amd import _lib
+    lib = _lib.load()
+    assert lib.cec_version().startswith(b"cessec")
+    assert lib.cec_strerror(_lib.CEC_ETOOFEW) == b"too few shards given"
+    assert lib.cec_strerror(_lib.CEC_ESHARDLEN) == b"shard sizes do not match"
+
+
+def test_split_segment_matches_oracle(orc):
+    import cess_amd
+    from cess_amd import reedsolomon as rs
+    enc = object.__new__(rs.Encoder)  # Split is host-only; skip device codec creation
+    enc.DataShards, enc.ParityShards, enc.Shards = 2, 1, 3
+    for data in (b"a", b"abcde", bytes(range(256)) * 3):
+        got = rs.Encoder.Split(enc, data)
+        want = orc.ReedSolomon(2, 1).split(data)
+        assert [g.tobytes() for g in got] == [w.tobytes() for w in want]
+    with pytest.raises(cess_amd.ErrShortData):
+        rs.Encoder.Split(enc, b"")
+
+
+def test_python_api_errors_without_gpu():
+    import cess_amd
+    with pytest.raises(cess_amd.ErrInvShardNum):
+        cess_amd.New(0, 1)
+    with pytest.raises(cess_amd.ErrInvShardNum):
+        cess_amd.New(2, -1)
+    with pytest.raises(cess_amd.ErrMaxShardNum):
+        cess_amd.New(200, 57)
+    enc = cess_amd.New(3, 0)  # no parity: no device codec needed
+    sh = [np.ones(4, np.uint8)] * 3
+    enc.Encode(sh)
+    assert enc.Verify(sh)
+    with pytest.raises(cess_amd.ErrTooFewShards):
+        enc.Encode(sh[:2])
+    with pytest.raises(cess_amd.ErrShardNoData):
+        enc.Encode([np.zeros(0, np.uint8)] * 3)
+    with pytest.raises(cess_amd.ErrShardSize):
+        enc.Encode([np.ones(4, np.uint8), np.ones(5, np.uint8), np.ones(4, np.uint8)])
+
+
+def test_join(tmp_path):
+    import io
+    import cess_amd
+    from cess_amd import reedsolomon as rs
+    enc = object.__new__(rs.Encoder)
+    enc.DataShards, enc.ParityShards, enc.Shards = 2, 1, 3
+    shards = rs.Encoder.Split(enc, b"hello world")
+    buf = io.BytesIO()
+    rs.Encoder.Join(enc, buf, shards, 11)
+    assert buf.getvalue() == b"hello world"
+    with pytest.raises(cess_amd.ErrReconstructRequired):
+        rs.Encoder.Join(enc, io.BytesIO(), [None, shards[1]], 11)
+    with pytest.raises(cess_amd.ErrShortData):
+        rs.Encoder.Join(enc, io.BytesIO(), shards, 100)
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+    import cess_amd
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(cess_amd.HipError):
+        cess_amd.New(2, 1)
+
+
+@pytest.fixture(scope="module")
+def plan_dump(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("native") / "gf_plan_dump")
+    subprocess.run(["g++", "-std=c++20", "-O1", "-fconstexpr-ops-limit=2000000000",
+                    os.path.join(ROOT, "tests", "native", "gf_plan_dump.cpp"), "-o", exe],
+                   check=True)
+    return exe
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (4, 2), (10, 4), (32, 32), (100, 30)])
+def test_product_matrix_and_plans_match_oracle(plan_dump, orc, k, m):
+    n = k + m
+    rng = np.random.default_rng(n)
+    pats = []
+    for _ in range(4):
+        e = int(rng.integers(1, m + 1))
+        erased = set(rng.choice(n, size=e, replace=False).tolist())
+        pats.append(("".join("0" if i in erased else "1" for i in range(n)),
+                     int(rng.integers(0, 2))))
+    pats.append(("0" * (m + 1) + "1" * (k - 1), 0))  # too few -> error
+    args = [plan_dump, str(k), str(m)]
+    for p, d in pats:
+        args += [p, str(d)]
+    lines = subprocess.run(args, capture_output=True, text=True, check=True).stdout.splitlines()
+    e = list(map(int, lines[0].split()[1:]))
+    assert e == sum(orc.build_matrix(k, n), [])
+    rs = orc.ReedSolomon(k, m)
+    for (p, d), line in zip(pats, lines[1:]):
+        tok = line.split()
+        rc = int(tok[1])
+        present = [c == "1" for c in p]
+        if sum(present) < k:
+            assert rc == -1
+            continue
+        assert rc == 0
+        i_in, i_out, i_coef = tok.index("in"), tok.index("out"), tok.index("coef")
+        surv, outs, rows = rs.decode_plan(present, data_only=bool(d))
+        assert list(map(int, tok[i_in + 1:i_out])) == surv
+        assert list(map(int, tok[i_out + 1:i_coef])) == outs
+        assert list(map(int, tok[i_coef + 1:])) == sum(rows, [])
