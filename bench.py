@@ -66,7 +66,8 @@ def cpu_baseline(k: int, m: int, F: int, target_s: float) -> dict:
     from oracle.c_oracle import load_c_oracle
     orc = load_c_oracle()
     simd = orc.orc_set_simd(-1)
-    nseg = 8 if k * F >= 8 * MiB else 64
+    # same workload shape as the GPU step (1 GiB of segments), larger than the host's LLC
+    nseg = max(1, (1 << 30) // (k * F))
     data = np.empty(nseg * k * F, np.uint8)
     par = np.empty(nseg * m * F, np.uint8)
     orc.orc_fill_synthetic(data.ctypes.data, k * F, nseg, 0, SEED0 + 2)
@@ -75,7 +76,8 @@ def cpu_baseline(k: int, m: int, F: int, target_s: float) -> dict:
     t1 = orc.orc_encode_batch(k, m, data.ctypes.data, par.ctypes.data, nseg, F, threads, 1)
     reps = max(1, int(target_s / max(t1, 1e-6)))
     t = orc.orc_encode_batch(k, m, data.ctypes.data, par.ctypes.data, nseg, F, threads, reps)
-    st = orc.orc_encode_batch(k, m, data.ctypes.data, par.ctypes.data, 1, F, 1, 1)
+    n1 = min(nseg, 8)
+    st = orc.orc_encode_batch(k, m, data.ctypes.data, par.ctypes.data, n1, F, 1, 1)
     per_seg = (k + m) * F
     return {
         "value": round(reps * nseg * per_seg / t / GB, 3),
@@ -85,7 +87,7 @@ def cpu_baseline(k: int, m: int, F: int, target_s: float) -> dict:
         "sample": f"{reps} x {nseg} segments of {k * F // MiB} MiB, RS({k},{m}), "
                   f"{'AVX2 split-nibble' if simd == 1 else 'scalar table'} C oracle, "
                   f"{threads} threads, {t:.1f} s",
-        "value_1thread": round(per_seg / st / GB, 3),
+        "value_1thread": round(n1 * per_seg / st / GB, 3),
         "cpu_model": cpu_model(),
     }
 
@@ -111,6 +113,9 @@ def main() -> None:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
+    ap.add_argument("--sweep", type=str, default="",
+                    help="comma list of CT variants: interleaved A/B in one process, prints "
+                         "median launch ms per variant and exits")
     args = ap.parse_args()
 
     import torch
@@ -155,6 +160,37 @@ def main() -> None:
             enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
             if d_hex is not None:
                 enc.Sha256Batch(d_data, d_par, nseg, F, d_hex, stream=stream)
+
+    def step_codec():  # the codec kernel alone (config 5's step also hashes)
+        if args.config == 3:
+            enc.ReconstructBatch(d_data, d_par, nseg, F, present, stream=stream)
+        else:
+            enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
+
+    if args.sweep:
+        step = step_codec  # noqa: F811
+        variants = [int(v) for v in args.sweep.split(",")]
+        times = {v: [] for v in variants}
+        for _ in range(args.warmup):
+            step()
+        for rnd in range(args.steps):
+            for v in variants:
+                enc.set_option(2, v)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                step()
+                a.record(stream)
+                step()
+                step()
+                b.record(stream)
+                torch.cuda.synchronize(dev)
+                times[v].append(a.elapsed_time(b) / 2)
+        per_seg = (k + m) * F
+        for v in variants:
+            med = float(np.median(times[v]))
+            print(json.dumps({"config": args.config, "variant": v, "median_ms": round(med, 4),
+                              "min_ms": round(float(np.min(times[v])), 4),
+                              "GBps": round(nseg * per_seg / med / 1e6, 1)}), flush=True)
+        return
 
     for _ in range(args.warmup):
         step()

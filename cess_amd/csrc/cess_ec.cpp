@@ -116,9 +116,9 @@ struct cec_codec {
 
 namespace {
 
-hipStream_t pick_stream(cec_codec* c, void* s) {
-  return s ? reinterpret_cast<hipStream_t>(s) : c->stream;
-}
+// Batched calls run on the caller's stream; NULL is the HIP null (legacy default) stream, as
+// in the HIP API itself (torch's default stream has handle 0).
+hipStream_t pick_stream(cec_codec*, void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 Layout batch_layout(const cec_codec* c, const uint8_t* d_data, const uint8_t* d_parity,
                     size_t shard_len) {

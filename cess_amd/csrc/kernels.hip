@@ -26,6 +26,7 @@
 namespace cec {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // Every lambda on the compile-time path is force-inlined: an outlined body turns into a call
 // with the Layout spilled to scratch.
@@ -49,15 +50,15 @@ __device__ __forceinline__ uint8_t* shard_ptr_ct(const Layout& L, uint32_t seg) 
   else return L.parity + seg * L.par_seg_stride + (uint64_t)(IDX - K) * L.shard_stride;
 }
 
-template <bool NT>
-__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-  else return *reinterpret_cast<const u32x4*>(p);
+template <bool NT, class TV = u32x4>
+__device__ __forceinline__ TV ld16(const uint8_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const TV*>(p));
+  else return *reinterpret_cast<const TV*>(p);
 }
-template <bool NT>
-__device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-  else *reinterpret_cast<u32x4*>(p) = v;
+template <bool NT, class TV = u32x4>
+__device__ __forceinline__ void st16(uint8_t* p, TV v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<TV*>(p));
+  else *reinterpret_cast<TV*>(p) = v;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -167,6 +168,9 @@ __device__ __forceinline__ u32x4 xor3(u32x4 a, u32x4 b, u32x4 c) {
   return u32x4{xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y), xor3(a.z, b.z, c.z),
                xor3(a.w, b.w, c.w)};
 }
+__device__ __forceinline__ u32x2 xor3(u32x2 a, u32x2 b, u32x2 c) {
+  return u32x2{xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y)};
+}
 template <class T>
 __device__ __forceinline__ T xor2(T a, T b) {
   return xor3(a, b, T(0));
@@ -230,14 +234,20 @@ __device__ __forceinline__ void ct_column_horner(LD ld, ST st) {
   });
 }
 
-template <class P, class T, class LD, class ST>
+// Streaming form for wide codes: one accumulator per output, input columns consumed in order.
+// PF input loads are kept in flight (a static register ring): column j+PF is issued before
+// column j is multiplied in, so HBM latency hides behind the XOR work of PF columns.
+template <class P, int PF, class T, class LD, class ST>
 __device__ __forceinline__ void ct_column_stream(LD ld, ST st) {
   T acc[P::NO];
+  T ring[PF];
   static_for<P::NO>([&](auto O) CEC_AI { acc[O] = T(0); });
+  static_for<(PF < P::NI ? PF : P::NI)>([&](auto J) CEC_AI { ring[J] = ld(J); });
   static_for<P::NI>([&](auto J) CEC_AI {
     constexpr int j = J;
     T p[8];
-    p[0] = ld(J);
+    p[0] = ring[j % PF];
+    if constexpr (j + PF < P::NI) ring[j % PF] = ld(std::integral_constant<int, j + PF>{});
     static_for<7>([&](auto B) CEC_AI {
       constexpr int b = B + 1;
       if constexpr (b <= P::v.hb_col[j]) p[b] = xt(p[b - 1]);
@@ -246,16 +256,16 @@ __device__ __forceinline__ void ct_column_stream(LD ld, ST st) {
       constexpr int o = O;
       acc[o] = mul_acc<P::v.c[o][j]>(acc[o], p);
     });
-    // Keep one input column live at a time.
+    // Keep one column's powers live at a time (the loads above are already issued).
     if constexpr (P::NO > 8) __builtin_amdgcn_sched_barrier(0);
   });
   static_for<P::NO>([&](auto O) CEC_AI { st(O, acc[O]); });
 }
 
 // Byte-wise finish of the last (len % 16) bytes, run by the last block of each segment.
-template <class P>
+template <class P, int VB>
 __device__ __forceinline__ void ct_tail(const Layout& L, uint32_t seg) {
-  const uint64_t t0 = L.len & ~uint64_t(15);
+  const uint64_t t0 = L.len - L.len % VB;
   const uint64_t i = t0 + threadIdx.x;
   if (i >= L.len) return;
   auto ld = [&](auto J) CEC_AI -> uint32_t {
@@ -265,27 +275,28 @@ __device__ __forceinline__ void ct_tail(const Layout& L, uint32_t seg) {
     shard_ptr_ct<P::K, P::v.out[O]>(L, seg)[i] = (uint8_t)y;
   };
   if constexpr (use_horner<P>(1)) ct_column_horner<P, uint32_t>(ld, st);
-  else ct_column_stream<P, uint32_t>(ld, st);
+  else ct_column_stream<P, 1, uint32_t>(ld, st);
 }
 
-template <class P, int U, bool NT>
+template <class P, int U, bool NT, class TV = u32x4, int PF = 1>
 __global__ __launch_bounds__(256) void k_ct(Layout L, const uint32_t* __restrict__ seg_list,
                                             uint32_t seg0) {
+  constexpr int VB = sizeof(TV);  // bytes per lane per shard per column
   const uint32_t seg = seg_list ? seg_list[seg0 + blockIdx.y] : seg0 + blockIdx.y;
-  const uint64_t nvec = L.len >> 4;
+  const uint64_t nvec = L.len / VB;
   const uint64_t base = (uint64_t)blockIdx.x * (256 * U) + threadIdx.x;
   // Shard pointers are recomputed per use (scalar base + index * stride): holding 2 * (NI + NO)
   // SGPRs of pointers live across the body overflows the SGPR file for wide codes.
   auto column = [&](uint64_t v) CEC_AI {
-    const uint64_t off = v << 4;
+    const uint64_t off = v * VB;
     auto ld = [&](auto J) CEC_AI {
-      return ld16<NT>(shard_ptr_ct<P::K, P::v.in[J]>(L, seg) + off);
+      return ld16<NT, TV>(shard_ptr_ct<P::K, P::v.in[J]>(L, seg) + off);
     };
-    auto st = [&](auto O, u32x4 y) CEC_AI {
-      st16<NT>(shard_ptr_ct<P::K, P::v.out[O]>(L, seg) + off, y);
+    auto st = [&](auto O, TV y) CEC_AI {
+      st16<NT, TV>(shard_ptr_ct<P::K, P::v.out[O]>(L, seg) + off, y);
     };
-    if constexpr (use_horner<P>(U)) ct_column_horner<P, u32x4>(ld, st);
-    else ct_column_stream<P, u32x4>(ld, st);
+    if constexpr (use_horner<P>(U)) ct_column_horner<P, TV>(ld, st);
+    else ct_column_stream<P, PF, TV>(ld, st);
   };
   if (base + (U - 1) * 256 < nvec) {  // full tile: no per-element predicate
     static_for<U>([&](auto u) CEC_AI { column(base + u * 256); });
@@ -294,7 +305,7 @@ __global__ __launch_bounds__(256) void k_ct(Layout L, const uint32_t* __restrict
       if (base + u * 256 < nvec) column(base + u * 256);
     });
   }
-  if ((L.len & 15) && blockIdx.x == gridDim.x - 1) ct_tail<P>(L, seg);
+  if ((L.len % VB) && blockIdx.x == gridDim.x - 1) ct_tail<P, VB>(L, seg);
 }
 
 // Byte-granular variant for layouts whose shard starts are not 16-byte aligned.
@@ -311,7 +322,7 @@ __global__ __launch_bounds__(256) void k_ct_bytes(Layout L, const uint32_t* __re
     shard_ptr_ct<P::K, P::v.out[O]>(L, seg)[i] = (uint8_t)y;
   };
   if constexpr (use_horner<P>(1)) ct_column_horner<P, uint32_t>(ld, st);
-  else ct_column_stream<P, uint32_t>(ld, st);
+  else ct_column_stream<P, 1, uint32_t>(ld, st);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -557,15 +568,15 @@ void for_seg_chunks(uint32_t nseg, F f) {
   for (uint32_t s0 = 0; s0 < nseg; s0 += kMaxGridY) f(s0, nseg - s0 < kMaxGridY ? nseg - s0 : kMaxGridY);
 }
 
-template <class P, int U, bool NT>
+template <class P, int U, bool NT, class TV = u32x4, int PF = 1>
 void run_ct(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
   if (layout_vec16_ok(L)) {
-    const uint64_t nvec = L.len >> 4;
+    const uint64_t nvec = L.len / sizeof(TV);
     uint64_t gx = (nvec + 256 * U - 1) / (256 * U);
     if (gx == 0) gx = 1;  // tail-only shard
     for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {
-      hipLaunchKernelGGL((k_ct<P, U, NT>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, seg_list,
-                         s0);
+      hipLaunchKernelGGL((k_ct<P, U, NT, TV, PF>), dim3((unsigned)gx, ny), dim3(256), 0, st, L,
+                         seg_list, s0);
     });
   } else {
     const uint64_t gx = (L.len + 255) / 256;
@@ -587,7 +598,21 @@ void run_ct_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hi
     case 3: run_ct<P, 1, true>(L, seg_list, nseg, st); break;
     case 4: run_ct<P, 2, true>(L, seg_list, nseg, st); break;
     case 5: run_ct<P, 4, true>(L, seg_list, nseg, st); break;
-    default: run_ct<P, 2, true>(L, seg_list, nseg, st); break;
+    default: run_ct<P, 1, true>(L, seg_list, nseg, st); break;  // r01 sweep winner
+  }
+}
+
+// Wide codes (streaming form): per-lane width and prefetch depth.
+template <class P>
+void run_wide_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  switch (g_ct_variant) {
+    case 0: run_ct<P, 1, false, u32x4, 1>(L, seg_list, nseg, st); break;
+    case 1: run_ct<P, 1, false, u32x4, 2>(L, seg_list, nseg, st); break;
+    case 2: run_ct<P, 1, false, u32x2, 2>(L, seg_list, nseg, st); break;
+    case 3: run_ct<P, 1, false, u32x2, 4>(L, seg_list, nseg, st); break;
+    case 4: run_ct<P, 1, true, u32x2, 4>(L, seg_list, nseg, st); break;
+    case 5: run_ct<P, 1, false, u32x2, 8>(L, seg_list, nseg, st); break;
+    default: run_ct<P, 1, false, u32x2, 4>(L, seg_list, nseg, st); break;
   }
 }
 
@@ -598,7 +623,7 @@ void set_ct_variant(int v) { g_ct_variant = v; }
 bool launch_encode_ct(int k, int m, const Layout& L, const uint32_t* seg_list, uint32_t nseg,
                       hipStream_t st) {
   if (k == 2 && m == 1) { run_ct_variant<EncCT<2, 1>>(L, seg_list, nseg, st); return true; }
-  if (k == 32 && m == 32) { run_ct<EncCT<32, 32>, 1, false>(L, seg_list, nseg, st); return true; }
+  if (k == 32 && m == 32) { run_wide_variant<EncCT<32, 32>>(L, seg_list, nseg, st); return true; }
   return false;
 }
 

@@ -71,8 +71,8 @@ int cec_reconstruct(cec_codec* codec, uint8_t* const* shards, const uint8_t* pre
 int cec_verify(cec_codec* codec, uint8_t* const* shards, size_t shard_len, int* ok);
 
 /* Batched device-resident API. d_data: [nseg][k][shard_len], d_parity: [nseg][m][shard_len],
- * both in HBM. Work is enqueued on `hip_stream` (NULL = the codec's own stream) and the call
- * returns without waiting. */
+ * both in HBM. Work is enqueued on `hip_stream` (NULL = the HIP null stream, as in the HIP API)
+ * and the call returns without waiting. */
 int cec_encode_batch(cec_codec* codec, const uint8_t* d_data, uint8_t* d_parity, size_t nseg,
                      size_t shard_len, void* hip_stream);
 /* Rebuild missing shards in place in the same layout. `present` is a host array of k+m flags
