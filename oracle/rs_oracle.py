@@ -28,6 +28,8 @@ no erasure crate). Its published algorithm, restated here:
 Hash convention [ecosystem, unpinned by the reference]: fragment / segment Hash = the 64 ASCII
 characters of lowercase hex SHA-256 (FIPS 180-4) of the bytes.
 
+PARITY STATUS: RS arithmetic is *parity unpinned by the reference* (it holds no codec, no RS
+test and no RS fixture); SHA-256 is pinned by the reference's own NIST SHAVS files.
 Pinning: public known answers (Backblaze / klauspost TestOneEncode RS(5,5), galois and matrix
 unit-test values) and NIST SHAVS vectors from the reference's own tree
 (utils/ring/third_party/NIST/SHAVS/SHA256{Short,Long}Msg.rsp). See tests/test_oracle.py.
