@@ -1,0 +1,143 @@
+"""Multi-GPU placement and the degraded-read gather.
+
+One process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on MI355X, "gloo" on
+CPU for tests). Encode needs no collective: segments are independent, each rank encodes a
+contiguous range (`shard_range`). The one real exchange is a degraded read / repair: the k
+surviving fragments of a segment live on different GPUs and must meet on the GPU that rebuilds
+the lost one. RCCL has no XOR reduction (rccl.h ncclRedOp_t: sum/prod/max/min/avg), so
+survivors are moved with grouped point-to-point send/recv (`batch_isend_irecv`) and decoded
+locally by libcessec.
+
+Placement mirrors the chain's miner assignment, which spreads a segment's fragments over
+distinct miners (c-pallets/file-bank/src/functions.rs:187-283, `random_assign_miner`, and
+`:256-276`): fragment f of segment s is stored on GPU (s + f) mod G.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+
+def shard_range(nseg: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous [start, stop) segment range of `rank` (encode sharding, no collective)."""
+    base, extra = divmod(nseg, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def fragment_owner(seg: int, frag: int, world: int) -> int:
+    return (seg + frag) % world
+
+
+@dataclass
+class FragmentStore:
+    """Fragments a rank holds under the (s + f) mod G placement: `slots[(s, f)]` indexes the
+    rows of `data`, a [nslots, F] uint8 tensor (HBM on GPU ranks)."""
+
+    slots: Dict[Tuple[int, int], int]
+    data: "object"  # torch.Tensor [nslots, F]
+
+
+def local_fragments(nseg: int, n: int, world: int, rank: int) -> List[Tuple[int, int]]:
+    return [(s, f) for s in range(nseg) for f in range(n) if fragment_owner(s, f, world) == rank]
+
+
+@dataclass
+class GatherPlan:
+    """Who sends which survivor to whom for a set of lost fragments."""
+
+    # per decoding rank: ordered list of segments it rebuilds
+    segments: Dict[int, List[int]]
+    # (segment, survivor fragment) -> (source rank, destination rank)
+    moves: Dict[Tuple[int, int], Tuple[int, int]]
+    # segment -> present flags (k+m) as seen by the decoder (survivors used + nothing else)
+    present: Dict[int, np.ndarray]
+    # segment -> erased fragment indices
+    lost: Dict[int, List[int]]
+    bytes_moved: int
+
+
+def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
+                frag_bytes: int) -> GatherPlan:
+    """Plan the survivor gather for `lost` = {segment: erased fragment indices}.
+
+    The decoder of a segment is the home GPU of its first lost fragment (repair restores the
+    fragment where it lives). Survivors = the first k present fragments in index order (the
+    codec's survivor choice), so exactly k fragments per segment are read."""
+    n = k + m
+    segs: Dict[int, List[int]] = {}
+    moves = {}
+    present = {}
+    moved = 0
+    for s in sorted(lost):
+        erased = set(lost[s])
+        if len(erased) > m:
+            raise ValueError(f"segment {s}: {len(erased)} erasures > m = {m}")
+        dec = fragment_owner(s, min(erased), world)
+        segs.setdefault(dec, []).append(s)
+        surv = [f for f in range(n) if f not in erased][:k]
+        flags = np.zeros(n, np.uint8)
+        flags[surv] = 1
+        present[s] = flags
+        for f in surv:
+            src = fragment_owner(s, f, world)
+            moves[(s, f)] = (src, dec)
+            if src != dec:
+                moved += frag_bytes
+    return GatherPlan(segs, moves, present, {s: sorted(set(v)) for s, v in lost.items()}, moved)
+
+
+def gather_survivors(plan: GatherPlan, store: FragmentStore, k: int, m: int, rank: int,
+                     group=None):
+    """Run the gather for this rank. Returns (staging_data [nseg_d][k][F],
+    staging_parity [nseg_d][m][F], present [nseg_d][k+m], segment list) on the decoding rank;
+    the staging tensors hold every used survivor at its shard index (erased slots zero).
+    Non-decoding ranks only send and return None for the staging tensors."""
+    import torch
+    import torch.distributed as dist
+
+    F = store.data.shape[1]
+    dev = store.data.device
+    mysegs = plan.segments.get(rank, [])
+    row = {s: i for i, s in enumerate(mysegs)}
+    sd = torch.zeros((len(mysegs), k, F), dtype=torch.uint8, device=dev)
+    sp = torch.zeros((len(mysegs), m, F), dtype=torch.uint8, device=dev)
+
+    def dst_view(s, f):
+        return sd[row[s], f] if f < k else sp[row[s], f - k]
+
+    ops = []
+    for (s, f), (src, dst) in sorted(plan.moves.items()):
+        if src == dst == rank:
+            dst_view(s, f).copy_(store.data[store.slots[(s, f)]])
+        elif src == rank:
+            ops.append(dist.P2POp(dist.isend, store.data[store.slots[(s, f)]], dst, group))
+        elif dst == rank:
+            ops.append(dist.P2POp(dist.irecv, dst_view(s, f), src, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    if not mysegs:
+        return None, None, None, []
+    present = np.stack([plan.present[s] for s in mysegs])
+    return sd, sp, present, mysegs
+
+
+def degraded_read(plan: GatherPlan, store: FragmentStore, enc, rank: int, group=None):
+    """Gather survivors over RCCL and rebuild the lost fragments on this rank's GPU with
+    libcessec. Returns {(segment, fragment): tensor[F]} of rebuilt fragments for this rank."""
+    k, m = enc.DataShards, enc.ParityShards
+    sd, sp, present, segs = gather_survivors(plan, store, k, m, rank, group)
+    if not segs:
+        return {}
+    import torch
+    enc.ReconstructBatch(sd, sp, len(segs), sd.shape[2], present,
+                         stream=torch.cuda.current_stream(sd.device))
+    # unused survivors are rebuilt too (they are absent from the staging); return the lost ones
+    out = {}
+    for i, s in enumerate(segs):
+        for f in plan.lost[s]:
+            out[(s, f)] = sd[i, f] if f < k else sp[i, f - k]
+    return out

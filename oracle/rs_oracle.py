@@ -243,9 +243,11 @@ FRAGMENT_COUNT = 3                # runtime/src/lib.rs:1027
 def segment_list(file_bytes: bytes, k: int = 2, m: int = 1, segment_size: int = SEGMENT_SIZE):
     """[(segment hash, [fragment hashes])] for a file: 16 MiB segments (last zero padded),
     each split into k fragments + m parity, every piece hashed (types.rs:13-16 record)."""
+    if len(file_bytes) == 0:
+        raise ValueError("short data")
     rs = ReedSolomon(k, m)
     out = []
-    nseg = max(1, (len(file_bytes) + segment_size - 1) // segment_size)
+    nseg = (len(file_bytes) + segment_size - 1) // segment_size
     for s in range(nseg):
         seg = np.zeros(segment_size, dtype=np.uint8)
         chunk = np.frombuffer(file_bytes[s * segment_size:(s + 1) * segment_size], dtype=np.uint8)

@@ -268,3 +268,28 @@ def test_sha256_batch_matches_hashlib(torch, cess):
             for i in range(k + m):
                 buf = data[s, i] if i < k else par[s, i - k]
                 assert hx[s, i].tobytes().decode() == sha(buf)
+
+
+@pytest.mark.parametrize("size,seg,k,m,hash_on", [
+    (3 * (1 << 20) + 12345, 1 << 20, 2, 1, "host"),
+    (5 * (1 << 20) + 7, 1 << 20, 2, 1, "gpu"),
+    (2 * (1 << 20) - 5, 1 << 19, 32, 32, "auto"),
+    (40 * MiB + 3, 16 * MiB, 2, 1, "auto"),
+])
+def test_segment_list_pipeline(torch, cess, orc, size, seg, k, m, hash_on):
+    """§8f rank 1: file -> segments -> fragments -> SegmentList, vs the oracle."""
+    from cess_amd.segments import SegmentEncoder, check_file_spec, needed_space
+    rng = np.random.default_rng(size)
+    blob = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+    se = SegmentEncoder(k, m, seg, batch_segments=2, hash_on=hash_on)
+    frags = {}
+    rec = se.encode_file(blob, on_fragment=lambda s, i, b: frags.__setitem__((s, i), sha(b)))
+    se.close()
+    want = orc.segment_list(blob, k, m, seg)
+    assert [(s.hash, s.fragment_list) for s in rec.segments] == want
+    assert rec.file_hash.decode() == hashlib.sha256(blob).hexdigest()
+    assert rec.size == size
+    assert check_file_spec(rec.segments, k + m)
+    assert needed_space(rec.segments, seg) == len(want) * seg * 15 // 10
+    for (s, i), h in frags.items():
+        assert h.encode() == want[s][1][i]
