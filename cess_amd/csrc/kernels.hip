@@ -429,6 +429,14 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) {
   return __builtin_amdgcn_alignbit(x, x, n);
 }
 
+// v_bitop3 truth tables (index = a<<2 | b<<1 | c): Ch = a ? b : c, Maj = majority.
+__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+  return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+
 __device__ __forceinline__ void sha256_block(uint32_t (&h)[8], uint32_t (&w)[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
 #pragma unroll
@@ -438,17 +446,15 @@ __device__ __forceinline__ void sha256_block(uint32_t (&h)[8], uint32_t (&w)[16]
       wt = w[t];
     } else {
       const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
-      const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+      const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
       wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
       w[t & 15] = wt;
     }
-    const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
-    const uint32_t ch = (e & f) ^ (~e & g);
-    const uint32_t t1 = hh + S1 + ch + kSha256K[t] + wt;
-    const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
-    const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
-    const uint32_t t2 = S0 + maj;
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+    const uint32_t t1 = hh + S1 + ch(e, f, g) + kSha256K[t] + wt;
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+    const uint32_t t2 = S0 + maj(a, b, c);
     hh = g; g = f; f = e; e = d + t1;
     d = c; c = b; b = a; a = t1 + t2;
   }
@@ -467,24 +473,38 @@ __global__ __launch_bounds__(64) void k_sha256(const uint8_t* const* __restrict_
   uint32_t w[16];
   const uint64_t nfull = len >> 6;
   const bool al16 = ((uintptr_t)src & 15) == 0;
-  for (uint64_t blk = 0; blk < nfull; ++blk) {
-    const uint8_t* p = src + (blk << 6);
-    if (al16) {
+  if (al16) {
+    // The next block's 64 bytes are loaded while this block is compressed: one HBM round trip
+    // per block (~1-2 us under load) would otherwise sit on every lane's serial chain.
+    u32x4 nx[4];
+    if (nfull) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(src + 16 * q);
+    }
+    for (uint64_t blk = 0; blk < nfull; ++blk) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(p + 16 * q);
-        w[4 * q + 0] = __builtin_bswap32(v.x);
-        w[4 * q + 1] = __builtin_bswap32(v.y);
-        w[4 * q + 2] = __builtin_bswap32(v.z);
-        w[4 * q + 3] = __builtin_bswap32(v.w);
+        w[4 * q + 0] = __builtin_bswap32(nx[q].x);
+        w[4 * q + 1] = __builtin_bswap32(nx[q].y);
+        w[4 * q + 2] = __builtin_bswap32(nx[q].z);
+        w[4 * q + 3] = __builtin_bswap32(nx[q].w);
       }
-    } else {
+      if (blk + 1 < nfull) {
+        const uint8_t* p = src + ((blk + 1) << 6);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+      }
+      sha256_block(h, w);
+    }
+  } else {
+    for (uint64_t blk = 0; blk < nfull; ++blk) {
+      const uint8_t* p = src + (blk << 6);
 #pragma unroll
       for (int q = 0; q < 16; ++q)
         w[q] = (uint32_t)p[4 * q] << 24 | (uint32_t)p[4 * q + 1] << 16 |
                (uint32_t)p[4 * q + 2] << 8 | (uint32_t)p[4 * q + 3];
+      sha256_block(h, w);
     }
-    sha256_block(h, w);
   }
   // Padding: remaining r bytes, 0x80, zeros, 64-bit big-endian bit length.
   const uint32_t r = (uint32_t)(len & 63);
