@@ -39,6 +39,9 @@ CONFIGS = {
     3: (2, 1, 8 * MiB, 64, "degraded reconstruct RS(2,1), erased fragment = seg mod 3, 1 GiB"),
     4: (2, 1, 8 * MiB, 4096, "64 GiB file (4096 x 16 MiB segments) encoded, sharded over GPUs"),
     5: (32, 32, 512 * 1024, 64, "RS(32,32) encode of 1 GiB + SHA-256 of all 64 fragments"),
+    # stress variant of config 3 for the wide code (not a BASELINE config): every segment loses
+    # m random fragments; decode matrices are run-time (host-inverted per pattern)
+    6: (32, 32, 512 * 1024, 64, "RS(32,32) degraded reconstruct, 32 random erasures/segment"),
 }
 
 
@@ -149,12 +152,17 @@ def main() -> None:
     if args.config == 3:
         present = np.ones((nseg, k + m), np.uint8)
         present[np.arange(nseg), (seg0 + np.arange(nseg)) % (k + m)] = 0
+    elif args.config == 6:
+        rng = np.random.default_rng(seg0 + 6)
+        present = np.ones((nseg, k + m), np.uint8)
+        for s_ in range(nseg):
+            present[s_, rng.choice(k + m, size=m, replace=False)] = 0
     d_hex = None
     if args.config == 5:
         d_hex = torch.empty((nseg, k + m, 64), dtype=torch.uint8, device=dev)
 
     def step():
-        if args.config == 3:
+        if args.config in (3, 6):
             enc.ReconstructBatch(d_data, d_par, nseg, F, present, stream=stream)
         else:
             enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
@@ -162,7 +170,7 @@ def main() -> None:
                 enc.Sha256Batch(d_data, d_par, nseg, F, d_hex, stream=stream)
 
     def step_codec():  # the codec kernel alone (config 5's step also hashes)
-        if args.config == 3:
+        if args.config in (3, 6):
             enc.ReconstructBatch(d_data, d_par, nseg, F, present, stream=stream)
         else:
             enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
@@ -246,7 +254,7 @@ def main() -> None:
     tag = f"c{args.config}"
     traffic = load_traffic(tag)
     kernel_name = {2: "k_ct<EncCT<2,1>>", 3: "k_ct<Dec1CT<2,1,*>> / k_ct<EncCT<2,1>>",
-                   4: "k_ct<EncCT<2,1>>", 5: "k_ct<EncCT<32,32>>"}[args.config]
+                   4: "k_ct<EncCT<2,1>>", 5: "k_ct<EncCT<32,32>>", 6: "k_rt<32,1>"}[args.config]
     if args.generic:
         kernel_name = "k_rt"
     out = {

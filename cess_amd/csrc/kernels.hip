@@ -269,6 +269,69 @@ __device__ __forceinline__ void ct_column_stream(LD ld, ST st) {
   static_for<P::NO>([&](auto O) CEC_AI { st(O, acc[O]); });
 }
 
+// Nibble-window form (method of four Russians over the xtime basis): for input column j,
+// lo[v] = (v)·x and hi[v] = (16 v)·x for v = 1..15 are built from the powers with one XOR each
+// (only the entries some output uses, plus the entries they are built from), then every
+// (output, input) pair costs one v_bitop3: acc ^= lo[c & 15] ^ hi[c >> 4].
+template <unsigned USED>
+constexpr unsigned nibble_closure() {
+  unsigned need = USED & 0xFFFEu;
+  for (int v = 15; v >= 1; --v)
+    if ((need >> v & 1) && (v & (v - 1))) need |= 1u << (v & (v - 1));
+  return need;
+}
+
+template <class P, int J, int HALF>
+constexpr unsigned nibbles_used() {
+  unsigned u = 0;
+  for (int o = 0; o < P::NO; ++o) u |= 1u << ((P::v.c[o][J] >> (4 * HALF)) & 15);
+  return u;
+}
+
+template <class P, int PF, class T, class LD, class ST>
+__device__ __forceinline__ void ct_column_window(LD ld, ST st) {
+  T acc[P::NO];
+  T ring[PF];
+  static_for<P::NO>([&](auto O) CEC_AI { acc[O] = T(0); });
+  static_for<(PF < P::NI ? PF : P::NI)>([&](auto J) CEC_AI { ring[J] = ld(J); });
+  static_for<P::NI>([&](auto J) CEC_AI {
+    constexpr int j = J;
+    T p[8];
+    p[0] = ring[j % PF];
+    if constexpr (j + PF < P::NI) ring[j % PF] = ld(std::integral_constant<int, j + PF>{});
+    static_for<7>([&](auto B) CEC_AI {
+      constexpr int b = B + 1;
+      if constexpr (b <= P::v.hb_col[j]) p[b] = xt(p[b - 1]);
+    });
+    T lo[16], hi[16];
+    constexpr unsigned need_lo = nibble_closure<nibbles_used<P, j, 0>()>();
+    constexpr unsigned need_hi = nibble_closure<nibbles_used<P, j, 1>()>();
+    static_for<16>([&](auto V) CEC_AI {
+      constexpr int v = V;
+      constexpr int low = v & -v;                 // lowest set bit of v
+      constexpr int bit = low == 1 ? 0 : low == 2 ? 1 : low == 4 ? 2 : 3;
+      if constexpr (v > 0 && (need_lo >> v & 1)) {
+        if constexpr ((v & (v - 1)) == 0) lo[v] = p[bit];
+        else lo[v] = xor2(lo[v & (v - 1)], p[bit]);
+      }
+      if constexpr (v > 0 && (need_hi >> v & 1)) {
+        if constexpr ((v & (v - 1)) == 0) hi[v] = p[bit + 4];
+        else hi[v] = xor2(hi[v & (v - 1)], p[bit + 4]);
+      }
+    });
+    static_for<P::NO>([&](auto O) CEC_AI {
+      constexpr int o = O;
+      constexpr unsigned c = P::v.c[o][j];
+      constexpr unsigned cl = c & 15, chh = c >> 4;
+      if constexpr (cl && chh) acc[o] = xor3(acc[o], lo[cl], hi[chh]);
+      else if constexpr (cl) acc[o] = xor2(acc[o], lo[cl]);
+      else if constexpr (chh) acc[o] = xor2(acc[o], hi[chh]);
+    });
+    if constexpr (P::NO > 8) __builtin_amdgcn_sched_barrier(0);
+  });
+  static_for<P::NO>([&](auto O) CEC_AI { st(O, acc[O]); });
+}
+
 // Byte-wise finish of the last (len % 16) bytes, run by the last block of each segment.
 template <class P, int VB>
 __device__ __forceinline__ void ct_tail(const Layout& L, uint32_t seg) {
@@ -285,7 +348,7 @@ __device__ __forceinline__ void ct_tail(const Layout& L, uint32_t seg) {
   else ct_column_stream<P, 1, uint32_t>(ld, st);
 }
 
-template <class P, int U, bool NT, class TV = u32x4, int PF = 1>
+template <class P, int U, bool NT, class TV = u32x4, int PF = 1, bool WIN = false>
 __global__ __launch_bounds__(256) void k_ct(Layout L, const uint32_t* __restrict__ seg_list,
                                             uint32_t seg0) {
   constexpr int VB = sizeof(TV);  // bytes per lane per shard per column
@@ -303,6 +366,7 @@ __global__ __launch_bounds__(256) void k_ct(Layout L, const uint32_t* __restrict
       st16<NT, TV>(shard_ptr_ct<P::K, P::v.out[O]>(L, seg) + off, y);
     };
     if constexpr (use_horner<P>(U)) ct_column_horner<P, TV>(ld, st);
+    else if constexpr (WIN) ct_column_window<P, PF, TV>(ld, st);
     else ct_column_stream<P, PF, TV>(ld, st);
   };
   if (base + (U - 1) * 256 < nvec) {  // full tile: no per-element predicate
@@ -595,15 +659,15 @@ void for_seg_chunks(uint32_t nseg, F f) {
   for (uint32_t s0 = 0; s0 < nseg; s0 += kMaxGridY) f(s0, nseg - s0 < kMaxGridY ? nseg - s0 : kMaxGridY);
 }
 
-template <class P, int U, bool NT, class TV = u32x4, int PF = 1>
+template <class P, int U, bool NT, class TV = u32x4, int PF = 1, bool WIN = false>
 void run_ct(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
   if (layout_vec16_ok(L)) {
     const uint64_t nvec = L.len / sizeof(TV);
     uint64_t gx = (nvec + 256 * U - 1) / (256 * U);
     if (gx == 0) gx = 1;  // tail-only shard
     for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {
-      hipLaunchKernelGGL((k_ct<P, U, NT, TV, PF>), dim3((unsigned)gx, ny), dim3(256), 0, st, L,
-                         seg_list, s0);
+      hipLaunchKernelGGL((k_ct<P, U, NT, TV, PF, WIN>), dim3((unsigned)gx, ny), dim3(256), 0, st,
+                         L, seg_list, s0);
     });
   } else {
     const uint64_t gx = (L.len + 255) / 256;
@@ -639,7 +703,11 @@ void run_wide_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, 
     case 3: run_ct<P, 1, false, u32x2, 4>(L, seg_list, nseg, st); break;
     case 4: run_ct<P, 1, true, u32x2, 4>(L, seg_list, nseg, st); break;
     case 5: run_ct<P, 1, false, u32x2, 8>(L, seg_list, nseg, st); break;
-    default: run_ct<P, 1, false, u32x2, 2>(L, seg_list, nseg, st); break;  // r01 sweep
+    case 6: run_ct<P, 1, false, u32x2, 2, true>(L, seg_list, nseg, st); break;
+    case 7: run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st); break;
+    case 8: run_ct<P, 1, false, u32x2, 4, true>(L, seg_list, nseg, st); break;
+    case 9: run_ct<P, 1, false, u32x4, 2, true>(L, seg_list, nseg, st); break;
+    default: run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st); break;  // r01 sweep
   }
 }
 
