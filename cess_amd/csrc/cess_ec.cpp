@@ -44,46 +44,71 @@ int set_err(int code, const std::string& msg) {
                      std::string(#expr) + ": " + hipGetErrorString(_e));                \
   } while (0)
 
-// One launch of the run-time kernel: up to kRtMaxOut outputs from nin survivors.
-struct RtLaunch {
-  cec::RtSel sel{};
-  int nin = 0, nout = 0;
-  uint32_t* dcoef = nullptr;  // device [nin][bucket]
+// A run-time program: chunks of up to kRtMaxOut outputs, each a device block in the layout of
+// kernels.h (header, input indices, output indices, coefficients [nin][nob]).
+struct RtChunk {
+  uint32_t* dev = nullptr;
+  int nin = 0, nout = 0, nob = 0;
 };
 
 struct Program {
-  std::vector<RtLaunch> launches;
+  std::vector<RtChunk> chunks;
   int nout = 0;     // total outputs
   int single = -1;  // the one missing shard when exactly one output (compile-time decode)
+  uint8_t in_idx[cec::kMaxShards] = {};   // survivors read (host copy)
+  uint8_t out_idx[cec::kMaxShards] = {};  // shards written (host copy)
 };
 
 void free_program(Program& p) {
-  for (auto& l : p.launches)
-    if (l.dcoef) (void)hipFree(l.dcoef);
-  p.launches.clear();
+  for (auto& c : p.chunks)
+    if (c.dev) (void)hipFree(c.dev);
+  p.chunks.clear();
 }
 
-// Upload coefficient rows for outputs out_idx[o] (coef[o][j]) as run-time launches.
+// Upload coefficient rows for outputs out_idx[o] (coef[o][j]) as run-time chunks.
 int build_program(const uint8_t* in_idx, int nin, const uint8_t* out_idx, int nout,
                   const BigMat& coef, Program& prog) {
   prog.nout = nout;
   prog.single = nout == 1 ? out_idx[0] : -1;
+  std::memcpy(prog.in_idx, in_idx, nin);
+  std::memcpy(prog.out_idx, out_idx, nout);
   for (int o0 = 0; o0 < nout; o0 += cec::kRtMaxOut) {
-    RtLaunch l;
-    l.nin = nin;
-    l.nout = std::min(cec::kRtMaxOut, nout - o0);
-    const int nb = cec::rt_bucket(l.nout);
-    for (int j = 0; j < nin; ++j) l.sel.in[j] = in_idx[j];
-    for (int o = 0; o < l.nout; ++o) l.sel.out[o] = out_idx[o0 + o];
-    std::vector<uint32_t> h((size_t)nin * nb, 0u);
-    for (int j = 0; j < nin; ++j)
-      for (int o = 0; o < l.nout; ++o) h[(size_t)j * nb + o] = coef.v[o0 + o][j];
-    HIP_TRY(hipMalloc(&l.dcoef, h.size() * sizeof(uint32_t)));
-    prog.launches.push_back(l);
-    HIP_TRY(hipMemcpy(l.dcoef, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    RtChunk c;
+    c.nin = nin;
+    c.nout = std::min(cec::kRtMaxOut, nout - o0);
+    c.nob = cec::rt_bucket(c.nout);
+    std::vector<uint32_t> h(cec::rt_chunk_bytes(nin, c.nob) / sizeof(uint32_t), 0u);
+    h[0] = (uint32_t)nin;
+    h[1] = (uint32_t)c.nout;
+    h[2] = (uint32_t)c.nob;
+    for (int j = 0; j < nin; ++j) h[4 + j] = in_idx[j];
+    for (int o = 0; o < c.nout; ++o) h[4 + 256 + o] = out_idx[o0 + o];
+    uint32_t* hb = h.data() + 4 + 512;
+    uint32_t* mk = h.data() + cec::kRtHeaderWords;
+    for (int j = 0; j < nin; ++j) {
+      int top = -1;
+      for (int o = 0; o < c.nout; ++o) {
+        const unsigned cf = coef.v[o0 + o][j];
+        for (int b = 0; b < 8; ++b)
+          if (cf >> b & 1) {
+            mk[((size_t)j * 8 + b) * c.nob + o] = 0xFFFFFFFFu;
+            top = std::max(top, b);
+          }
+      }
+      hb[j] = (uint32_t)top;
+    }
+    HIP_TRY(hipMalloc(&c.dev, h.size() * sizeof(uint32_t)));
+    prog.chunks.push_back(c);
+    HIP_TRY(hipMemcpy(c.dev, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   }
   return CEC_OK;
 }
+
+// One multi-pattern run-time launch of the per-segment reconstruct path.
+struct PsLaunch {
+  int nob = 0;
+  size_t off = 0, count = 0;  // into the cached segment-list / chunk-pointer arrays
+};
 
 }  // namespace
 
@@ -97,12 +122,17 @@ struct cec_codec {
   // staging for the host-buffer API: [n][stride]
   uint8_t* stage = nullptr;
   size_t stage_bytes = 0;
-  // cached grouping of the last per-segment reconstruct call
+  // cached plan of the last per-segment reconstruct call: either compile-time launches per
+  // pattern (ps_ct: pattern key, offset, count into ps_list) or multi-pattern run-time
+  // launches (ps_rt: segment list + per-segment chunk pointers)
   std::string ps_key;
   bool ps_valid = false;
   uint32_t* ps_list = nullptr;
   size_t ps_list_bytes = 0;
-  std::vector<std::pair<std::string, std::pair<size_t, size_t>>> ps_work;
+  uint8_t* ps_ptrs = nullptr;  // const uint32_t* [count] per launch
+  size_t ps_ptrs_bytes = 0;
+  std::vector<std::pair<std::string, std::pair<size_t, size_t>>> ps_ct;
+  std::vector<PsLaunch> ps_rt;
 
   ~cec_codec() {
     (void)hipSetDevice(device);
@@ -110,6 +140,7 @@ struct cec_codec {
     for (auto& kv : decode_cache) free_program(kv.second);
     if (stage) (void)hipFree(stage);
     if (ps_list) (void)hipFree(ps_list);
+    if (ps_ptrs) (void)hipFree(ps_ptrs);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -135,8 +166,8 @@ Layout batch_layout(const cec_codec* c, const uint8_t* d_data, const uint8_t* d_
 
 void run_program(const Program& p, const Layout& L, const uint32_t* seg_list, uint32_t nseg,
                  hipStream_t st) {
-  for (const auto& l : p.launches)
-    cec::launch_matvec_rt(L, l.sel, l.nin, l.nout, l.dcoef, seg_list, nseg, st);
+  for (const auto& c : p.chunks)
+    cec::launch_matvec_rt(L, c.dev, nullptr, c.nob, seg_list, nseg, st);
 }
 
 int check_launch() {
@@ -177,6 +208,7 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, const Progr
     (void)hipDeviceSynchronize();
     for (auto& kv : c->decode_cache) free_program(kv.second);
     c->decode_cache.clear();
+    c->ps_valid = false;  // its chunk pointers referred to the freed programs
   }
   Program prog;
   if (plan->nout > 0) {
@@ -343,40 +375,89 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
     if (rc) return rc;
     return do_decode(c, *p, L, nullptr, (uint32_t)nseg, st);
   }
-  // Group segments by pattern; one launch sequence per distinct pattern over its segment list.
-  // The grouping and its device-side segment lists are cached for a repeated pattern array
-  // (the degraded-read bench and repair loops call with the same erasure map every time).
+  // Per-segment patterns. Segments are grouped by pattern once and the grouping is cached for a
+  // repeated pattern array (degraded-read bench and repair loops pass the same map each call).
+  //  * every pattern has a compile-time single-erasure kernel (RS(2,1)): one launch per
+  //    pattern over its segment list;
+  //  * otherwise: one multi-pattern run-time launch per (chunk index, bucket), each segment's
+  //    workgroup row reading its own pattern's chunk, so a batch where every segment has a
+  //    different erasure map is still one full-grid launch.
   std::string pkey(reinterpret_cast<const char*>(present), nseg * n);
   for (auto& ch : pkey) ch = ch ? 1 : 0;
   pkey.push_back(data_only ? 1 : 0);
+  pkey.push_back(c->force_generic ? 1 : 0);
   if (c->ps_key != pkey || !c->ps_valid) {
     c->ps_valid = false;
+    c->ps_ct.clear();
+    c->ps_rt.clear();
     std::unordered_map<std::string, std::vector<uint32_t>> groups;
     for (size_t s = 0; s < nseg; ++s) groups[pkey.substr(s * n, n)].push_back((uint32_t)s);
-    std::vector<uint32_t> hl;
-    std::vector<std::pair<std::string, std::pair<size_t, size_t>>> work;
+    bool all_ct = !c->force_generic;
+    std::vector<std::pair<const Program*, const std::vector<uint32_t>*>> progs;
     for (auto& g : groups) {
       const Program* p = nullptr;
       int rc = get_decode(c, reinterpret_cast<const uint8_t*>(g.first.data()), data_only != 0, &p);
       if (rc) return rc;
       if (!p->nout) continue;
-      work.push_back({g.first, {hl.size(), g.second.size()}});
-      hl.insert(hl.end(), g.second.begin(), g.second.end());
+      progs.push_back({p, &g.second});
+      if (p->single < 0 || !cec::has_decode_ct(c->k, c->m, p->single)) all_ct = false;
+    }
+    std::vector<uint32_t> hl;
+    std::vector<const uint32_t*> hp;
+    if (all_ct) {
+      for (auto& g : groups) {
+        const Program* p = nullptr;
+        get_decode(c, reinterpret_cast<const uint8_t*>(g.first.data()), data_only != 0, &p);
+        if (!p->nout) continue;
+        c->ps_ct.push_back({g.first, {hl.size(), g.second.size()}});
+        hl.insert(hl.end(), g.second.begin(), g.second.end());
+      }
+    } else {
+      size_t maxchunks = 0;
+      for (auto& pr : progs) maxchunks = std::max(maxchunks, pr.first->chunks.size());
+      for (size_t ci = 0; ci < maxchunks; ++ci) {
+        std::unordered_map<int, std::vector<std::pair<uint32_t, const uint32_t*>>> byb;
+        for (auto& pr : progs)
+          if (ci < pr.first->chunks.size())
+            for (uint32_t sg : *pr.second)
+              byb[pr.first->chunks[ci].nob].push_back({sg, pr.first->chunks[ci].dev});
+        for (auto& b : byb) {
+          PsLaunch l;
+          l.nob = b.first;
+          l.off = hl.size();
+          l.count = b.second.size();
+          for (auto& e : b.second) {
+            hl.push_back(e.first);
+            hp.push_back(e.second);
+          }
+          c->ps_rt.push_back(l);
+        }
+      }
     }
     int rc = ensure(reinterpret_cast<uint8_t**>(&c->ps_list), &c->ps_list_bytes,
                     std::max<size_t>(hl.size(), 1) * sizeof(uint32_t));
     if (rc) return rc;
+    rc = ensure(&c->ps_ptrs, &c->ps_ptrs_bytes, std::max<size_t>(hp.size(), 1) * sizeof(void*));
+    if (rc) return rc;
     if (!hl.empty())
       HIP_TRY(hipMemcpy(c->ps_list, hl.data(), hl.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    c->ps_work = std::move(work);
+    if (!hp.empty())
+      HIP_TRY(hipMemcpy(c->ps_ptrs, hp.data(), hp.size() * sizeof(void*), hipMemcpyHostToDevice));
     c->ps_key = std::move(pkey);
     c->ps_valid = true;
   }
-  for (const auto& w : c->ps_work) {
+  for (const auto& w : c->ps_ct) {
     const Program* p = nullptr;
     int rc = get_decode(c, reinterpret_cast<const uint8_t*>(w.first.data()), data_only != 0, &p);
     if (rc) return rc;
     rc = do_decode(c, *p, L, c->ps_list + w.second.first, (uint32_t)w.second.second, st);
+    if (rc) return rc;
+  }
+  const uint32_t* const* ptrs = reinterpret_cast<const uint32_t* const*>(c->ps_ptrs);
+  for (const auto& l : c->ps_rt) {
+    cec::launch_matvec_rt(L, nullptr, ptrs + l.off, l.nob, c->ps_list + l.off,
+                          (uint32_t)l.count, st);
+    int rc = check_launch();
     if (rc) return rc;
   }
   return CEC_OK;
@@ -492,20 +573,18 @@ int cec_reconstruct(cec_codec* c, uint8_t* const* shards, const uint8_t* present
   if (rc) return rc;
   Layout L = stage_layout(c, shard_len);
   // Upload only the survivors the plan reads.
-  const auto& first = p->launches[0];
-  for (int j = 0; j < first.nin; ++j) {
-    const int i = first.sel.in[j];
+  for (int j = 0; j < c->k; ++j) {
+    const int i = p->in_idx[j];
     HIP_TRY(hipMemcpyAsync(c->stage + i * stride, shards[i], shard_len, hipMemcpyHostToDevice,
                            c->stream));
   }
   rc = do_decode(c, *p, L, nullptr, 1, c->stream);
   if (rc) return rc;
-  for (const auto& l : p->launches)
-    for (int o = 0; o < l.nout; ++o) {
-      const int i = l.sel.out[o];
-      HIP_TRY(hipMemcpyAsync(shards[i], c->stage + i * stride, shard_len, hipMemcpyDeviceToHost,
-                             c->stream));
-    }
+  for (int o = 0; o < p->nout; ++o) {
+    const int i = p->out_idx[o];
+    HIP_TRY(hipMemcpyAsync(shards[i], c->stage + i * stride, shard_len, hipMemcpyDeviceToHost,
+                           c->stream));
+  }
   HIP_TRY(hipStreamSynchronize(c->stream));
   return CEC_OK;
 }

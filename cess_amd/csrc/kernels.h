@@ -20,11 +20,15 @@ struct Layout {
   int k;
 };
 
-// Survivor / output shard indices for the run-time-coefficient kernel (passed by value).
-struct RtSel {
-  uint8_t in[256];
-  uint8_t out[256];
-};
+// One run-time-coefficient program chunk in HBM: up to kRtMaxOut outputs from `nin` inputs.
+// Layout (all uint32): header {nin, nout, nob, 0}, in[256], out[256], hb[256] (highest set
+// coefficient bit of input column j, -1 for a zero column), then masks[nin][8][nob]:
+// masks[j][b][o] = 0xFFFFFFFF when bit b of coef[o][j] is set (zero padded to the bucket nob).
+constexpr int kRtMaxOut = 32;
+constexpr size_t kRtHeaderWords = 4 + 256 + 256 + 256;
+inline size_t rt_chunk_bytes(int nin, int nob) {
+  return (kRtHeaderWords + (size_t)nin * 8 * nob) * sizeof(uint32_t);
+}
 
 // True when every shard start and the shard length allow 16-byte vector access.
 bool layout_vec16_ok(const Layout& L);
@@ -38,14 +42,16 @@ bool launch_encode_ct(int k, int m, const Layout& L, const uint32_t* seg_list, u
 bool launch_decode_ct(int k, int m, int missing, const Layout& L, const uint32_t* seg_list,
                       uint32_t nseg, hipStream_t st);
 
-// Largest output count one run-time launch handles; more outputs are split over launches.
-constexpr int kRtMaxOut = 32;
+// Whether a compile-time single-erasure decode kernel exists for (k, m, missing).
+bool has_decode_ct(int k, int m, int missing);
+
 // Bucketed output count the run-time kernel is instantiated for (>= nout).
 int rt_bucket(int nout);
-// Run-time coefficient GF matvec: out[r] = XOR_j coef[j][r] * in[j]. `dcoef` is a device array
-// laid out [nin][rt_bucket(nout)] of uint32 (one coefficient byte per word, zero padded).
-void launch_matvec_rt(const Layout& L, const RtSel& sel, int nin, int nout, const uint32_t* dcoef,
-                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
+// Run-time coefficient GF matvec: out[r] = XOR_j coef[j][r] * in[j]. Either every segment uses
+// the chunk `chunk`, or listed segment y uses per_seg[y] (all chunks of one launch share the
+// bucket `nob`). Chunks are device memory laid out as described at RtChunk above.
+void launch_matvec_rt(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
+                      int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
 
 // SHA-256 of `n` equal-length buffers, written as 64 lowercase hex characters each into
 // `hex_out` (device, n * 64 bytes). If `ptrs` is null, buffer i is shard (i % nshards) of

@@ -182,6 +182,17 @@ template <class T>
 __device__ __forceinline__ T xor2(T a, T b) {
   return xor3(a, b, T(0));
 }
+// a ^ (b & m), m a wave-uniform mask (truth table 0x78)
+__device__ __forceinline__ uint32_t bitop3_xand(uint32_t a, uint32_t b, uint32_t m) {
+  return __builtin_amdgcn_bitop3_b32(a, b, m, 0x78);
+}
+__device__ __forceinline__ u32x2 bitop3_xand(u32x2 a, u32x2 b, uint32_t m) {
+  return u32x2{bitop3_xand(a.x, b.x, m), bitop3_xand(a.y, b.y, m)};
+}
+__device__ __forceinline__ u32x4 bitop3_xand(u32x4 a, u32x4 b, uint32_t m) {
+  return u32x4{bitop3_xand(a.x, b.x, m), bitop3_xand(a.y, b.y, m), bitop3_xand(a.z, b.z, m),
+               bitop3_xand(a.w, b.w, m)};
+}
 
 struct BitList {
   int n;
@@ -399,81 +410,111 @@ __global__ __launch_bounds__(256) void k_ct_bytes(Layout L, const uint32_t* __re
 // ---------------------------------------------------------------------------------------------
 // Run-time coefficients
 // ---------------------------------------------------------------------------------------------
-template <class T>
-__device__ __forceinline__ T sel_mask(T p, uint32_t m) {
-  return p & m;
+// One workgroup row (blockIdx.y) = one segment; its program chunk (indices + coefficients) is
+// read with scalar loads, so segments with different erasure patterns share one launch. Per
+// input column: the xtime powers up to the column's highest coefficient bit, then one
+// v_bitop3 (acc ^= pow_b & mask) per (output, bit) with masks expanded on the SALU. The next
+// input column's loads are issued before the current column is multiplied in.
+// Program chunks are read through the constant address space: they are never written while a
+// kernel runs, so uniform-address loads become s_load (SGPR results, SALU mask expansion).
+typedef const uint32_t __attribute__((address_space(4))) cu32;
+__device__ __forceinline__ const cu32* as_const(const uint32_t* p) {
+  return (const cu32*)(uintptr_t)p;
 }
 
-// coef layout: [nin][NOB] uint32, one coefficient per word.
-template <int NOB, int U, class T, class LD>
-__device__ __forceinline__ void rt_accumulate(T (&acc)[NOB][U], int nin,
-                                              const uint32_t* __restrict__ coef, LD ld) {
-  for (int j = 0; j < nin; ++j) {
-    T p[8][U];
+template <int NOB, int U, class TV, class T, class LD>
+__device__ __forceinline__ void rt_accumulate(T (&acc)[NOB][U], const cu32* __restrict__ P,
+                                              LD ld) {
+  const uint32_t nin = P[0];
+  const cu32* __restrict__ hbs = P + 4 + 512;
+  const cu32* __restrict__ masks = P + kRtHeaderWords;
+  T cur[U], nxt[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) p[0][u] = ld(j, u);
+  for (int u = 0; u < U; ++u) cur[u] = ld(P[4], u);
+  for (uint32_t j = 0; j < nin; ++j) {
+    if (j + 1 < nin) {
 #pragma unroll
-    for (int b = 1; b < 8; ++b)
+      for (int u = 0; u < U; ++u) nxt[u] = ld(P[4 + j + 1], u);
+    }
+    const int hb = (int)hbs[j];
+    T p[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) p[b][u] = xt(p[b - 1][u]);
+    for (int u = 0; u < U; ++u) p[u] = cur[u];
 #pragma unroll
-    for (int o = 0; o < NOB; ++o) {
-      const uint32_t c = coef[j * NOB + o];
+    for (int b = 0; b < 8; ++b) {
+      if (b > hb) break;  // wave-uniform: no higher coefficient bit in this column
+      if (b > 0) {
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const uint32_t m = (uint32_t)(-(int32_t)((c >> b) & 1u));
+        for (int u = 0; u < U; ++u) p[u] = xt(p[u]);
+      }
+      const cu32* __restrict__ mk = masks + (j * 8 + b) * NOB;
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc[o][u] ^= p[b][u] & m;
+      for (int o = 0; o < NOB; ++o) {
+        const uint32_t m = mk[o];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[o][u] = bitop3_xand(acc[o][u], p[u], m);
       }
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = nxt[u];
   }
 }
 
-template <int NOB, int U>
-__global__ __launch_bounds__(256) void k_rt(Layout L, RtSel sel, int nin, int nout,
-                                            const uint32_t* __restrict__ coef,
+__device__ __forceinline__ const uint32_t* as_const_ptr(const uint32_t* const* a, uint32_t y) {
+  typedef const uint64_t __attribute__((address_space(4))) cu64;
+  return (const uint32_t*)(uintptr_t)((const cu64*)(uintptr_t)a)[y];
+}
+
+template <int NOB, int U, class TV>
+__global__ __launch_bounds__(256) void k_rt(Layout L, const uint32_t* __restrict__ chunk,
+                                            const uint32_t* const* __restrict__ per_seg,
                                             const uint32_t* __restrict__ seg_list, uint32_t seg0,
                                             int vec_ok) {
-  const uint32_t seg = seg_list ? seg_list[seg0 + blockIdx.y] : seg0 + blockIdx.y;
+  const uint32_t y = seg0 + blockIdx.y;
+  const uint32_t seg = seg_list ? seg_list[y] : y;
+  const cu32* __restrict__ P = as_const(per_seg ? as_const_ptr(per_seg, y) : chunk);
+  const uint32_t nout = P[1];
+  const cu32* __restrict__ out_idx = P + 4 + 256;
+  constexpr int VB = sizeof(TV);
   if (vec_ok) {
-    const uint64_t nvec = L.len >> 4;
+    const uint64_t nvec = L.len / VB;
     const uint64_t base = (uint64_t)blockIdx.x * (256 * U) + threadIdx.x;
-    u32x4 acc[NOB][U];
+    TV acc[NOB][U];
 #pragma unroll
     for (int o = 0; o < NOB; ++o)
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc[o][u] = u32x4(0);
-    auto ld = [&](int j, int u) CEC_AI -> u32x4 {
+      for (int u = 0; u < U; ++u) acc[o][u] = TV(0);
+    auto ld = [&](uint32_t sh, int u) CEC_AI -> TV {
       const uint64_t v = base + u * 256;
-      if (v >= nvec) return u32x4(0);
-      return ld16<false>(shard_ptr(L, sel.in[j], seg) + (v << 4));
+      if (v >= nvec) return TV(0);
+      return ld16<false, TV>(shard_ptr(L, (int)sh, seg) + v * VB);
     };
-    rt_accumulate<NOB, U, u32x4>(acc, nin, coef, ld);
+    rt_accumulate<NOB, U, TV>(acc, P, ld);
 #pragma unroll
     for (int o = 0; o < NOB; ++o) {
-      if (o < nout) {
-        uint8_t* dst = shard_ptr(L, sel.out[o], seg);
+      if (o < (int)nout) {
+        uint8_t* dst = shard_ptr(L, (int)out_idx[o], seg);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const uint64_t v = base + u * 256;
-          if (v < nvec) st16<false>(dst + (v << 4), acc[o][u]);
+          if (v < nvec) st16<false, TV>(dst + v * VB, acc[o][u]);
         }
       }
     }
-    if (!(L.len & 15) || blockIdx.x != gridDim.x - 1) return;
+    if (!(L.len % VB) || blockIdx.x != gridDim.x - 1) return;
   }
   // byte path: whole shard (vec_ok == 0, grid covers len) or the tail (last block)
-  const uint64_t i = vec_ok ? (L.len & ~uint64_t(15)) + threadIdx.x
+  const uint64_t i = vec_ok ? (L.len - L.len % VB) + threadIdx.x
                             : (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= L.len) return;
   uint32_t acc[NOB][1];
 #pragma unroll
   for (int o = 0; o < NOB; ++o) acc[o][0] = 0;
-  auto ld = [&](int j, int) CEC_AI -> uint32_t { return shard_ptr(L, sel.in[j], seg)[i]; };
-  rt_accumulate<NOB, 1, uint32_t>(acc, nin, coef, ld);
+  auto ld = [&](uint32_t sh, int) CEC_AI -> uint32_t { return shard_ptr(L, (int)sh, seg)[i]; };
+  rt_accumulate<NOB, 1, uint32_t>(acc, P, ld);
 #pragma unroll
   for (int o = 0; o < NOB; ++o)
-    if (o < nout) shard_ptr(L, sel.out[o], seg)[i] = (uint8_t)acc[o][0];
+    if (o < (int)nout) shard_ptr(L, (int)out_idx[o], seg)[i] = (uint8_t)acc[o][0];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -741,35 +782,39 @@ int rt_bucket(int nout) {
   return kRtMaxOut;
 }
 
+bool has_decode_ct(int k, int m, int missing) {
+  return k == 2 && m == 1 && missing >= 0 && missing < 3;
+}
+
 namespace {
-template <int NOB, int U>
-void run_rt(const Layout& L, const RtSel& sel, int nin, int nout, const uint32_t* dcoef,
+template <int NOB, int U, class TV>
+void run_rt(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
             const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
   const int vec_ok = layout_vec16_ok(L) ? 1 : 0;
-  uint64_t gx = vec_ok ? (L.len / 16 + 256 * U - 1) / (256 * U) : (L.len + 255) / 256;
+  uint64_t gx = vec_ok ? (L.len / sizeof(TV) + 256 * U - 1) / (256 * U) : (L.len + 255) / 256;
   if (gx == 0) gx = 1;
-  for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {
-    hipLaunchKernelGGL((k_rt<NOB, U>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, sel, nin,
-                       nout, dcoef, seg_list, s0, vec_ok);
+  for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) {
+    hipLaunchKernelGGL((k_rt<NOB, U, TV>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, chunk,
+                       per_seg, seg_list, s0, vec_ok);
   });
 }
 }  // namespace
 
-void launch_matvec_rt(const Layout& L, const RtSel& sel, int nin, int nout, const uint32_t* dcoef,
-                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
-  switch (rt_bucket(nout)) {
-    case 1: run_rt<1, 2>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
-    case 2: run_rt<2, 2>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
-    case 3: run_rt<3, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
-    case 4: run_rt<4, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
-    case 5: run_rt<5, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
-    case 6: run_rt<6, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
-    case 7: run_rt<7, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
-    case 8: run_rt<8, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
-    case 12: run_rt<12, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
-    case 16: run_rt<16, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
-    case 24: run_rt<24, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
-    default: run_rt<32, 1>(L, sel, nin, nout, dcoef, seg_list, nseg, st); break;
+void launch_matvec_rt(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
+                      int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  switch (nob) {
+    case 1: run_rt<1, 1, u32x4>(L, chunk, per_seg, seg_list, nseg, st); break;
+    case 2: run_rt<2, 1, u32x4>(L, chunk, per_seg, seg_list, nseg, st); break;
+    case 3: run_rt<3, 1, u32x4>(L, chunk, per_seg, seg_list, nseg, st); break;
+    case 4: run_rt<4, 1, u32x4>(L, chunk, per_seg, seg_list, nseg, st); break;
+    case 5: run_rt<5, 1, u32x4>(L, chunk, per_seg, seg_list, nseg, st); break;
+    case 6: run_rt<6, 1, u32x4>(L, chunk, per_seg, seg_list, nseg, st); break;
+    case 7: run_rt<7, 1, u32x2>(L, chunk, per_seg, seg_list, nseg, st); break;
+    case 8: run_rt<8, 1, u32x2>(L, chunk, per_seg, seg_list, nseg, st); break;
+    case 12: run_rt<12, 1, u32x2>(L, chunk, per_seg, seg_list, nseg, st); break;
+    case 16: run_rt<16, 1, uint32_t>(L, chunk, per_seg, seg_list, nseg, st); break;
+    case 24: run_rt<24, 1, uint32_t>(L, chunk, per_seg, seg_list, nseg, st); break;
+    default: run_rt<32, 1, uint32_t>(L, chunk, per_seg, seg_list, nseg, st); break;
   }
 }
 

@@ -293,3 +293,93 @@ def test_segment_list_pipeline(torch, cess, orc, size, seg, k, m, hash_on):
     assert needed_space(rec.segments, seg) == len(want) * seg * 15 // 10
     for (s, i), h in frags.items():
         assert h.encode() == want[s][1][i]
+
+
+def test_degraded_read_single_rank(torch, cess, corc):
+    """distributed.degraded_read end to end on one GPU (world 1: every survivor is local, so
+    no P2P op is issued; the decode runs through libcessec)."""
+    from cess_amd import distributed as D
+    k, m, F, nseg = 2, 1, 1 << 16, 6
+    rng = np.random.default_rng(11)
+    full = []
+    for s in range(nseg):
+        data = [rng.integers(0, 256, F, dtype=np.uint8) for _ in range(k)]
+        full.append(data + c_encode(corc, k, m, data))
+    mine = D.local_fragments(nseg, k + m, 1, 0)
+    store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
+                            torch.from_numpy(np.stack([full[s][f] for s, f in mine])).cuda())
+    lost = {s: [s % 3] for s in range(nseg)}
+    plan = D.plan_gather(lost, k, m, 1, F)
+    assert plan.bytes_moved == 0
+    out = D.degraded_read(plan, store, cess.New(k, m), 0)
+    torch.cuda.synchronize()
+    assert len(out) == nseg
+    for (s, f), t in out.items():
+        assert np.array_equal(t.cpu().numpy(), full[s][f])
+
+
+def test_cli_encode_and_verify(tmp_path, orc):
+    import json
+    import subprocess
+    import sys
+    rng = np.random.default_rng(3)
+    blob = rng.integers(0, 256, 3 * MiB + 5, dtype=np.uint8).tobytes()
+    src = tmp_path / "f.bin"
+    src.write_bytes(blob)
+    outdir = tmp_path / "frags"
+    r = subprocess.run([sys.executable, "-m", "cess_amd.cli", "encode", str(src), "--out",
+                        str(outdir), "--segment-size", str(1 << 20)], capture_output=True,
+                       text=True, timeout=300, check=True)
+    rec = json.loads(r.stdout)
+    want = orc.segment_list(blob, 2, 1, 1 << 20)
+    assert [(s["hash"].encode(), [f.encode() for f in s["fragment_list"]])
+            for s in rec["segments"]] == want
+    assert rec["check_file_spec"] and rec["needed_space"] == 4 * (1 << 20) * 15 // 10
+    files = sorted(p.name for p in outdir.iterdir())
+    assert files == sorted({f.decode() for _, fl in want for f in fl})
+    for p in outdir.iterdir():
+        assert hashlib.sha256(p.read_bytes()).hexdigest() == p.name
+
+
+def test_max_shards_256(cess, corc):
+    """k + m = 256 (the GF(2^8) limit): run-time kernel, outputs split over chunks of 32."""
+    k, m, ln = 200, 56, 272
+    rng = np.random.default_rng(256)
+    data = [rng.integers(0, 256, ln, dtype=np.uint8) for _ in range(k)]
+    want = c_encode(corc, k, m, data)
+    enc = cess.New(k, m)
+    shards = data + [np.zeros(ln, np.uint8) for _ in range(m)]
+    enc.Encode(shards)
+    assert all(np.array_equal(a, b) for a, b in zip(shards[k:], want))
+    erased = set(rng.choice(k + m, size=m, replace=False).tolist())
+    full = data + want
+    sh = [None if i in erased else full[i].copy() for i in range(k + m)]
+    enc.Reconstruct(sh)
+    assert all(np.array_equal(a, b) for a, b in zip(sh, full))
+    with pytest.raises(cess.ErrMaxShardNum):
+        cess.New(200, 57)
+
+
+def test_more_segments_than_grid_y(torch, cess, corc):
+    """nseg > 65535 splits the launch over grid.y chunks (encode and per-segment decode)."""
+    k, m, ln, nseg = 2, 1, 32, 70000
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    d_data = to_dev(torch, data)
+    d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
+    enc = cess.New(k, m)
+    enc.EncodeBatch(d_data, d_par, nseg, ln)
+    torch.cuda.synchronize()
+    par = d_par.cpu().numpy()
+    want = np.zeros_like(par)
+    corc.orc_encode_batch(k, m, data.ctypes.data, want.ctypes.data, nseg, ln, 8, 1)
+    assert np.array_equal(par, want)
+    present = np.ones((nseg, 3), np.uint8)
+    present[np.arange(nseg), np.arange(nseg) % 3] = 0
+    for generic in (0, 1):
+        enc.set_option(1, generic)
+        dd = to_dev(torch, data * present[:, :k, None])
+        dp = to_dev(torch, want * present[:, k:, None])
+        enc.ReconstructBatch(dd, dp, nseg, ln, present)
+        torch.cuda.synchronize()
+        assert np.array_equal(dd.cpu().numpy(), data) and np.array_equal(dp.cpu().numpy(), want)
