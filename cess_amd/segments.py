@@ -8,7 +8,9 @@ What the chain consumes (reference):
   * space locked = segments x SEGMENT_SIZE x 15 / 10 (lib.rs:440);
   * `Hash([u8; 64])` (primitives/common/src/lib.rs:16).
 Hash convention [ecosystem, unpinned by the reference]: 64 lowercase hex chars of SHA-256; the
-last segment is zero padded to SEGMENT_SIZE; the file hash is SHA-256 of the file bytes.
+last segment is zero padded to SEGMENT_SIZE. File hash [build convention]: SHA-256 (hex) of the
+concatenated hex segment hashes — a two-level hash, so no serial pass over the whole file
+(one serial SHA-256 stream caps a file at ~2 GB/s).
 
 Pipeline (one GPU): batches of up to 64 segments (1 GiB) go through pinned host buffers and two
 device slots. Batch i+1's H2D copy and encode overlap the hashing of batch i. Hashes are
@@ -59,6 +61,14 @@ class FileRecord:
                 "segments": [s.to_json() for s in self.segments]}
 
 
+def file_hash(seg_list: List[SegmentList]) -> bytes:
+    """SHA-256 hex over the concatenated segment hashes (two-level file hash)."""
+    h = hashlib.sha256()
+    for sgl in seg_list:
+        h.update(sgl.hash)
+    return h.hexdigest().encode()
+
+
 def check_file_spec(seg_list: List[SegmentList],
                     fragment_count: int = geometry.FRAGMENT_COUNT) -> bool:
     """c-pallets/file-bank/src/functions.rs:4-14."""
@@ -69,6 +79,56 @@ def needed_space(seg_list: List[SegmentList],
                  segment_size: int = geometry.SEGMENT_SIZE) -> int:
     """c-pallets/file-bank/src/lib.rs:440: segments x SEGMENT_SIZE x 15 / 10."""
     return len(seg_list) * (segment_size * 15 // 10)
+
+
+class _Limited(io.RawIOBase):
+    """Read at most `n` bytes from a file object."""
+
+    def __init__(self, f, n: int):
+        self.f, self.left = f, n
+
+    def readable(self):
+        return True
+
+    def readinto(self, b):
+        if self.left <= 0:
+            return 0
+        mv = memoryview(b)[: self.left]
+        n = self.f.readinto(mv)
+        self.left -= n or 0
+        return n
+
+
+def encode_file_sharded(path: str, rank: int, world: int, group=None, **kw) -> Optional[FileRecord]:
+    """Encode a file across `world` GPU ranks (one process per GPU): rank r encodes a
+    contiguous range of segments (distributed.shard_range) with no data exchange, then the
+    SegmentLists are gathered on rank 0 (object gather over the process group), which returns
+    the whole-file record. Other ranks return None."""
+    import os as _os
+
+    from .distributed import shard_range
+    seg_size = kw.get("segment_size", geometry.SEGMENT_SIZE)
+    size = _os.path.getsize(path)
+    nseg = (size + seg_size - 1) // seg_size
+    a, b = shard_range(nseg, world, rank)
+    part = []
+    if b > a:
+        se = SegmentEncoder(**kw)
+        part = se.encode_range(path, a, b).segments
+        se.close()
+    if world > 1:
+        import torch.distributed as dist
+        parts = [None] * world if rank == 0 else None
+        dist.gather_object(part, parts, dst=0, group=group)
+        if rank != 0:
+            return None
+    else:
+        parts = [part]
+    rec = FileRecord(b"", size)
+    for p in parts:
+        rec.segments.extend(p)
+    rec.file_hash = file_hash(rec.segments)
+    return rec
 
 
 class SegmentEncoder:
@@ -102,7 +162,7 @@ class SegmentEncoder:
                                   device=self.dev) for _ in range(2)]
         self.events = [None, None]
 
-    def _read_batch(self, f: BinaryIO, slot: int, file_hash) -> int:
+    def _read_batch(self, f: BinaryIO, slot: int) -> int:
         """Fill slot's pinned buffer with up to `batch` segments; returns segments read."""
         buf = self.h_data[slot].numpy().reshape(-1)
         got = 0
@@ -115,7 +175,6 @@ class SegmentEncoder:
             got += n
         if got == 0:
             return 0
-        file_hash.update(mv[:got])
         self._bytes += got
         nseg = (got + self.seg - 1) // self.seg
         if got < nseg * self.seg:  # zero-pad the last segment
@@ -136,18 +195,23 @@ class SegmentEncoder:
             ev.record(st)
         self.events[slot] = ev
 
-    def _finish(self, slot: int, nseg: int, seg_base: int, out: FileRecord,
-                on_fragment: Optional[Callable]) -> None:
+    def _submit_host_hashes(self, slot: int, nseg: int):
+        """Segment hashes (and data-fragment hashes on the host path) need only the host copy:
+        start them as soon as the batch is read, beside the GPU work."""
         data = self.h_data[slot].numpy()
-        k, m = self.k, self.m
-        # segment hashes (and data-fragment hashes on the host path) need only host data,
-        # so they start before the GPU batch completes
         seg_futs = [self.pool.submit(sha256_hex, memoryview(data[s].reshape(-1)))
                     for s in range(nseg)]
         dfuts = None
         if self.hash_on == "host":
-            dfuts = [[self.pool.submit(sha256_hex, memoryview(data[s, i])) for i in range(k)]
-                     for s in range(nseg)]
+            dfuts = [[self.pool.submit(sha256_hex, memoryview(data[s, i]))
+                      for i in range(self.k)] for s in range(nseg)]
+        return seg_futs, dfuts
+
+    def _finish(self, slot: int, nseg: int, seg_base: int, futs, out: FileRecord,
+                on_fragment: Optional[Callable]) -> None:
+        data = self.h_data[slot].numpy()
+        k, m = self.k, self.m
+        seg_futs, dfuts = futs
         self.events[slot].synchronize()
         par = self.h_par[slot].numpy()
         if self.hash_on == "host":
@@ -164,6 +228,17 @@ class SegmentEncoder:
                 for i in range(k + m):
                     on_fragment(seg_base + s, i, data[s, i] if i < k else par[s, i - k])
 
+    def encode_range(self, path: str, seg_start: int, seg_stop: int,
+                     on_fragment: Optional[Callable[[int, int, np.ndarray], None]] = None
+                     ) -> FileRecord:
+        """Encode segments [seg_start, seg_stop) of a file (one rank's shard of a file encoded
+        across GPUs). `file_hash` of the result covers only this range's segments."""
+        with open(path, "rb") as f:
+            f.seek(seg_start * self.seg)
+            limited = io.BufferedReader(_Limited(f, (seg_stop - seg_start) * self.seg))
+            rec = self.encode_file(limited, on_fragment=on_fragment)
+        return rec
+
     def encode_file(self, src: Union[str, bytes, BinaryIO],
                     on_fragment: Optional[Callable[[int, int, np.ndarray], None]] = None
                     ) -> FileRecord:
@@ -175,21 +250,22 @@ class SegmentEncoder:
             f, close = open(src, "rb"), True
         else:
             f, close = src, False
-        fh = hashlib.sha256()
         out = FileRecord(b"", 0)
         self._bytes = 0
         try:
             pending = None  # (slot, nseg, seg_base)
             seg_base, slot = 0, 0
             while True:
-                nseg = self._read_batch(f, slot, fh)
+                nseg = self._read_batch(f, slot)
+                futs = None
                 if nseg:
                     self._launch(slot, nseg)
+                    futs = self._submit_host_hashes(slot, nseg)
                 if pending is not None:
                     self._finish(*pending, out, on_fragment)
                 if not nseg:
                     break
-                pending = (slot, nseg, seg_base)
+                pending = (slot, nseg, seg_base, futs)
                 seg_base += nseg
                 slot ^= 1
         finally:
@@ -199,7 +275,7 @@ class SegmentEncoder:
             from .reedsolomon import ErrShortData
             raise ErrShortData(ErrShortData.__doc__)
         out.size = self._bytes
-        out.file_hash = fh.hexdigest().encode()
+        out.file_hash = file_hash(out.segments)
         return out
 
     def close(self):

@@ -26,7 +26,8 @@ no erasure crate). Its published algorithm, restated here:
     its inverse rebuilds missing data shards; missing parity is then re-encoded from the data.
   * Split: perShard = ceil(len / k); shard i = data[i*perShard:(i+1)*perShard], zero padded.
 Hash convention [ecosystem, unpinned by the reference]: fragment / segment Hash = the 64 ASCII
-characters of lowercase hex SHA-256 (FIPS 180-4) of the bytes.
+characters of lowercase hex SHA-256 (FIPS 180-4) of the bytes; file hash [build convention] =
+SHA-256 hex over the concatenated segment hashes.
 
 PARITY STATUS: RS arithmetic is *parity unpinned by the reference* (it holds no codec, no RS
 test and no RS fixture); SHA-256 is pinned by the reference's own NIST SHAVS files.
@@ -256,6 +257,14 @@ def segment_list(file_bytes: bytes, k: int = 2, m: int = 1, segment_size: int = 
         shards[k:] = rs.encode(shards[:k])
         out.append((sha256_hex(seg), [sha256_hex(x) for x in shards]))
     return out
+
+
+def file_hash(segments) -> bytes:
+    """[build convention, unpinned] SHA-256 hex over the concatenated hex segment hashes."""
+    h = hashlib.sha256()
+    for seg_hash, _ in segments:
+        h.update(seg_hash)
+    return h.hexdigest().encode()
 
 
 _M64 = np.uint64(0xFFFFFFFFFFFFFFFF)

@@ -287,7 +287,7 @@ def test_segment_list_pipeline(torch, cess, orc, size, seg, k, m, hash_on):
     se.close()
     want = orc.segment_list(blob, k, m, seg)
     assert [(s.hash, s.fragment_list) for s in rec.segments] == want
-    assert rec.file_hash.decode() == hashlib.sha256(blob).hexdigest()
+    assert rec.file_hash == orc.file_hash(want)
     assert rec.size == size
     assert check_file_spec(rec.segments, k + m)
     assert needed_space(rec.segments, seg) == len(want) * seg * 15 // 10
@@ -383,3 +383,24 @@ def test_more_segments_than_grid_y(torch, cess, corc):
         enc.ReconstructBatch(dd, dp, nseg, ln, present)
         torch.cuda.synchronize()
         assert np.array_equal(dd.cpu().numpy(), data) and np.array_equal(dp.cpu().numpy(), want)
+
+
+def test_encode_file_sharded_single_rank(tmp_path, orc):
+    from cess_amd.segments import encode_file_sharded
+    rng = np.random.default_rng(21)
+    blob = rng.integers(0, 256, 5 * MiB + 77, dtype=np.uint8).tobytes()
+    p = tmp_path / "g.bin"
+    p.write_bytes(blob)
+    for world_slice in range(3):  # each rank's range on its own, as a world of 3 would do
+        from cess_amd.distributed import shard_range
+        a, b = shard_range(6, 3, world_slice)
+        from cess_amd.segments import SegmentEncoder
+        se = SegmentEncoder(2, 1, 1 << 20, batch_segments=2)
+        rec = se.encode_range(str(p), a, b)
+        se.close()
+        want = orc.segment_list(blob, 2, 1, 1 << 20)[a:b]
+        assert [(s.hash, s.fragment_list) for s in rec.segments] == want
+    rec = encode_file_sharded(str(p), 0, 1, segment_size=1 << 20, batch_segments=4)
+    assert [(s.hash, s.fragment_list) for s in rec.segments] == orc.segment_list(
+        blob, 2, 1, 1 << 20)
+    assert rec.file_hash == orc.file_hash(orc.segment_list(blob, 2, 1, 1 << 20))

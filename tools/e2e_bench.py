@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Host-resident end-to-end rate of the file -> SegmentList pipeline (PCIe-inclusive; never the
+bench `value`): a synthetic in-memory file is read through pinned buffers, copied to HBM,
+encoded, parity copied back and every segment/fragment hashed (host SHA-NI or GPU SHA-256).
+
+usage: python tools/e2e_bench.py [--gib 2] [--k 2 --m 1] [--hash auto|host|gpu]"""
+import argparse
+import io
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=2.0)
+    ap.add_argument("--k", type=int, default=2)
+    ap.add_argument("--m", type=int, default=1)
+    ap.add_argument("--hash", default="auto")
+    ap.add_argument("--threads", type=int, default=16)
+    args = ap.parse_args()
+    from cess_amd.segments import SegmentEncoder
+    from oracle.c_oracle import load_c_oracle
+    seg = 16 << 20
+    nseg = int(args.gib * (1 << 30)) // seg
+    buf = np.empty(nseg * seg, np.uint8)
+    load_c_oracle().orc_fill_synthetic(buf.ctypes.data, seg, nseg, 0, 0xCE550009)
+    se = SegmentEncoder(args.k, args.m, seg, batch_segments=64, hash_on=args.hash,
+                        hash_threads=args.threads)
+    se.encode_file(io.BytesIO(buf[: 64 * seg].tobytes()))  # warm-up (allocations, pools)
+    f = io.BytesIO(memoryview(buf))
+    t0 = time.perf_counter()
+    rec = se.encode_file(f)
+    dt = time.perf_counter() - t0
+    se.close()
+    print(json.dumps({"e2e_GBps_file_bytes": round(nseg * seg / dt / 1e9, 2), "seconds": round(dt, 3),
+                      "segments": len(rec.segments), "k": args.k, "m": args.m,
+                      "hash_on": se.hash_on, "threads": args.threads}))
+
+
+if __name__ == "__main__":
+    main()
