@@ -359,13 +359,13 @@ __device__ __forceinline__ void ct_tail(const Layout& L, uint32_t seg) {
   else ct_column_stream<P, 1, uint32_t>(ld, st);
 }
 
-template <class P, int U, bool NT, class TV = u32x4, int PF = 1, bool WIN = false>
-__global__ __launch_bounds__(256) void k_ct(Layout L, const uint32_t* __restrict__ seg_list,
+template <class P, int U, bool NT, class TV = u32x4, int PF = 1, bool WIN = false, int BS = 256>
+__global__ __launch_bounds__(BS) void k_ct(Layout L, const uint32_t* __restrict__ seg_list,
                                             uint32_t seg0) {
   constexpr int VB = sizeof(TV);  // bytes per lane per shard per column
   const uint32_t seg = seg_list ? seg_list[seg0 + blockIdx.y] : seg0 + blockIdx.y;
   const uint64_t nvec = L.len / VB;
-  const uint64_t base = (uint64_t)blockIdx.x * (256 * U) + threadIdx.x;
+  const uint64_t base = (uint64_t)blockIdx.x * (BS * U) + threadIdx.x;
   // Shard pointers are recomputed per use (scalar base + index * stride): holding 2 * (NI + NO)
   // SGPRs of pointers live across the body overflows the SGPR file for wide codes.
   auto column = [&](uint64_t v) CEC_AI {
@@ -380,14 +380,40 @@ __global__ __launch_bounds__(256) void k_ct(Layout L, const uint32_t* __restrict
     else if constexpr (WIN) ct_column_window<P, PF, TV>(ld, st);
     else ct_column_stream<P, PF, TV>(ld, st);
   };
-  if (base + (U - 1) * 256 < nvec) {  // full tile: no per-element predicate
-    static_for<U>([&](auto u) CEC_AI { column(base + u * 256); });
+  if (base + (U - 1) * BS < nvec) {  // full tile: no per-element predicate
+    static_for<U>([&](auto u) CEC_AI { column(base + u * BS); });
   } else {
     static_for<U>([&](auto u) CEC_AI {
-      if (base + u * 256 < nvec) column(base + u * 256);
+      if (base + u * BS < nvec) column(base + u * BS);
     });
   }
   if ((L.len % VB) && blockIdx.x == gridDim.x - 1) ct_tail<P, VB>(L, seg);
+}
+
+// Persistent grid-stride variant: a fixed grid walks the flattened (segment, tile) space.
+template <class P, bool NT, int BS>
+__global__ __launch_bounds__(BS) void k_ct_persist(Layout L, const uint32_t* __restrict__ seg_list,
+                                                   uint32_t nseg, uint64_t tiles_per_seg) {
+  using TV = u32x4;
+  const uint64_t nvec = L.len / 16;
+  const uint64_t total = (uint64_t)nseg * tiles_per_seg;
+  for (uint64_t t = blockIdx.x; t < total; t += gridDim.x) {
+    const uint32_t y = (uint32_t)(t / tiles_per_seg);
+    const uint64_t tile = t - (uint64_t)y * tiles_per_seg;
+    const uint32_t seg = seg_list ? seg_list[y] : y;
+    const uint64_t v = tile * BS + threadIdx.x;
+    if (v < nvec) {
+      const uint64_t off = v * 16;
+      auto ld = [&](auto J) CEC_AI {
+        return ld16<NT, TV>(shard_ptr_ct<P::K, P::v.in[J]>(L, seg) + off);
+      };
+      auto st = [&](auto O, TV yv) CEC_AI {
+        st16<NT, TV>(shard_ptr_ct<P::K, P::v.out[O]>(L, seg) + off, yv);
+      };
+      ct_column_horner<P, TV>(ld, st);
+    }
+    if ((L.len % 16) && tile == tiles_per_seg - 1 && BS >= 16) ct_tail<P, 16>(L, seg);
+  }
 }
 
 // Byte-granular variant for layouts whose shard starts are not 16-byte aligned.
@@ -700,15 +726,15 @@ void for_seg_chunks(uint32_t nseg, F f) {
   for (uint32_t s0 = 0; s0 < nseg; s0 += kMaxGridY) f(s0, nseg - s0 < kMaxGridY ? nseg - s0 : kMaxGridY);
 }
 
-template <class P, int U, bool NT, class TV = u32x4, int PF = 1, bool WIN = false>
+template <class P, int U, bool NT, class TV = u32x4, int PF = 1, bool WIN = false, int BS = 256>
 void run_ct(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
   if (layout_vec16_ok(L)) {
     const uint64_t nvec = L.len / sizeof(TV);
-    uint64_t gx = (nvec + 256 * U - 1) / (256 * U);
+    uint64_t gx = (nvec + BS * U - 1) / (BS * U);
     if (gx == 0) gx = 1;  // tail-only shard
     for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {
-      hipLaunchKernelGGL((k_ct<P, U, NT, TV, PF, WIN>), dim3((unsigned)gx, ny), dim3(256), 0, st,
-                         L, seg_list, s0);
+      hipLaunchKernelGGL((k_ct<P, U, NT, TV, PF, WIN, BS>), dim3((unsigned)gx, ny), dim3(BS), 0,
+                         st, L, seg_list, s0);
     });
   } else {
     const uint64_t gx = (L.len + 255) / 256;
@@ -730,6 +756,17 @@ void run_ct_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hi
     case 3: run_ct<P, 1, true>(L, seg_list, nseg, st); break;
     case 4: run_ct<P, 2, true>(L, seg_list, nseg, st); break;
     case 5: run_ct<P, 4, true>(L, seg_list, nseg, st); break;
+    case 6: run_ct<P, 1, true, u32x4, 1, false, 512>(L, seg_list, nseg, st); break;
+    case 7: run_ct<P, 1, true, u32x4, 1, false, 128>(L, seg_list, nseg, st); break;
+    case 8: run_ct<P, 1, true, u32x4, 1, false, 1024>(L, seg_list, nseg, st); break;
+    case 9: case 10: case 11: {
+      if (!layout_vec16_ok(L) || (L.len & 15)) { run_ct<P, 1, true>(L, seg_list, nseg, st); break; }
+      const uint64_t tiles = (L.len / 16 + 255) / 256;
+      const unsigned grid = g_ct_variant == 9 ? 2048 : g_ct_variant == 10 ? 4096 : 8192;
+      hipLaunchKernelGGL((k_ct_persist<P, true, 256>), dim3(grid), dim3(256), 0, st, L, seg_list,
+                         nseg, tiles);
+      break;
+    }
     default: run_ct<P, 1, true>(L, seg_list, nseg, st); break;  // r01 sweep winner
   }
 }
