@@ -128,9 +128,17 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs for a one-GPU box: CESS_DIST_BACKEND=gloo CESS_DEVICE=0 runs several ranks
+    # on one GPU. The driver's multi-GPU run uses the defaults (RCCL, one rank per GPU).
+    backend = os.environ.get("CESS_DIST_BACKEND", "nccl")
+    if "CESS_DEVICE" in os.environ:
+        local = int(os.environ["CESS_DEVICE"])
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -222,7 +230,8 @@ def main() -> None:
 
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if world > 1:
-        t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, launch_ms], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, launch_ms = float(t[0]), float(t[1])
 

@@ -108,17 +108,28 @@ def gather_survivors(plan: GatherPlan, store: FragmentStore, k: int, m: int, ran
     def dst_view(s, f):
         return sd[row[s], f] if f < k else sp[row[s], f - k]
 
-    ops = []
+    # RCCL/NCCL moves HBM buffers directly (xGMI); gloo (CPU tests, rehearsals) needs host
+    # buffers, so device tensors are staged through host memory on that backend.
+    stage = dev.type == "cuda" and dist.is_initialized() and dist.get_backend(group) == "gloo"
+    ops, copies = [], []
     for (s, f), (src, dst) in sorted(plan.moves.items()):
         if src == dst == rank:
             dst_view(s, f).copy_(store.data[store.slots[(s, f)]])
         elif src == rank:
-            ops.append(dist.P2POp(dist.isend, store.data[store.slots[(s, f)]], dst, group))
+            t = store.data[store.slots[(s, f)]]
+            ops.append(dist.P2POp(dist.isend, t.cpu() if stage else t, dst, group))
         elif dst == rank:
-            ops.append(dist.P2POp(dist.irecv, dst_view(s, f), src, group))
+            t = dst_view(s, f)
+            if stage:
+                h = torch.empty(t.shape, dtype=t.dtype)
+                copies.append((t, h))
+                t = h
+            ops.append(dist.P2POp(dist.irecv, t, src, group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
+    for t, h in copies:
+        t.copy_(h)
     if not mysegs:
         return None, None, None, []
     present = np.stack([plan.present[s] for s in mysegs])
