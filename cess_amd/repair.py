@@ -1,0 +1,93 @@
+"""Repair (restoral) service and idle fillers.
+
+Restoral flow on chain (reference c-pallets/file-bank/src/lib.rs):
+  * `generate_restoral_order(file_hash, restoral_fragment)` (:943-984) marks a fragment
+    unavailable (`avail = false`, :971);
+  * a miner claims it (`claim_restoral_order`, :989-1014), rebuilds the fragment off chain from
+    k surviving fragments of the same segment, and
+  * `restoral_order_complete(fragment_hash)` (:1075-1122) marks it available again.
+The off-chain step is what this module does: rebuild one fragment and check that its SHA-256
+hex equals the `FragmentInfo.hash` recorded for it (types.rs:70-76) before reporting.
+
+Idle fillers (`upload_filler`, lib.rs:798-833) are 8 MiB blocks whose content generator is not
+in the reference; here they are the splitmix64 counter stream of libcessec (parity unpinned).
+"""
+from __future__ import annotations
+
+import hashlib
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import geometry
+from .reedsolomon import CecError, Encoder, ErrTooFewShards
+
+
+class ErrFragmentHashMismatch(CecError, ValueError):
+    """rebuilt fragment does not match the recorded fragment hash"""
+
+
+def repair_fragment(enc: Encoder, survivors: Dict[int, np.ndarray], index: int,
+                    expected_hash: Optional[bytes] = None) -> np.ndarray:
+    """Rebuild fragment `index` of one segment from `survivors` ({fragment index: bytes}, at
+    least k of them) on the GPU. With `expected_hash` (64 hex chars), raise
+    ErrFragmentHashMismatch unless SHA-256(rebuilt) equals it."""
+    n = enc.Shards
+    if not 0 <= index < n:
+        raise ValueError("fragment index out of range")
+    if len([i for i in survivors if i != index]) < enc.DataShards:
+        raise ErrTooFewShards(ErrTooFewShards.__doc__)
+    shards: List[Optional[np.ndarray]] = [None] * n
+    for i, b in survivors.items():
+        if i != index:
+            shards[i] = np.ascontiguousarray(b, dtype=np.uint8)
+    if index < enc.DataShards:
+        enc.ReconstructData(shards)
+    else:
+        enc.Reconstruct(shards)
+    out = shards[index]
+    if expected_hash is not None:
+        got = hashlib.sha256(out).hexdigest().encode()
+        if got != bytes(expected_hash):
+            raise ErrFragmentHashMismatch(f"fragment {index}: {got.decode()} != "
+                                          f"{bytes(expected_hash).decode()}")
+    return out
+
+
+def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, present,
+                 expected: Optional[Sequence[Dict[int, bytes]]] = None, stream=None):
+    """Rebuild every missing fragment of an HBM-resident batch in place (one launch for all
+    erasure patterns) and, with `expected` ([{fragment index: recorded hash}] per segment),
+    return per-segment booleans: rebuilt fragments hash to the recorded values (hashed on the
+    host from one D2H copy per fragment, SHA-NI)."""
+    import torch
+    enc.ReconstructBatch(d_data, d_parity, nseg, shard_len, present, stream=stream)
+    if expected is None:
+        return None
+    if stream is None:
+        torch.cuda.current_stream(d_data.device).synchronize()
+    else:
+        stream.synchronize()
+    k = enc.DataShards
+    ok = []
+    for s in range(nseg):
+        good = True
+        for i, h in expected[s].items():
+            t = d_data[s, i] if i < k else d_parity[s, i - k]
+            good &= hashlib.sha256(t.cpu().numpy()).hexdigest().encode() == bytes(h)
+        ok.append(good)
+    return ok
+
+
+def generate_fillers(n: int, seed: int = 0xF111E5, filler_size: int = geometry.FRAGMENT_SIZE,
+                     first: int = 0, device: int = 0):
+    """n idle fillers of `filler_size` bytes generated in HBM (splitmix64 counter stream,
+    filler i = segment first+i of the generator) with their SHA-256 hex hashes (as
+    `upload_filler` records them). Returns (device tensor [n][filler_size], [hash])."""
+    import torch
+    from .reedsolomon import fill_synthetic
+    d = torch.empty((n, filler_size), dtype=torch.uint8, device=torch.device("cuda", device))
+    fill_synthetic(d, filler_size, n, first, seed)
+    torch.cuda.synchronize(device)
+    hashes = [hashlib.sha256(d[i].cpu().numpy()).hexdigest().encode() for i in range(n)]
+    return d, hashes

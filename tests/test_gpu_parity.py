@@ -404,3 +404,52 @@ def test_encode_file_sharded_single_rank(tmp_path, orc):
     assert [(s.hash, s.fragment_list) for s in rec.segments] == orc.segment_list(
         blob, 2, 1, 1 << 20)
     assert rec.file_hash == orc.file_hash(orc.segment_list(blob, 2, 1, 1 << 20))
+
+
+def test_repair_fragment_and_hash_check(cess, corc, orc):
+    """§8f rank 2: restoral — rebuild one fragment from peer survivors, check the recorded hash."""
+    from cess_amd.repair import ErrFragmentHashMismatch, repair_fragment
+    k, m, F = 2, 1, 1 << 20
+    rng = np.random.default_rng(5)
+    data = [rng.integers(0, 256, F, dtype=np.uint8) for _ in range(k)]
+    full = data + c_encode(corc, k, m, data)
+    hashes = [orc.sha256_hex(x) for x in full]
+    enc = cess.New(k, m)
+    for lost in range(3):
+        surv = {i: full[i] for i in range(3) if i != lost}
+        got = repair_fragment(enc, surv, lost, hashes[lost])
+        assert np.array_equal(got, full[lost])
+    bad = {0: full[0], 2: full[2].copy()}
+    bad[2][7] ^= 1
+    with pytest.raises(ErrFragmentHashMismatch):
+        repair_fragment(enc, bad, 1, hashes[1])
+    with pytest.raises(cess.ErrTooFewShards):
+        repair_fragment(enc, {0: full[0]}, 1)
+
+
+def test_repair_batch_wide(torch, cess, corc, orc):
+    from cess_amd.repair import repair_batch
+    k, m, F, nseg = 10, 4, 4096, 5
+    rng = np.random.default_rng(6)
+    data = rng.integers(0, 256, (nseg, k, F), dtype=np.uint8)
+    par = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = np.ones((nseg, k + m), np.uint8)
+    expected = []
+    for s in range(nseg):
+        lost = rng.choice(k + m, size=1 + s % m, replace=False)
+        present[s, lost] = 0
+        expected.append({int(i): orc.sha256_hex(data[s, i] if i < k else par[s, i - k])
+                         for i in lost})
+    dd = to_dev(torch, data * present[:, :k, None])
+    dp = to_dev(torch, par * present[:, k:, None])
+    ok = repair_batch(cess.New(k, m), dd, dp, nseg, F, present, expected)
+    assert ok == [True] * nseg
+
+
+def test_generate_fillers(torch, orc):
+    from cess_amd.repair import generate_fillers
+    d, hashes = generate_fillers(3, filler_size=1 << 16, first=7)
+    for i in range(3):
+        want = orc.synthetic_segment(0xF111E5, 7 + i, 1 << 16)
+        assert np.array_equal(d[i].cpu().numpy(), want)
+        assert hashes[i] == orc.sha256_hex(want)
