@@ -453,3 +453,19 @@ def test_generate_fillers(torch, orc):
         want = orc.synthetic_segment(0xF111E5, 7 + i, 1 << 16)
         assert np.array_equal(d[i].cpu().numpy(), want)
         assert hashes[i] == orc.sha256_hex(want)
+
+
+def test_c_abi_consumer(tmp_path):
+    """A plain C program against include/cess_ec.h (no Python): encode, verify, every single
+    erasure rebuilt, error codes — what a cgo/FFI binding exercises."""
+    import subprocess
+    from tests.conftest import ROOT
+    exe = tmp_path / "cabi_roundtrip"
+    lib = f"{ROOT}/cess_amd"
+    orc = f"{ROOT}/oracle/build"
+    subprocess.run(["gcc", "-O2", f"{ROOT}/tests/native/cabi_roundtrip.c", f"-I{ROOT}/include",
+                    f"-L{lib}", "-lcessec", f"-L{orc}", "-loracle",
+                    f"-Wl,-rpath,{lib}:{orc}", "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "cabi roundtrip ok" in r.stdout
