@@ -342,7 +342,7 @@ int cec_set_option(cec_codec* c, int option, int value) {
       c->force_generic = value != 0;
       return CEC_OK;
     case CEC_OPT_CT_VARIANT:
-      if (value < -1 || value > 15) return set_err(CEC_EINVAL, "variant out of range");
+      if (value < -1 || value > 31) return set_err(CEC_EINVAL, "variant out of range");
       cec::set_ct_variant(value);
       return CEC_OK;
   }

@@ -343,6 +343,135 @@ __device__ __forceinline__ void ct_column_window(LD ld, ST st) {
   static_for<P::NO>([&](auto O) CEC_AI { st(O, acc[O]); });
 }
 
+// ---------------------------------------------------------------------------------------------
+// Horner form over input groups (wide codes)
+// ---------------------------------------------------------------------------------------------
+// gfx950 dual-issues only some VALU ops at the SIMD-32 rate (tools/valu_bench.hip, r01 sweep):
+// v_add/v_sub/v_and/v_or/v_xor/v_bitop3/v_lshrrev_b32 run at 2 cycles per wave64 instruction,
+// while v_lshlrev_b32, v_perm, v_alignbit, v_add3 and every other 3-source integer op take 4.
+// xt_fast is 2*x on four packed bytes from full-rate ops only (6 ops, 6 "slots" vs 8 for xt):
+// t = sign bits, v = t - (t >> 7) = 0x7F in each byte whose top bit is set, a = x without the
+// sign bits, result = (a + a) ^ (v & 0x1D1D1D1D). a + a is written as v_add_u32 in asm:
+// LLVM would turn it into a left shift, which is a half-rate instruction here.
+__device__ __forceinline__ uint32_t add_self(uint32_t a) {
+  uint32_t r;
+  asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+__device__ __forceinline__ uint32_t xt_fast(uint32_t x) {
+  const uint32_t t = x & 0x80808080u;
+  const uint32_t v = t - (t >> 7);
+  return __builtin_amdgcn_bitop3_b32(add_self(x ^ t), v, 0x1d1d1d1du, 0x78);  // a ^ (b & c)
+}
+
+// Same value without inline asm: the second addend is an opaque copy of a (one more full-rate
+// op) so LLVM cannot fold a + a into a shift; the asm form instead costs a hazard s_nop.
+__device__ __forceinline__ uint32_t xt_fast2(uint32_t x) {
+  const uint32_t t = x & 0x80808080u;
+  const uint32_t v = t - (t >> 7);
+  const uint32_t a2 = __builtin_amdgcn_bitop3_b32(x, t, 0u, 0x3C);  // x ^ t
+  return __builtin_amdgcn_bitop3_b32((x ^ t) + a2, v, 0x1d1d1d1du, 0x78);
+}
+
+// Output row o of a wide code is evaluated by Horner's rule over coefficient bits,
+//   y = 2*y ^ S_b,   S_b = XOR of x_j over inputs j whose coefficient c[o][j] has bit b set,
+// with S_b read from per-group tables: inputs are split into groups of G = 4 and every XOR
+// combination of a group's inputs (up to 15 values, only those some (o, b) uses) is built once
+// per column. Per (output, bit): one xtime (6 full-rate ops) + one v_bitop3 per two groups.
+// Against the nibble-window form this moves the 7 xtimes per INPUT to 7 per OUTPUT and shrinks
+// the per-input tables from 22 XORs + 7 xtimes to ~2.75 XORs (11 per group of 4).
+template <class P, int G>
+struct HGroup {
+  static constexpr int NG = (P::NI + G - 1) / G;
+  static constexpr int gsize(int g) { return g * G + G <= P::NI ? G : P::NI - g * G; }
+  // combination index of group g for output o, bit b
+  static constexpr unsigned idx(int o, int b, int g) {
+    unsigned r = 0;
+    for (int i = 0; i < gsize(g); ++i) r |= (unsigned)((P::v.c[o][g * G + i] >> b) & 1) << i;
+    return r;
+  }
+  // combinations group g needs (used ones + the ones they are built from)
+  static constexpr unsigned need(int g) {
+    unsigned u = 0;
+    for (int o = 0; o < P::NO; ++o)
+      for (int b = 0; b < 8; ++b) u |= 1u << idx(o, b, g);
+    u &= ~1u;
+    for (int v = (1 << G) - 1; v >= 1; --v)
+      if ((u >> v & 1) && (v & (v - 1))) u |= 1u << (v & (v - 1));
+    return u;
+  }
+  struct Terms {
+    int n;
+    int g[NG];
+    int v[NG];
+  };
+  static constexpr Terms terms(int o, int b) {
+    Terms t{};
+    for (int g = 0; g < NG; ++g) {
+      const unsigned v = idx(o, b, g);
+      if (v) { t.g[t.n] = g; t.v[t.n] = (int)v; ++t.n; }
+    }
+    return t;
+  }
+};
+
+constexpr int ctz_c(unsigned v) {
+  int b = 0;
+  while (!(v >> b & 1)) ++b;
+  return b;
+}
+
+// FL bit 1: xt_fast2 instead of xt_fast; bit 2: scheduling barrier between output rows.
+template <class P, int G, int FL, class LD, class ST>
+__device__ __forceinline__ void ct_column_hgroup(LD ld, ST st) {
+  using H = HGroup<P, G>;
+  uint32_t comb[H::NG][1 << G];
+  static_for<H::NG>([&](auto Gi) CEC_AI {
+    constexpr int g = Gi;
+    constexpr unsigned need = H::need(g);
+    static_for<(1 << G)>([&](auto V) CEC_AI {
+      constexpr int v = V;
+      if constexpr (v > 0 && (need >> v & 1)) {
+        constexpr int bit = ctz_c(v);
+        if constexpr ((v & (v - 1)) == 0) comb[g][v] = ld(std::integral_constant<int, g * G + bit>{});
+        else comb[g][v] = xor2(comb[g][v & (v - 1)], comb[g][1 << bit]);
+      }
+    });
+  });
+  static_for<P::NO>([&](auto O) CEC_AI {
+    constexpr int o = O;
+    constexpr int top = P::v.hb_row[o];
+    uint32_t y = 0;
+    static_for<8>([&](auto B) CEC_AI {
+      constexpr int b = 7 - B;
+      if constexpr (b <= top) {
+        constexpr typename H::Terms tl = H::terms(o, b);
+        if constexpr (b == top) {
+          // first bit: y = XOR of the terms (the top bit of row o has at least one)
+          if constexpr (tl.n >= 3)
+            y = xor3(comb[tl.g[0]][tl.v[0]], comb[tl.g[1]][tl.v[1]], comb[tl.g[2]][tl.v[2]]);
+          else if constexpr (tl.n == 2)
+            y = xor2(comb[tl.g[0]][tl.v[0]], comb[tl.g[1]][tl.v[1]]);
+          else
+            y = comb[tl.g[0]][tl.v[0]];
+        } else {
+          if constexpr (FL & 2) y = xt_fast2(y);
+          else y = xt_fast(y);
+        }
+        constexpr int s0 = b == top ? (tl.n >= 3 ? 3 : tl.n) : 0;
+        static_for<(tl.n - s0 + 1) / 2>([&](auto Q) CEC_AI {
+          constexpr int i = s0 + 2 * Q;
+          if constexpr (i + 1 < tl.n)
+            y = xor3(y, comb[tl.g[i]][tl.v[i]], comb[tl.g[i + 1]][tl.v[i + 1]]);
+          else
+            y = xor2(y, comb[tl.g[i]][tl.v[i]]);
+        });
+      }
+    });
+    st(O, y);
+  });
+}
+
 // Byte-wise finish of the last (len % 16) bytes, run by the last block of each segment.
 template <class P, int VB>
 __device__ __forceinline__ void ct_tail(const Layout& L, uint32_t seg) {
@@ -357,6 +486,29 @@ __device__ __forceinline__ void ct_tail(const Layout& L, uint32_t seg) {
   };
   if constexpr (use_horner<P>(1)) ct_column_horner<P, uint32_t>(ld, st);
   else ct_column_stream<P, 1, uint32_t>(ld, st);
+}
+
+// One 4-byte column of every shard per lane; shard addresses are a uniform 64-bit base plus
+// a 32-bit lane offset (global_load/store with an SGPR base: no per-access VALU address math).
+// The host checks len < 2^32.
+// FL bit 0: nontemporal loads and stores (other bits: ct_column_hgroup).
+template <class P, int G, int FL = 0, int BS = 256>
+__global__ __launch_bounds__(BS) void k_hg(Layout L, const uint32_t* __restrict__ seg_list,
+                                           uint32_t seg0) {
+  const uint32_t seg = seg_list ? seg_list[seg0 + blockIdx.y] : seg0 + blockIdx.y;
+  const uint32_t nvec = (uint32_t)(L.len / 4);
+  const uint32_t v = blockIdx.x * BS + threadIdx.x;
+  if (v < nvec) {
+    const uint32_t off = v * 4;
+    auto ld = [&](auto J) CEC_AI -> uint32_t {
+      return ld16<(FL & 1) != 0, uint32_t>(shard_ptr_ct<P::K, P::v.in[J]>(L, seg) + off);
+    };
+    auto st = [&](auto O, uint32_t y) CEC_AI {
+      st16<(FL & 1) != 0, uint32_t>(shard_ptr_ct<P::K, P::v.out[O]>(L, seg) + off, y);
+    };
+    ct_column_hgroup<P, G, FL>(ld, st);
+  }
+  if ((L.len % 4) && blockIdx.x == gridDim.x - 1) ct_tail<P, 4>(L, seg);
 }
 
 template <class P, int U, bool NT, class TV = u32x4, int PF = 1, bool WIN = false, int BS = 256>
@@ -771,7 +923,26 @@ void run_ct_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hi
   }
 }
 
-// Wide codes (streaming form): per-lane width and prefetch depth.
+// Horner-over-groups kernel; needs 4-byte-aligned shards and 32-bit lane offsets (else the
+// nibble-window kernel).
+template <class P, int G, int FL, int BS = 256>
+void run_hg(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  const uintptr_t bits = (uintptr_t)L.data | (uintptr_t)L.parity | L.shard_stride |
+                         L.data_seg_stride | L.par_seg_stride;
+  if ((bits & 3) || L.len >= (1ull << 32)) {
+    run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st);
+    return;
+  }
+  uint64_t gx = (L.len / 4 + BS - 1) / BS;
+  if (gx == 0) gx = 1;
+  for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {
+    hipLaunchKernelGGL((k_hg<P, G, FL, BS>), dim3((unsigned)gx, ny), dim3(BS), 0, st, L,
+                       seg_list, s0);
+  });
+}
+
+// Wide codes: nibble-window / streaming forms (per-lane width, prefetch depth) and the Horner
+// form over input groups.
 template <class P>
 void run_wide_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
   switch (g_ct_variant) {
@@ -785,7 +956,14 @@ void run_wide_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, 
     case 7: run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st); break;
     case 8: run_ct<P, 1, false, u32x2, 4, true>(L, seg_list, nseg, st); break;
     case 9: run_ct<P, 1, false, u32x4, 2, true>(L, seg_list, nseg, st); break;
-    default: run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st); break;  // r01 sweep
+    case 11: run_hg<P, 3, 0>(L, seg_list, nseg, st); break;
+    case 12: run_hg<P, 4, 1>(L, seg_list, nseg, st); break;
+    case 13: run_hg<P, 4, 2>(L, seg_list, nseg, st); break;
+    case 14: run_hg<P, 4, 4>(L, seg_list, nseg, st); break;
+    case 15: run_hg<P, 4, 0, 128>(L, seg_list, nseg, st); break;
+    case 16: run_hg<P, 4, 0, 512>(L, seg_list, nseg, st); break;
+    case 10: run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st); break;  // r01 default
+    default: run_hg<P, 4, 0>(L, seg_list, nseg, st); break;  // r01 sweep: 3.11 -> 5.26 TB/s
   }
 }
 

@@ -151,14 +151,16 @@ def test_reconstruct_batch_per_segment(torch, cess, corc, k, m, ln, nseg, generi
     assert np.array_equal(d_par.cpu().numpy(), par * present[:, k:, None])
 
 
-def test_ct_variants_identical(torch, cess, corc):
-    k, m, ln, nseg = 2, 1, (1 << 16) + 48, 4
+@pytest.mark.parametrize("k,m,ln", [(2, 1, (1 << 16) + 48), (32, 32, (1 << 14) + 4),
+                                    (32, 32, 3000 * 4 + 7), (32, 32, 5)])
+def test_ct_variants_identical(torch, cess, corc, k, m, ln):
+    nseg = 4
     rng = np.random.default_rng(7)
     data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
     want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
     d_data = to_dev(torch, data)
     enc = cess.New(k, m)
-    for v in range(-1, 12):
+    for v in range(-1, 17):
         enc.set_option(2, v)
         d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
         enc.EncodeBatch(d_data, d_par, nseg, ln)
