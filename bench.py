@@ -38,7 +38,8 @@ CONFIGS = {
     2: (2, 1, 8 * MiB, 64, "batched RS(2,1) encode of 1 GiB of 16 MiB segments per GPU"),
     3: (2, 1, 8 * MiB, 64, "degraded reconstruct RS(2,1), erased fragment = seg mod 3, 1 GiB"),
     4: (2, 1, 8 * MiB, 4096, "64 GiB file (4096 x 16 MiB segments) encoded, sharded over GPUs"),
-    5: (32, 32, 512 * 1024, 64, "RS(32,32) encode of 1 GiB + SHA-256 of all 64 fragments"),
+    5: (32, 32, 512 * 1024, 64, "RS(32,32) encode of 1 GiB + SHA-256 of all 64 fragments "
+                                "(encode and hash pipelined over steps)"),
     # stress variant of config 3 for the wide code (not a BASELINE config): every segment loses
     # m random fragments; decode matrices are run-time (host-inverted per pattern)
     6: (32, 32, 512 * 1024, 64, "RS(32,32) degraded reconstruct, 32 random erasures/segment"),
@@ -95,14 +96,18 @@ def cpu_baseline(k: int, m: int, F: int, target_s: float) -> dict:
     }
 
 
-def load_traffic(tag: str):
-    """Per-launch HBM bytes from the PMC pass (profiles/traffic_<tag>.json), if collected."""
+def load_traffic(tag: str, algo_bytes: int, kernel: str):
+    """Per-launch HBM bytes from the PMC passes (profiles/traffic_<tag>.json), if they were
+    collected for this kernel at this launch size; None otherwise."""
     path = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
     try:
         with open(path) as f:
-            return json.load(f).get("bytes_per_launch")
+            t = json.load(f)
     except (OSError, ValueError):
         return None
+    if t.get("algorithmic_bytes_per_launch") != algo_bytes or t.get("kernel") not in kernel:
+        return None
+    return t.get("bytes_per_launch")
 
 
 def main() -> None:
@@ -113,6 +118,10 @@ def main() -> None:
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--variant", type=int, default=-1, help="CT kernel variant (tuning)")
     ap.add_argument("--generic", action="store_true", help="force run-time-coefficient kernel")
+    ap.add_argument("--segments", type=int, default=0,
+                    help="segments per GPU (default: the config's; config 5 at 1024 = 16 GiB in "
+                         "flight, enough fragments to give every SIMD a SHA-256 wave)")
+    ap.add_argument("--sha-mode", type=int, default=0, help="0 auto, 1 one wave, 2 two waves")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
@@ -143,6 +152,9 @@ def main() -> None:
     torch.cuda.set_device(dev)
 
     k, m, F, nseg_cfg, desc = CONFIGS[args.config]
+    if args.segments:
+        nseg_cfg = args.segments
+        desc = f"{desc} [{args.segments} segments per GPU = {args.segments * k * F / 2**30:g} GiB]"
     nseg = nseg_cfg // world if args.config == 4 else nseg_cfg
     seg0 = rank * nseg
     stream = torch.cuda.current_stream(dev)
@@ -154,6 +166,7 @@ def main() -> None:
     if args.generic:
         enc.set_option(1, 1)
     enc.set_option(2, args.variant)
+    enc.set_option(3, args.sha_mode)
     enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)  # valid parity for config 3
 
     present = None
@@ -167,15 +180,32 @@ def main() -> None:
             present[s_, rng.choice(k + m, size=m, replace=False)] = 0
     d_hex = None
     if args.config == 5:
+        # Two-stage pipeline over steps: step i encodes into parity buffer i % 2 on the launch
+        # stream, then hashes every fragment of that segment batch on a second stream, so the
+        # hash of step i overlaps the encode of step i + 1 (the data batch is read-only and
+        # shared; parity and hex output are double-buffered).
         d_hex = torch.empty((nseg, k + m, 64), dtype=torch.uint8, device=dev)
+        pipe_par = [d_par, torch.empty_like(d_par)]
+        pipe_hex = [d_hex, torch.empty_like(d_hex)]
+        sha_stream = torch.cuda.Stream(dev)
+        ev_enc = [torch.cuda.Event(), torch.cuda.Event()]
+        ev_sha = [torch.cuda.Event(), torch.cuda.Event()]
+        pipe_i = [0]
 
     def step():
         if args.config in (3, 6):
             enc.ReconstructBatch(d_data, d_par, nseg, F, present, stream=stream)
+        elif args.config == 5:
+            b = pipe_i[0] % 2
+            pipe_i[0] += 1
+            stream.wait_event(ev_sha[b])  # parity buffer b no longer being hashed
+            enc.EncodeBatch(d_data, pipe_par[b], nseg, F, stream=stream)
+            ev_enc[b].record(stream)
+            sha_stream.wait_event(ev_enc[b])
+            enc.Sha256Batch(d_data, pipe_par[b], nseg, F, pipe_hex[b], stream=sha_stream)
+            ev_sha[b].record(sha_stream)
         else:
             enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
-            if d_hex is not None:
-                enc.Sha256Batch(d_data, d_par, nseg, F, d_hex, stream=stream)
 
     def step_codec():  # the codec kernel alone (config 5's step also hashes)
         if args.config in (3, 6):
@@ -254,18 +284,20 @@ def main() -> None:
         enc_ms = timed(lambda: enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream), 20)
         sha_ms = timed(lambda: enc.Sha256Batch(d_data, d_par, nseg, F, d_hex, stream=stream), 3)
         achieved = bytes_step_gpu / (enc_ms * 1e-3) / GB
+        launch_ms = enc_ms  # the step's events also hold the pipeline's wait on the hash stream
         sha_note = {"sha256_ms": round(sha_ms, 3), "encode_ms": round(enc_ms, 4),
                     "sha256_GBps": round(bytes_step_gpu / (sha_ms * 1e-3) / GB, 2),
-                    "streams": nseg * (k + m),
+                    "streams": nseg * (k + m), "sha_mode": args.sha_mode,
+                    "pipeline": "hash of step i on a second stream overlaps encode of step i+1",
                     "note": "SHA-256 is one sequential chain per fragment: bounded by streams x "
-                            "per-lane issue rate, reported apart from the HBM roofline"}
+                            "per-wave issue rate, reported apart from the HBM roofline"}
 
     tag = f"c{args.config}"
-    traffic = load_traffic(tag)
-    kernel_name = {2: "k_ct<EncCT<2,1>>", 3: "k_ct<Dec1CT<2,1,*>> / k_ct<EncCT<2,1>>",
-                   4: "k_ct<EncCT<2,1>>", 5: "k_ct<EncCT<32,32>>", 6: "k_rt<32,1>"}[args.config]
+    kernel_name = {2: "k_ct<EncCT<2, 1>>", 3: "k_ct<Dec1CT<2, 1, *>> / k_ct<EncCT<2, 1>>",
+                   4: "k_ct<EncCT<2, 1>>", 5: "k_hg<EncCT<32, 32>, 4>", 6: "k_rt<32, 1>"}[args.config]
     if args.generic:
         kernel_name = "k_rt"
+    traffic = load_traffic(tag, bytes_step_gpu, kernel_name)
     out = {
         "metric": METRIC,
         "value": round(value, 2),

@@ -20,6 +20,7 @@
 
 namespace cec {
 void set_ct_variant(int v);
+void set_sha_mode(int v);
 }
 
 namespace {
@@ -344,6 +345,10 @@ int cec_set_option(cec_codec* c, int option, int value) {
     case CEC_OPT_CT_VARIANT:
       if (value < -1 || value > 31) return set_err(CEC_EINVAL, "variant out of range");
       cec::set_ct_variant(value);
+      return CEC_OK;
+    case CEC_OPT_SHA_MODE:
+      if (value < 0 || value > 2) return set_err(CEC_EINVAL, "sha mode out of range");
+      cec::set_sha_mode(value);
       return CEC_OK;
   }
   return set_err(CEC_EINVAL, "unknown option");

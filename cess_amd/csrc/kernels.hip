@@ -829,6 +829,160 @@ __global__ __launch_bounds__(64) void k_sha256(const uint8_t* const* __restrict_
   }
 }
 
+// Two waves per group of 64 buffers. Each buffer's hash is one serial chain, so with few
+// buffers (a 1 GiB RS(32,32) batch is 4096 fragments = 64 waves on a 1024-SIMD chip) the time
+// is the per-block instruction count of ONE wave. The message schedule does not depend on the
+// chaining state, so wave 0 (producer) loads block i+1, byte-swaps it and expands W[0..63] + K
+// into LDS while wave 1 (consumer) runs the 64 rounds of block i: the consumer's chain drops from
+// ~1460 to ~900 VALU instructions per block. LDS ring: 2 buffers x 64 words x 64 lanes (32 KiB),
+// [buf][word/4][lane][4] so every ds_write/read_b128 covers 1 KiB contiguous. One barrier per
+// block; the padding block(s) go through the same pipeline.
+__device__ __forceinline__ const uint8_t* sha_src(const uint8_t* const* ptrs, const Layout& L,
+                                                  int nshards, uint64_t i) {
+  return ptrs ? ptrs[i] : shard_ptr(L, (int)(i % nshards), (uint32_t)(i / nshards));
+}
+
+__device__ __forceinline__ void sha_expand_store(uint32_t (&w)[16], u32x4* __restrict__ dst) {
+  // dst[q * 64] = {W+K}[4q .. 4q+3] for this lane
+#pragma unroll
+  for (int t = 0; t < 64; t += 4) {
+    uint32_t o[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int u = t + s;
+      uint32_t wt;
+      if (u < 16) {
+        wt = w[u];
+      } else {
+        const uint32_t w15 = w[(u + 1) & 15], w2 = w[(u + 14) & 15];
+        const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+        const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+        wt = w[u & 15] + s0 + w[(u + 9) & 15] + s1;
+        w[u & 15] = wt;
+      }
+      o[s] = wt + kSha256K[u];
+    }
+    dst[(t / 4) * 64] = u32x4{o[0], o[1], o[2], o[3]};
+  }
+}
+
+__global__ __launch_bounds__(128) void k_sha256_2w(const uint8_t* const* __restrict__ ptrs,
+                                                   Layout L, int nshards, uint64_t n,
+                                                   uint64_t len, uint8_t* __restrict__ hex_out) {
+  __shared__ u32x4 ring[2][16][64];
+  const int lane = threadIdx.x & 63;
+  // wave-uniform by construction (SGPR), so the two sides' barriers never run under one EXEC mask
+  const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  const uint64_t i = (uint64_t)blockIdx.x * 64 + lane;
+  const bool live = i < n;
+  const uint64_t nfull = len >> 6;
+  const uint32_t r = (uint32_t)(len & 63);
+  const uint64_t nb = nfull + (r >= 56 ? 2 : 1);  // blocks including padding
+  if (producer) {
+    const uint8_t* src = live ? sha_src(ptrs, L, nshards, i) : nullptr;
+    const bool al16 = live && ((uintptr_t)src & 15) == 0;
+    u32x4 nx[4] = {};
+    if (al16 && nfull) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(src + 16 * q);
+    }
+    for (uint64_t blk = 0; blk < nb; ++blk) {
+      uint32_t w[16];
+      if (blk < nfull) {
+        if (al16) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            w[4 * q + 0] = __builtin_bswap32(nx[q].x);
+            w[4 * q + 1] = __builtin_bswap32(nx[q].y);
+            w[4 * q + 2] = __builtin_bswap32(nx[q].z);
+            w[4 * q + 3] = __builtin_bswap32(nx[q].w);
+          }
+          if (blk + 1 < nfull) {
+            const uint8_t* p = src + ((blk + 1) << 6);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+          }
+        } else if (live) {
+          const uint8_t* p = src + (blk << 6);
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            w[q] = (uint32_t)p[4 * q] << 24 | (uint32_t)p[4 * q + 1] << 16 |
+                   (uint32_t)p[4 * q + 2] << 8 | (uint32_t)p[4 * q + 3];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) w[q] = 0;
+        }
+      } else {
+        // padding block(s): remaining r bytes, 0x80, zeros, 64-bit big-endian bit length
+        const bool first_pad = blk == nfull;
+        const uint8_t* p = live ? src + (nfull << 6) : nullptr;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          uint32_t word = 0;
+          if (first_pad) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const uint32_t pos = 4 * q + s;
+              const uint32_t byte = pos < r ? (live ? p[pos] : 0u) : (pos == r ? 0x80u : 0u);
+              word |= byte << (24 - 8 * s);
+            }
+          }
+          w[q] = word;
+        }
+        if (blk == nb - 1) {
+          const uint64_t bits = len << 3;
+          w[14] = (uint32_t)(bits >> 32);
+          w[15] = (uint32_t)bits;
+        }
+      }
+      sha_expand_store(w, &ring[blk & 1][0][lane]);
+      __syncthreads();
+    }
+    __syncthreads();  // matches the consumer's final iteration
+  } else {
+    uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                     0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    __syncthreads();  // block 0 produced
+    for (uint64_t blk = 0; blk < nb; ++blk) {
+      const u32x4* src = &ring[blk & 1][0][lane];
+      uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const u32x4 kw4 = src[q * 64];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const uint32_t kw = s == 0 ? kw4.x : s == 1 ? kw4.y : s == 2 ? kw4.z : kw4.w;
+          const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+          const uint32_t t1 = hh + S1 + ch(e, f, g) + kw;
+          const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+          const uint32_t t2 = S0 + maj(a, b, c);
+          hh = g; g = f; f = e; e = d + t1;
+          d = c; c = b; b = a; a = t1 + t2;
+        }
+      }
+      h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+      __syncthreads();  // this buffer consumed / next one produced
+    }
+    if (live) {
+      uint8_t* o = hex_out + i * 64;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        uint32_t word = h[q];
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const uint32_t nib = (word >> (28 - 4 * s)) & 15u;
+          const uint32_t chr = nib < 10 ? '0' + nib : 'a' + nib - 10;
+          if (s < 4) lo |= chr << (8 * s);
+          else hi |= chr << (8 * (s - 4));
+        }
+        *reinterpret_cast<uint32_t*>(o + 8 * q) = lo;
+        *reinterpret_cast<uint32_t*>(o + 8 * q + 4) = hi;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Synthetic segments
 // ---------------------------------------------------------------------------------------------
@@ -1033,13 +1187,25 @@ void launch_matvec_rt(const Layout& L, const uint32_t* chunk, const uint32_t* co
   }
 }
 
+namespace {
+int g_sha_mode = 0;  // 0 auto, 1 one wave, 2 two waves per 64 buffers
+}
+void set_sha_mode(int v) { g_sha_mode = v; }
+
 void launch_sha256_hex(const uint8_t* const* ptrs, const Layout* L, int nshards, uint64_t n,
                        uint64_t len, uint8_t* hex_out, hipStream_t st) {
   if (n == 0) return;
   Layout dummy{};
   const unsigned g = (unsigned)((n + 63) / 64);
-  hipLaunchKernelGGL(k_sha256, dim3(g), dim3(64), 0, st, ptrs, L ? *L : dummy, nshards, n, len,
-                     hex_out);
+  // Two waves per group while the groups leave SIMDs idle (latency regime: one serial chain
+  // per buffer); one wave per group once 2 * groups would exceed the chip's 1024 SIMDs.
+  const bool two = g_sha_mode == 2 || (g_sha_mode == 0 && g <= 512);
+  if (two)
+    hipLaunchKernelGGL(k_sha256_2w, dim3(g), dim3(128), 0, st, ptrs, L ? *L : dummy, nshards, n,
+                       len, hex_out);
+  else
+    hipLaunchKernelGGL(k_sha256, dim3(g), dim3(64), 0, st, ptrs, L ? *L : dummy, nshards, n, len,
+                       hex_out);
 }
 
 void launch_fill_splitmix(uint8_t* out, uint64_t seg_bytes, uint64_t nseg, uint64_t seg0,

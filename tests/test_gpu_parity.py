@@ -247,7 +247,16 @@ def test_full_geometry_rs3232(torch, cess, corc):
     assert torch.equal(d_data, ref_d) and torch.equal(d_par, ref_p)
 
 
-def test_sha256_shavs_on_gpu(torch, cess):
+@pytest.fixture(params=[1, 2], ids=["sha1wave", "sha2wave"])
+def sha_mode(request, cess):
+    """Run a SHA-256 test with each kernel form (CEC_OPT_SHA_MODE), then restore auto."""
+    enc = cess.New(2, 1)
+    enc.set_option(3, request.param)
+    yield request.param
+    enc.set_option(3, 0)
+
+
+def test_sha256_shavs_on_gpu(torch, cess, sha_mode):
     vecs = parse_shavs("SHA256ShortMsg.rsp") + parse_shavs("SHA256LongMsg.rsp")
     bufs = [torch.from_numpy(np.frombuffer(msg, np.uint8).copy() if msg else
                              np.zeros(1, np.uint8)).cuda() for msg, _ in vecs]
@@ -256,7 +265,20 @@ def test_sha256_shavs_on_gpu(torch, cess):
         assert got.decode() == md, len(msg)
 
 
-def test_sha256_batch_matches_hashlib(torch, cess):
+@pytest.mark.parametrize("length", [0, 1, 55, 56, 63, 64, 119, 120, 1000, 4096 + 17])
+def test_sha256_many_unaligned(torch, cess, sha_mode, length):
+    """130 buffers (three 64-lane groups, the last partial) at odd and 16-byte-aligned starts."""
+    n = 130
+    rng = np.random.default_rng(length)
+    pool = rng.integers(0, 256, n * (length + 32), dtype=np.uint8)
+    d_pool = torch.from_numpy(pool).cuda()
+    offs = [j * (length + 32) + (j % 5) * 3 for j in range(n)]
+    got = cess.sha256_hex_device([d_pool.data_ptr() + o for o in offs], length)
+    for j, o in enumerate(offs):
+        assert got[j].decode() == sha(pool[o:o + length]), j
+
+
+def test_sha256_batch_matches_hashlib(torch, cess, sha_mode):
     for (k, m, F, nseg) in [(2, 1, 4096 + 7, 3), (32, 32, 65536, 2), (2, 1, 1 << 20, 4)]:
         rng = np.random.default_rng(F)
         data = rng.integers(0, 256, (nseg, k, F), dtype=np.uint8)
