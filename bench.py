@@ -43,6 +43,10 @@ CONFIGS = {
     # stress variant of config 3 for the wide code (not a BASELINE config): every segment loses
     # m random fragments; decode matrices are run-time (host-inverted per pattern)
     6: (32, 32, 512 * 1024, 64, "RS(32,32) degraded reconstruct, 32 random erasures/segment"),
+    # single-fragment repair of the wide code (the restoral case: one lost fragment per segment)
+    7: (32, 32, 512 * 1024, 64, "RS(32,32) repair of one random fragment per segment, 1 GiB"),
+    # a common general-purpose code with no compile-time kernel: run-time coefficients
+    8: (10, 4, 2 * MiB, 64, "RS(10,4) encode (run-time coefficients), 1.25 GiB of 20 MiB segments"),
 }
 
 
@@ -122,6 +126,8 @@ def main() -> None:
                     help="segments per GPU (default: the config's; config 5 at 1024 = 16 GiB in "
                          "flight, enough fragments to give every SIMD a SHA-256 wave)")
     ap.add_argument("--sha-mode", type=int, default=0, help="0 auto, 1 one wave, 2 two waves")
+    ap.add_argument("--rt-mode", type=int, default=0,
+                    help="run-time kernel: 0 Horner over input groups (k <= 32), 1 per-bit masks")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
@@ -167,17 +173,19 @@ def main() -> None:
         enc.set_option(1, 1)
     enc.set_option(2, args.variant)
     enc.set_option(3, args.sha_mode)
+    enc.set_option(4, args.rt_mode)
     enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)  # valid parity for config 3
 
     present = None
     if args.config == 3:
         present = np.ones((nseg, k + m), np.uint8)
         present[np.arange(nseg), (seg0 + np.arange(nseg)) % (k + m)] = 0
-    elif args.config == 6:
-        rng = np.random.default_rng(seg0 + 6)
+    elif args.config in (6, 7):
+        rng = np.random.default_rng(seg0 + args.config)
         present = np.ones((nseg, k + m), np.uint8)
+        ne = m if args.config == 6 else 1
         for s_ in range(nseg):
-            present[s_, rng.choice(k + m, size=m, replace=False)] = 0
+            present[s_, rng.choice(k + m, size=ne, replace=False)] = 0
     d_hex = None
     if args.config == 5:
         # Two-stage pipeline over steps: step i encodes into parity buffer i % 2 on the launch
@@ -193,7 +201,7 @@ def main() -> None:
         pipe_i = [0]
 
     def step():
-        if args.config in (3, 6):
+        if args.config in (3, 6, 7):
             enc.ReconstructBatch(d_data, d_par, nseg, F, present, stream=stream)
         elif args.config == 5:
             b = pipe_i[0] % 2
@@ -208,7 +216,7 @@ def main() -> None:
             enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
 
     def step_codec():  # the codec kernel alone (config 5's step also hashes)
-        if args.config in (3, 6):
+        if args.config in (3, 6, 7):
             enc.ReconstructBatch(d_data, d_par, nseg, F, present, stream=stream)
         else:
             enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
@@ -230,7 +238,7 @@ def main() -> None:
                 b.record(stream)
                 torch.cuda.synchronize(dev)
                 times[v].append(a.elapsed_time(b) / 2)
-        per_seg = (k + m) * F
+        per_seg = (k + (1 if args.config == 7 else m)) * F
         for v in variants:
             med = float(np.median(times[v]))
             print(json.dumps({"config": args.config, "variant": v, "median_ms": round(med, 4),
@@ -265,7 +273,9 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, launch_ms = float(t[0]), float(t[1])
 
-    per_seg = (k + m) * F  # algorithmic bytes per segment (read k*F, write m*F)
+    # algorithmic bytes per segment: read k*F, write m*F (encode) or one erased fragment each
+    # (config 7 repairs one fragment: (k+1)*F)
+    per_seg = (k + (1 if args.config == 7 else m)) * F
     bytes_step_gpu = nseg * per_seg
     value = world * bytes_step_gpu * args.steps / elapsed / GB
     achieved = bytes_step_gpu / (launch_ms * 1e-3) / GB
@@ -294,8 +304,11 @@ def main() -> None:
 
     tag = f"c{args.config}"
     kernel_name = {2: "k_ct<EncCT<2, 1>>", 3: "k_ct<Dec1CT<2, 1, *>> / k_ct<EncCT<2, 1>>",
-                   4: "k_ct<EncCT<2, 1>>", 5: "k_hg<EncCT<32, 32>, 4>", 6: "k_rt<32, 1>"}[args.config]
+                   4: "k_ct<EncCT<2, 1>>", 5: "k_hg<EncCT<32, 32>, 4>", 6: "k_rth<8>", 7: "k_rth<8>",
+                   8: "k_rth<3>"}[args.config]
     if args.generic:
+        kernel_name = "k_rth" if k <= 32 else "k_rt"
+    if args.rt_mode == 1 and (args.generic or args.config in (6, 7, 8)):
         kernel_name = "k_rt"
     traffic = load_traffic(tag, bytes_step_gpu, kernel_name)
     out = {

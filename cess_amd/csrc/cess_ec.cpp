@@ -21,6 +21,7 @@
 namespace cec {
 void set_ct_variant(int v);
 void set_sha_mode(int v);
+void set_rt_mode(int v);
 }
 
 namespace {
@@ -98,6 +99,24 @@ int build_program(const uint8_t* in_idx, int nin, const uint8_t* out_idx, int no
       }
       hb[j] = (uint32_t)top;
     }
+    if (nin <= cec::kRthMaxIn) {
+      // Horner section (kernels.h): per output row, its top bit and per (bit, group) the
+      // combination index of the group's inputs whose coefficient has that bit
+      const size_t hoff = cec::kRtHeaderWords + (size_t)nin * 8 * c.nob;
+      h[3] = (uint32_t)hoff;
+      uint32_t* top = h.data() + hoff;
+      uint32_t* ix = top + 32;
+      for (int o = 0; o < c.nout; ++o) {
+        int t = -1;
+        for (int j = 0; j < nin; ++j)
+          for (int b = 0; b < 8; ++b)
+            if (coef.v[o0 + o][j] >> b & 1) t = std::max(t, b);
+        top[o] = (uint32_t)t;
+        for (int b = 0; b < 8; ++b)
+          for (int j = 0; j < nin; ++j)
+            if (coef.v[o0 + o][j] >> b & 1) ix[((size_t)o * 8 + b) * 8 + j / 4] |= 1u << (j % 4);
+      }
+    }
     HIP_TRY(hipMalloc(&c.dev, h.size() * sizeof(uint32_t)));
     prog.chunks.push_back(c);
     HIP_TRY(hipMemcpy(c.dev, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -107,7 +126,7 @@ int build_program(const uint8_t* in_idx, int nin, const uint8_t* out_idx, int no
 
 // One multi-pattern run-time launch of the per-segment reconstruct path.
 struct PsLaunch {
-  int nob = 0;
+  int nob = 0, nin = 0;
   size_t off = 0, count = 0;  // into the cached segment-list / chunk-pointer arrays
 };
 
@@ -165,10 +184,16 @@ Layout batch_layout(const cec_codec* c, const uint8_t* d_data, const uint8_t* d_
   return L;
 }
 
+void launch_chunk(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
+                  int nin, int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  if (nin <= cec::kRthMaxIn && cec::launch_matvec_rth(L, chunk, per_seg, nin, seg_list, nseg, st))
+    return;
+  cec::launch_matvec_rt(L, chunk, per_seg, nob, seg_list, nseg, st);
+}
+
 void run_program(const Program& p, const Layout& L, const uint32_t* seg_list, uint32_t nseg,
                  hipStream_t st) {
-  for (const auto& c : p.chunks)
-    cec::launch_matvec_rt(L, c.dev, nullptr, c.nob, seg_list, nseg, st);
+  for (const auto& c : p.chunks) launch_chunk(L, c.dev, nullptr, c.nin, c.nob, seg_list, nseg, st);
 }
 
 int check_launch() {
@@ -350,6 +375,10 @@ int cec_set_option(cec_codec* c, int option, int value) {
       if (value < 0 || value > 2) return set_err(CEC_EINVAL, "sha mode out of range");
       cec::set_sha_mode(value);
       return CEC_OK;
+    case CEC_OPT_RT_MODE:
+      if (value < 0 || value > 1) return set_err(CEC_EINVAL, "rt mode out of range");
+      cec::set_rt_mode(value);
+      return CEC_OK;
   }
   return set_err(CEC_EINVAL, "unknown option");
 }
@@ -422,13 +451,17 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
       for (auto& pr : progs) maxchunks = std::max(maxchunks, pr.first->chunks.size());
       for (size_t ci = 0; ci < maxchunks; ++ci) {
         std::unordered_map<int, std::vector<std::pair<uint32_t, const uint32_t*>>> byb;
+        int nin_max = 0;
         for (auto& pr : progs)
-          if (ci < pr.first->chunks.size())
+          if (ci < pr.first->chunks.size()) {
+            nin_max = std::max(nin_max, pr.first->chunks[ci].nin);
             for (uint32_t sg : *pr.second)
               byb[pr.first->chunks[ci].nob].push_back({sg, pr.first->chunks[ci].dev});
+          }
         for (auto& b : byb) {
           PsLaunch l;
           l.nob = b.first;
+          l.nin = nin_max;
           l.off = hl.size();
           l.count = b.second.size();
           for (auto& e : b.second) {
@@ -460,8 +493,8 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
   }
   const uint32_t* const* ptrs = reinterpret_cast<const uint32_t* const*>(c->ps_ptrs);
   for (const auto& l : c->ps_rt) {
-    cec::launch_matvec_rt(L, nullptr, ptrs + l.off, l.nob, c->ps_list + l.off,
-                          (uint32_t)l.count, st);
+    launch_chunk(L, nullptr, ptrs + l.off, l.nin, l.nob, c->ps_list + l.off, (uint32_t)l.count,
+                 st);
     int rc = check_launch();
     if (rc) return rc;
   }

@@ -24,10 +24,17 @@ struct Layout {
 // Layout (all uint32): header {nin, nout, nob, 0}, in[256], out[256], hb[256] (highest set
 // coefficient bit of input column j, -1 for a zero column), then masks[nin][8][nob]:
 // masks[j][b][o] = 0xFFFFFFFF when bit b of coef[o][j] is set (zero padded to the bucket nob).
+// When nin <= kRthMaxIn, header[3] is the word offset of a Horner section used by the
+// Horner-over-input-groups kernel (k_rth): top[32] (highest set coefficient bit of output row
+// o, 0xFFFFFFFF for a zero row), then idx[32][8][8]: idx[o][b][g] = the 4-bit combination of
+// input group g (inputs 4g..4g+3) whose coefficients in row o have bit b set.
 constexpr int kRtMaxOut = 32;
+constexpr int kRthMaxIn = 32;
 constexpr size_t kRtHeaderWords = 4 + 256 + 256 + 256;
+constexpr size_t kRthWords = 32 + 32 * 8 * 8;
 inline size_t rt_chunk_bytes(int nin, int nob) {
-  return (kRtHeaderWords + (size_t)nin * 8 * nob) * sizeof(uint32_t);
+  return (kRtHeaderWords + (size_t)nin * 8 * nob + (nin <= kRthMaxIn ? kRthWords : 0)) *
+         sizeof(uint32_t);
 }
 
 // True when every shard start and the shard length allow 16-byte vector access.
@@ -52,6 +59,10 @@ int rt_bucket(int nout);
 // bucket `nob`). Chunks are device memory laid out as described at RtChunk above.
 void launch_matvec_rt(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
                       int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
+// Same product from the chunks' Horner sections (every chunk of the launch has nin <= nin_max
+// <= kRthMaxIn). Returns false (nothing launched) if the form is disabled by the variant knob.
+bool launch_matvec_rth(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
+                       int nin_max, const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
 
 // SHA-256 of `n` equal-length buffers, written as 64 lowercase hex characters each into
 // `hex_out` (device, n * 64 bytes). If `ptrs` is null, buffer i is shard (i % nshards) of

@@ -695,6 +695,85 @@ __global__ __launch_bounds__(256) void k_rt(Layout L, const uint32_t* __restrict
     if (o < (int)nout) shard_ptr(L, (int)out_idx[o], seg)[i] = (uint8_t)acc[o][0];
 }
 
+// Horner over input groups with run-time coefficients (k_rth): the compile-time k_hg scheme
+// with the per-(output, bit, group) combination index read from the chunk's Horner section
+// through the constant address space. Each group's 16 combinations (entry 0 = 0) live in one
+// 16-VGPR vector and a wave-uniform index selects one with s_set_gpr_idx (one v_mov + two SALU
+// per read); per (output, bit) that is NG reads + NG XORs + one xtime, against 32 v_bitop3 masks
+// (one per input) plus 7 xtimes per input column in k_rt.
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+template <int NG, class LD, class ST>
+__device__ __forceinline__ void rth_column(const cu32* __restrict__ P, LD ld, ST st) {
+  const uint32_t nin = P[0], nout = P[1];
+  const cu32* __restrict__ in_idx = P + 4;
+  const cu32* __restrict__ out_idx = P + 4 + 256;
+  const cu32* __restrict__ top = P + P[3];
+  const cu32* __restrict__ ix = top + 32;
+  u32x16 comb[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    uint32_t x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = (uint32_t)(4 * g + i) < nin ? ld(in_idx[4 * g + i]) : 0u;
+    comb[g][0] = 0;
+    comb[g][1] = x[0];
+    comb[g][2] = x[1];
+    comb[g][4] = x[2];
+    comb[g][8] = x[3];
+#pragma unroll
+    for (int v = 3; v < 16; ++v)
+      if (v & (v - 1)) comb[g][v] = xor2(comb[g][v & (v - 1)], comb[g][v & -v]);
+  }
+  // Every row runs all 8 bits (index 0 reads the zero entry): a branch-free body lets the
+  // row's 64 indices arrive in a few s_load_dwordx16 ahead of use.
+  (void)top;
+  for (uint32_t o = 0; o < nout; ++o) {
+    const cu32* __restrict__ q = ix + o * 64;
+    uint32_t y = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; --b) {
+      if (b < 7) y = xt_fast(y);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) y ^= comb[g][q[b * 8 + g]];
+    }
+    st(out_idx[o], y);
+  }
+}
+
+template <int NG>
+__global__ __launch_bounds__(256) void k_rth(Layout L, const uint32_t* __restrict__ chunk,
+                                             const uint32_t* const* __restrict__ per_seg,
+                                             const uint32_t* __restrict__ seg_list, uint32_t seg0,
+                                             int vec_ok) {
+  const uint32_t y = seg0 + blockIdx.y;
+  const uint32_t seg = seg_list ? seg_list[y] : y;
+  const cu32* __restrict__ P = as_const(per_seg ? as_const_ptr(per_seg, y) : chunk);
+  if (vec_ok) {
+    const uint64_t nvec = L.len / 4;
+    const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v < nvec) {
+      const uint64_t off = v * 4;
+      auto ld = [&](uint32_t sh) CEC_AI -> uint32_t {
+        return *reinterpret_cast<const uint32_t*>(shard_ptr(L, (int)sh, seg) + off);
+      };
+      auto st = [&](uint32_t sh, uint32_t val) CEC_AI {
+        *reinterpret_cast<uint32_t*>(shard_ptr(L, (int)sh, seg) + off) = val;
+      };
+      rth_column<NG>(P, ld, st);
+    }
+    if (!(L.len % 4) || blockIdx.x != gridDim.x - 1) return;
+  }
+  // byte path: whole shard (vec_ok == 0, grid covers len) or the tail (last block); one byte
+  // per lane in the low byte of a dword (the arithmetic is byte-wise, upper bytes stay zero)
+  const uint64_t i = vec_ok ? (L.len - L.len % 4) + threadIdx.x
+                            : (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= L.len) return;
+  auto ld = [&](uint32_t sh) CEC_AI -> uint32_t { return shard_ptr(L, (int)sh, seg)[i]; };
+  auto st = [&](uint32_t sh, uint32_t val) CEC_AI { shard_ptr(L, (int)sh, seg)[i] = (uint8_t)val; };
+  rth_column<NG>(P, ld, st);
+}
+
 // ---------------------------------------------------------------------------------------------
 // SHA-256 (FIPS 180-4), one lane per buffer.
 // ---------------------------------------------------------------------------------------------
@@ -1191,6 +1270,42 @@ namespace {
 int g_sha_mode = 0;  // 0 auto, 1 one wave, 2 two waves per 64 buffers
 }
 void set_sha_mode(int v) { g_sha_mode = v; }
+
+namespace {
+int g_rt_mode = 0;  // 0: Horner-over-groups run-time kernel where possible, 1: always k_rt
+
+template <int NG>
+void run_rth(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
+             const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  const uintptr_t bits = (uintptr_t)L.data | (uintptr_t)L.parity | L.shard_stride |
+                         L.data_seg_stride | L.par_seg_stride;
+  const int vec_ok = (bits & 3) == 0;
+  uint64_t gx = vec_ok ? (L.len / 4 + 255) / 256 : (L.len + 255) / 256;
+  if (gx == 0) gx = 1;
+  for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) {
+    hipLaunchKernelGGL((k_rth<NG>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, chunk, per_seg,
+                       seg_list, s0, vec_ok);
+  });
+}
+}  // namespace
+
+void set_rt_mode(int v) { g_rt_mode = v; }
+
+bool launch_matvec_rth(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
+                       int nin_max, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  // measured (profiles/r01/rt_modes.txt): faster than k_rt from 4 inputs up (RS(10,4) encode
+  // 3.0 vs 2.7 TB/s, RS(32,32) one-fragment repair 4.0 vs 3.1, 32-erasure rebuild 1.1 vs 0.96);
+  // for 2-3 inputs k_rt's 16-byte columns win (RS(2,1) run-time encode 6.0 vs 2.9 TB/s)
+  if (g_rt_mode == 1 || nin_max > kRthMaxIn || nin_max < 4) return false;
+  const int ng = (nin_max + 3) / 4;
+  if (ng <= 1) run_rth<1>(L, chunk, per_seg, seg_list, nseg, st);
+  else if (ng == 2) run_rth<2>(L, chunk, per_seg, seg_list, nseg, st);
+  else if (ng == 3) run_rth<3>(L, chunk, per_seg, seg_list, nseg, st);
+  else if (ng == 4) run_rth<4>(L, chunk, per_seg, seg_list, nseg, st);
+  else if (ng <= 6) run_rth<6>(L, chunk, per_seg, seg_list, nseg, st);
+  else run_rth<8>(L, chunk, per_seg, seg_list, nseg, st);
+  return true;
+}
 
 void launch_sha256_hex(const uint8_t* const* ptrs, const Layout* L, int nshards, uint64_t n,
                        uint64_t len, uint8_t* hex_out, hipStream_t st) {

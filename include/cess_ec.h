@@ -108,6 +108,8 @@ int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t s
 #define CEC_OPT_CT_VARIANT 2    /* compile-time kernel unroll/cache variant, -1 = default */
 #define CEC_OPT_SHA_MODE 3      /* SHA-256 kernel: 0 = auto, 1 = one wave per 64 buffers,
                                    2 = two waves (schedule producer + rounds consumer) */
+#define CEC_OPT_RT_MODE 4       /* run-time-coefficient kernel: 0 = Horner over input groups
+                                   when k <= 32, 1 = always the per-bit mask kernel */
 int cec_set_option(cec_codec* codec, int option, int value);
 
 #ifdef __cplusplus

@@ -493,3 +493,38 @@ def test_c_abi_consumer(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "cabi roundtrip ok" in r.stdout
+
+
+@pytest.mark.parametrize("k,m,ln", [(32, 32, 4096 + 3), (10, 4, 1000), (17, 3, 4099),
+                                    (33, 3, 515), (1, 1, 9), (5, 5, 64)])
+def test_runtime_kernels_agree(torch, cess, corc, k, m, ln):
+    """k_rth (Horner over input groups, run-time indices) and k_rt (per-bit masks) against the
+    C oracle: encode and per-segment random-erasure reconstruct, vector body and byte tail."""
+    nseg = 3
+    rng = np.random.default_rng(k * 1000 + ln)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = np.ones((nseg, k + m), np.uint8)
+    for s in range(nseg):
+        present[s, rng.choice(k + m, size=m, replace=False)] = 0
+    enc = cess.New(k, m)
+    enc.set_option(1, 1)  # run-time coefficients for encode too
+    try:
+        for mode in (0, 1):
+            enc.set_option(4, mode)
+            d_data = to_dev(torch, data)
+            d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
+            enc.EncodeBatch(d_data, d_par, nseg, ln)
+            torch.cuda.synchronize()
+            assert np.array_equal(d_par.cpu().numpy(), want), ("encode", mode)
+            keep = torch.from_numpy(present[:, :k, None].astype(np.uint8)).cuda()
+            keep_p = torch.from_numpy(present[:, k:, None].astype(np.uint8)).cuda()
+            d_data *= keep
+            d_par *= keep_p
+            enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+            torch.cuda.synchronize()
+            assert np.array_equal(d_data.cpu().numpy(), data), ("reconstruct", mode)
+            assert np.array_equal(d_par.cpu().numpy(), want), ("reconstruct parity", mode)
+    finally:
+        enc.set_option(4, 0)
+
