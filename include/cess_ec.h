@@ -103,13 +103,14 @@ int cec_split_segment(const uint8_t* seg, size_t seg_len, int k, uint8_t* const*
 int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t seg0,
                        uint64_t seed, void* hip_stream);
 
-/* Options (tuning / testing). */
+/* Options (tuning / testing). CT_VARIANT, SHA_MODE and RT_MODE are process-wide kernel choices
+ * (the codec argument may be any live handle); FORCE_GENERIC is per codec. */
 #define CEC_OPT_FORCE_GENERIC 1 /* 1: always use the run-time-coefficient kernel */
 #define CEC_OPT_CT_VARIANT 2    /* compile-time kernel unroll/cache variant, -1 = default */
 #define CEC_OPT_SHA_MODE 3      /* SHA-256 kernel: 0 = auto, 1 = one wave per 64 buffers,
                                    2 = two waves (schedule producer + rounds consumer) */
 #define CEC_OPT_RT_MODE 4       /* run-time-coefficient kernel: 0 = Horner over input groups
-                                   when k <= 32, 1 = always the per-bit mask kernel */
+                                   when 4 <= inputs <= 32, 1 = always the per-bit mask kernel */
 int cec_set_option(cec_codec* codec, int option, int value);
 
 #ifdef __cplusplus
