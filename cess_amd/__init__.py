@@ -5,6 +5,7 @@ this package is the host-side mirror of the off-chain codec API (klauspost/reeds
 plus the CESS segment / fragment records.
 """
 from . import geometry
+from .hashq import HashQueue, sha256_blocks
 from .reedsolomon import (
     CecError,
     Encoder,
@@ -24,5 +25,6 @@ from .reedsolomon import (
 __all__ = [
     "geometry", "CecError", "Encoder", "New", "ErrInvShardNum", "ErrMaxShardNum",
     "ErrReconstructRequired", "ErrShardNoData", "ErrShardSize", "ErrShortData",
-    "ErrTooFewShards", "HipError", "fill_synthetic", "sha256_hex_device",
+    "ErrTooFewShards", "HipError", "fill_synthetic", "sha256_hex_device", "HashQueue",
+    "sha256_blocks",
 ]

@@ -4,7 +4,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint64, c_void_p
+from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CESS_EC_LIB", os.path.join(_HERE, "libcessec.so"))
@@ -31,6 +31,14 @@ SIGNATURES = {
     "cec_split_segment": (c_int, [c_void_p, c_size_t, c_int, POINTER(c_void_p), c_size_t]),
     "cec_fill_synthetic": (c_int, [c_void_p, c_size_t, c_size_t, c_uint64, c_uint64, c_void_p]),
     "cec_set_option": (c_int, [c_void_p, c_int, c_int]),
+    "cec_hashq_create": (c_int, [c_int, c_size_t, c_void_p, POINTER(c_void_p)]),
+    "cec_hashq_destroy": (None, [c_void_p]),
+    "cec_hashq_add": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_size_t,
+                              c_size_t, c_void_p, c_size_t, POINTER(c_uint64)]),
+    "cec_hashq_tick": (c_int, [c_void_p, c_uint32]),
+    "cec_hashq_finish": (c_int, [c_void_p]),
+    "cec_hashq_status": (c_int, [c_void_p, c_uint64, POINTER(c_int), POINTER(c_size_t),
+                                 POINTER(c_uint64)]),
 }
 
 CEC_OK = 0

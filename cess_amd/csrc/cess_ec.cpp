@@ -22,6 +22,7 @@ namespace cec {
 void set_ct_variant(int v);
 void set_sha_mode(int v);
 void set_rt_mode(int v);
+void set_tick_prefetch(int v);
 }
 
 namespace {
@@ -286,6 +287,11 @@ Layout stage_layout(cec_codec* c, size_t len) {
 
 }  // namespace
 
+namespace cec {
+// error reporting shared with hashq.cpp (same thread-local detail string)
+int set_error(int code, const std::string& msg) { return set_err(code, msg); }
+}  // namespace cec
+
 extern "C" {
 
 const char* cec_version(void) { return "cessec 0.1.0 gfx950"; }
@@ -378,6 +384,10 @@ int cec_set_option(cec_codec* c, int option, int value) {
     case CEC_OPT_RT_MODE:
       if (value < 0 || value > 1) return set_err(CEC_EINVAL, "rt mode out of range");
       cec::set_rt_mode(value);
+      return CEC_OK;
+    case CEC_OPT_TICK_PREFETCH:
+      if (value < 1 || value > 2) return set_err(CEC_EINVAL, "tick prefetch must be 1 or 2");
+      cec::set_tick_prefetch(value);
       return CEC_OK;
   }
   return set_err(CEC_EINVAL, "unknown option");

@@ -70,6 +70,29 @@ bool launch_matvec_rth(const Layout& L, const uint32_t* chunk, const uint32_t* c
 void launch_sha256_hex(const uint8_t* const* ptrs, const Layout* L, int nshards, uint64_t n,
                        uint64_t len, uint8_t* hex_out, hipStream_t st);
 
+// One chain of the streaming SHA-256 queue (hashq.cpp), 64 bytes in HBM. `blk` counts the
+// 64-byte blocks already compressed into `h`, padding blocks included; the chain is complete
+// when blk == (len >> 6) + ((len & 63) >= 56 ? 2 : 1), and its hex (if `hex` is set) is written
+// by the launch that completes it.
+struct ShaChain {
+  const uint8_t* src;
+  uint64_t len;
+  uint64_t blk;
+  uint8_t* hex;
+  uint32_t h[8];
+};
+static_assert(sizeof(ShaChain) == 64, "ShaChain is one 64-byte record");
+
+inline uint64_t sha256_blocks(uint64_t len) { return (len >> 6) + ((len & 63) >= 56 ? 2 : 1); }
+
+// Initialise n chains in slots slot0.. of the ring `tab` (capacity mask + 1, a power of two).
+void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
+                      const uint8_t* base, uint32_t per, uint64_t outer, uint64_t inner,
+                      uint64_t len, uint8_t* hex, uint64_t hex_outer, hipStream_t st);
+// Advance the n chains in slots head.. by at most max_blocks blocks each.
+void launch_sha256_tick(ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,
+                        uint32_t max_blocks, hipStream_t st);
+
 // Synthetic segment bytes: 64-bit word w of segment s = splitmix64(seed ^ (s << 32) ^ w),
 // little-endian; segments are seg_bytes long and contiguous from `out`.
 void launch_fill_splitmix(uint8_t* out, uint64_t seg_bytes, uint64_t nseg, uint64_t seg0,

@@ -1,0 +1,567 @@
+// SHA-256 kernels of libcessec (FIPS 180-4) for the fragment and segment hashes of CESS's
+// SegmentList (c-pallets/file-bank/src/types.rs:13-16): one-shot batch kernels (k_sha256,
+// k_sha256_2w) and the streaming hash-queue kernels (k_hashq_add, k_sha256_tick).
+#include "dev_util.h"
+#include "kernels.h"
+
+namespace cec {
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return xor3_u32(a, b, c);
+}
+
+// ---------------------------------------------------------------------------------------------
+// SHA-256 (FIPS 180-4), one lane per buffer.
+// ---------------------------------------------------------------------------------------------
+__constant__ uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) {
+  return __builtin_amdgcn_alignbit(x, x, n);
+}
+
+// v_bitop3 truth tables (index = a<<2 | b<<1 | c): Ch = a ? b : c, Maj = majority.
+__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+  return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+
+__device__ __forceinline__ void sha256_block(uint32_t (&h)[8], uint32_t (&w)[16]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+      const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+      wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
+      w[t & 15] = wt;
+    }
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+    const uint32_t t1 = hh + S1 + ch(e, f, g) + kSha256K[t] + wt;
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+    const uint32_t t2 = S0 + maj(a, b, c);
+    hh = g; g = f; f = e; e = d + t1;
+    d = c; c = b; b = a; a = t1 + t2;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+__global__ __launch_bounds__(64) void k_sha256(const uint8_t* const* __restrict__ ptrs, Layout L,
+                                               int nshards, uint64_t n, uint64_t len,
+                                               uint8_t* __restrict__ hex_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* src =
+      ptrs ? ptrs[i] : shard_ptr(L, (int)(i % nshards), (uint32_t)(i / nshards));
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint32_t w[16];
+  const uint64_t nfull = len >> 6;
+  const bool al16 = ((uintptr_t)src & 15) == 0;
+  if (al16) {
+    // The next block's 64 bytes are loaded while this block is compressed: one HBM round trip
+    // per block (~1-2 us under load) would otherwise sit on every lane's serial chain.
+    u32x4 nx[4];
+    if (nfull) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(src + 16 * q);
+    }
+    for (uint64_t blk = 0; blk < nfull; ++blk) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w[4 * q + 0] = __builtin_bswap32(nx[q].x);
+        w[4 * q + 1] = __builtin_bswap32(nx[q].y);
+        w[4 * q + 2] = __builtin_bswap32(nx[q].z);
+        w[4 * q + 3] = __builtin_bswap32(nx[q].w);
+      }
+      if (blk + 1 < nfull) {
+        const uint8_t* p = src + ((blk + 1) << 6);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+      }
+      sha256_block(h, w);
+    }
+  } else {
+    for (uint64_t blk = 0; blk < nfull; ++blk) {
+      const uint8_t* p = src + (blk << 6);
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        w[q] = (uint32_t)p[4 * q] << 24 | (uint32_t)p[4 * q + 1] << 16 |
+               (uint32_t)p[4 * q + 2] << 8 | (uint32_t)p[4 * q + 3];
+      sha256_block(h, w);
+    }
+  }
+  // Padding: remaining r bytes, 0x80, zeros, 64-bit big-endian bit length.
+  const uint32_t r = (uint32_t)(len & 63);
+  const uint8_t* p = src + (nfull << 6);
+  const uint64_t bits = len << 3;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t pos = 4 * q + s;
+      const uint32_t byte = pos < r ? p[pos] : (pos == r ? 0x80u : 0u);
+      word |= byte << (24 - 8 * s);
+    }
+    w[q] = word;
+  }
+  if (r >= 56) {
+    sha256_block(h, w);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) w[q] = 0;
+  }
+  w[14] = (uint32_t)(bits >> 32);
+  w[15] = (uint32_t)bits;
+  sha256_block(h, w);
+  uint8_t* o = hex_out + i * 64;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    uint32_t word = h[q];
+    uint32_t lo = 0, hi = 0;  // 8 hex chars of this word, packed little-endian for 2 stores
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const uint32_t nib = (word >> (28 - 4 * s)) & 15u;
+      const uint32_t ch = nib < 10 ? '0' + nib : 'a' + nib - 10;
+      if (s < 4) lo |= ch << (8 * s);
+      else hi |= ch << (8 * (s - 4));
+    }
+    *reinterpret_cast<uint32_t*>(o + 8 * q) = lo;
+    *reinterpret_cast<uint32_t*>(o + 8 * q + 4) = hi;
+  }
+}
+
+// Two waves per group of 64 buffers. Each buffer's hash is one serial chain, so with few
+// buffers (a 1 GiB RS(32,32) batch is 4096 fragments = 64 waves on a 1024-SIMD chip) the time
+// is the per-block instruction count of ONE wave. The message schedule does not depend on the
+// chaining state, so wave 0 (producer) loads block i+1, byte-swaps it and expands W[0..63] + K
+// into LDS while wave 1 (consumer) runs the 64 rounds of block i: the consumer's chain drops from
+// ~1460 to ~900 VALU instructions per block. LDS ring: 2 buffers x 64 words x 64 lanes (32 KiB),
+// [buf][word/4][lane][4] so every ds_write/read_b128 covers 1 KiB contiguous. One barrier per
+// block; the padding block(s) go through the same pipeline.
+__device__ __forceinline__ const uint8_t* sha_src(const uint8_t* const* ptrs, const Layout& L,
+                                                  int nshards, uint64_t i) {
+  return ptrs ? ptrs[i] : shard_ptr(L, (int)(i % nshards), (uint32_t)(i / nshards));
+}
+
+__device__ __forceinline__ void sha_expand_store(uint32_t (&w)[16], u32x4* __restrict__ dst) {
+  // dst[q * 64] = {W+K}[4q .. 4q+3] for this lane
+#pragma unroll
+  for (int t = 0; t < 64; t += 4) {
+    uint32_t o[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int u = t + s;
+      uint32_t wt;
+      if (u < 16) {
+        wt = w[u];
+      } else {
+        const uint32_t w15 = w[(u + 1) & 15], w2 = w[(u + 14) & 15];
+        const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+        const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+        wt = w[u & 15] + s0 + w[(u + 9) & 15] + s1;
+        w[u & 15] = wt;
+      }
+      o[s] = wt + kSha256K[u];
+    }
+    dst[(t / 4) * 64] = u32x4{o[0], o[1], o[2], o[3]};
+  }
+}
+
+__global__ __launch_bounds__(128) void k_sha256_2w(const uint8_t* const* __restrict__ ptrs,
+                                                   Layout L, int nshards, uint64_t n,
+                                                   uint64_t len, uint8_t* __restrict__ hex_out) {
+  __shared__ u32x4 ring[2][16][64];
+  const int lane = threadIdx.x & 63;
+  // wave-uniform by construction (SGPR), so the two sides' barriers never run under one EXEC mask
+  const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  const uint64_t i = (uint64_t)blockIdx.x * 64 + lane;
+  const bool live = i < n;
+  const uint64_t nfull = len >> 6;
+  const uint32_t r = (uint32_t)(len & 63);
+  const uint64_t nb = nfull + (r >= 56 ? 2 : 1);  // blocks including padding
+  if (producer) {
+    const uint8_t* src = live ? sha_src(ptrs, L, nshards, i) : nullptr;
+    const bool al16 = live && ((uintptr_t)src & 15) == 0;
+    u32x4 nx[4] = {};
+    if (al16 && nfull) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(src + 16 * q);
+    }
+    for (uint64_t blk = 0; blk < nb; ++blk) {
+      uint32_t w[16];
+      if (blk < nfull) {
+        if (al16) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            w[4 * q + 0] = __builtin_bswap32(nx[q].x);
+            w[4 * q + 1] = __builtin_bswap32(nx[q].y);
+            w[4 * q + 2] = __builtin_bswap32(nx[q].z);
+            w[4 * q + 3] = __builtin_bswap32(nx[q].w);
+          }
+          if (blk + 1 < nfull) {
+            const uint8_t* p = src + ((blk + 1) << 6);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+          }
+        } else if (live) {
+          const uint8_t* p = src + (blk << 6);
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            w[q] = (uint32_t)p[4 * q] << 24 | (uint32_t)p[4 * q + 1] << 16 |
+                   (uint32_t)p[4 * q + 2] << 8 | (uint32_t)p[4 * q + 3];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) w[q] = 0;
+        }
+      } else {
+        // padding block(s): remaining r bytes, 0x80, zeros, 64-bit big-endian bit length
+        const bool first_pad = blk == nfull;
+        const uint8_t* p = live ? src + (nfull << 6) : nullptr;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          uint32_t word = 0;
+          if (first_pad) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const uint32_t pos = 4 * q + s;
+              const uint32_t byte = pos < r ? (live ? p[pos] : 0u) : (pos == r ? 0x80u : 0u);
+              word |= byte << (24 - 8 * s);
+            }
+          }
+          w[q] = word;
+        }
+        if (blk == nb - 1) {
+          const uint64_t bits = len << 3;
+          w[14] = (uint32_t)(bits >> 32);
+          w[15] = (uint32_t)bits;
+        }
+      }
+      sha_expand_store(w, &ring[blk & 1][0][lane]);
+      __syncthreads();
+    }
+    __syncthreads();  // matches the consumer's final iteration
+  } else {
+    uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                     0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    __syncthreads();  // block 0 produced
+    for (uint64_t blk = 0; blk < nb; ++blk) {
+      const u32x4* src = &ring[blk & 1][0][lane];
+      uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const u32x4 kw4 = src[q * 64];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const uint32_t kw = s == 0 ? kw4.x : s == 1 ? kw4.y : s == 2 ? kw4.z : kw4.w;
+          const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+          const uint32_t t1 = hh + S1 + ch(e, f, g) + kw;
+          const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+          const uint32_t t2 = S0 + maj(a, b, c);
+          hh = g; g = f; f = e; e = d + t1;
+          d = c; c = b; b = a; a = t1 + t2;
+        }
+      }
+      h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+      __syncthreads();  // this buffer consumed / next one produced
+    }
+    if (live) {
+      uint8_t* o = hex_out + i * 64;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        uint32_t word = h[q];
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const uint32_t nib = (word >> (28 - 4 * s)) & 15u;
+          const uint32_t chr = nib < 10 ? '0' + nib : 'a' + nib - 10;
+          if (s < 4) lo |= chr << (8 * s);
+          else hi |= chr << (8 * (s - 4));
+        }
+        *reinterpret_cast<uint32_t*>(o + 8 * q) = lo;
+        *reinterpret_cast<uint32_t*>(o + 8 * q + 4) = hi;
+      }
+    }
+  }
+}
+
+// Streaming SHA-256 over many long buffers (the hash queue, hashq.cpp). A chain's state
+// (ShaChain, kernels.h) lives in HBM between launches, so one tick kernel advances every live
+// chain of the queue by at most `max_blocks` 64-byte blocks and chains of different batches,
+// lengths and ages share launches. With a window of several batches in flight the chip holds
+// tens of thousands of chains at once, where one batch alone (4096 fragments of a 1 GiB
+// RS(32,32) batch; 192 of a 1 GiB RS(2,1) batch) fills a few percent of its SIMDs. Same
+// two-wave structure as k_sha256_2w; chains of one wave may be at different blocks.
+__device__ __forceinline__ void sha_store_hex(uint8_t* __restrict__ o, const uint32_t (&h)[8]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t word = h[q];
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const uint32_t nib = (word >> (28 - 4 * s)) & 15u;
+      const uint32_t chr = nib < 10 ? '0' + nib : 'a' + nib - 10;
+      if (s < 4) lo |= chr << (8 * s);
+      else hi |= chr << (8 * (s - 4));
+    }
+    *reinterpret_cast<uint32_t*>(o + 8 * q) = lo;
+    *reinterpret_cast<uint32_t*>(o + 8 * q + 4) = hi;
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
+#define CEC_SHA_AI __attribute__((always_inline))
+
+template <int PF>
+__global__ __launch_bounds__(128) void k_sha256_tick(ShaChain* __restrict__ tab, uint32_t mask,
+                                                     uint64_t head, uint32_t n,
+                                                     uint32_t max_blocks) {
+  __shared__ u32x4 ring[2][16][64];
+  const int lane = threadIdx.x & 63;
+  const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  const uint32_t i = blockIdx.x * 64 + lane;
+  const bool live = i < n;
+  ShaChain* ch_ = &tab[(uint32_t)(head + i) & mask];
+  uint64_t len = 0, blk0 = 0;
+  if (live) {
+    len = ch_->len;
+    blk0 = ch_->blk;
+  }
+  const uint64_t nfull = len >> 6;
+  const uint32_t r = (uint32_t)(len & 63);
+  const uint64_t nb = nfull + (r >= 56 ? 2 : 1);  // blocks including padding
+  const uint64_t rem = live ? nb - blk0 : 0;
+  const uint32_t nblk = rem < max_blocks ? (uint32_t)rem : max_blocks;
+  // both waves see the same 64 chains, so they agree on the trip count (and barrier count)
+  const uint32_t trips = wave_max_u32(nblk);
+  if (trips == 0) return;
+  if (producer) {
+    const uint8_t* src = live ? ch_->src : nullptr;
+    const bool al16 = live && ((uintptr_t)src & 15) == 0;
+    // Fast phase: blocks every lane of the wave has as aligned message data (the bulk of a
+    // tick), one wave-uniform loop with the next block's loads in flight. General phase: the
+    // rest (padding blocks, unaligned buffers, lanes that are done), loaded directly.
+    const uint64_t dat = blk0 < nfull ? nfull - blk0 : 0;
+    const uint32_t mine = al16 ? (uint32_t)(dat < nblk ? dat : nblk) : 0u;
+    const uint32_t nfast = __builtin_amdgcn_readfirstlane(wave_min_u32(live ? mine : ~0u));
+    // lanes past n take no part in nfast; their loads are masked off
+    // nx[j] holds block b + j: PF blocks of loads in flight ahead of the one being expanded
+    u32x4 nx[PF][4] = {};
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      if ((uint32_t)j < nfast && live) {
+        const uint8_t* p = src + ((blk0 + j) << 6);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nx[j][q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+      }
+    auto expand = [&](u32x4 (&v)[4], uint32_t blk) CEC_SHA_AI {
+      uint32_t w[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w[4 * q + 0] = __builtin_bswap32(v[q].x);
+        w[4 * q + 1] = __builtin_bswap32(v[q].y);
+        w[4 * q + 2] = __builtin_bswap32(v[q].z);
+        w[4 * q + 3] = __builtin_bswap32(v[q].w);
+      }
+      const uint32_t nb_next = blk + PF;
+      if (nb_next < nfast && live) {
+        const uint8_t* p = src + ((blk0 + nb_next) << 6);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+      }
+      sha_expand_store(w, &ring[blk & 1][0][lane]);
+      __syncthreads();
+    };
+    uint32_t b = 0;
+    for (; b + PF <= nfast; b += PF) {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) expand(nx[j], b + j);
+    }
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      if (b < nfast) {
+        expand(nx[j], b);
+        ++b;
+      }
+    for (; b < trips; ++b) {
+      const uint64_t g = blk0 + b;
+      uint32_t w[16];
+      if (b < nblk && g < nfull) {
+        const uint8_t* p = src + (g << 6);
+        if (al16) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(p + 16 * q);
+            w[4 * q + 0] = __builtin_bswap32(v.x);
+            w[4 * q + 1] = __builtin_bswap32(v.y);
+            w[4 * q + 2] = __builtin_bswap32(v.z);
+            w[4 * q + 3] = __builtin_bswap32(v.w);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            w[q] = (uint32_t)p[4 * q] << 24 | (uint32_t)p[4 * q + 1] << 16 |
+                   (uint32_t)p[4 * q + 2] << 8 | (uint32_t)p[4 * q + 3];
+        }
+      } else if (b < nblk) {
+        // padding block(s): remaining r bytes, 0x80, zeros, 64-bit big-endian bit length
+        const bool first_pad = g == nfull;
+        const uint8_t* p = src + (nfull << 6);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          uint32_t word = 0;
+          if (first_pad) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const uint32_t pos = 4 * q + s;
+              const uint32_t byte = pos < r ? p[pos] : (pos == r ? 0x80u : 0u);
+              word |= byte << (24 - 8 * s);
+            }
+          }
+          w[q] = word;
+        }
+        if (g == nb - 1) {
+          const uint64_t bits = len << 3;
+          w[14] = (uint32_t)(bits >> 32);
+          w[15] = (uint32_t)bits;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) w[q] = 0;
+      }
+      sha_expand_store(w, &ring[b & 1][0][lane]);
+      __syncthreads();
+    }
+    __syncthreads();  // matches the consumer's final iteration
+  } else {
+    uint32_t h[8] = {};
+    if (live) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) h[q] = ch_->h[q];
+    }
+    __syncthreads();  // block 0 produced
+    for (uint32_t b = 0; b < trips; ++b) {
+      if (b < nblk) {
+        const u32x4* src = &ring[b & 1][0][lane];
+        uint32_t a = h[0], bb = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const u32x4 kw4 = src[q * 64];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const uint32_t kw = s == 0 ? kw4.x : s == 1 ? kw4.y : s == 2 ? kw4.z : kw4.w;
+            const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+            const uint32_t t1 = hh + S1 + ch(e, f, g) + kw;
+            const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+            const uint32_t t2 = S0 + maj(a, bb, c);
+            hh = g; g = f; f = e; e = d + t1;
+            d = c; c = bb; bb = a; a = t1 + t2;
+          }
+        }
+        h[0] += a; h[1] += bb; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+      }
+      __syncthreads();  // this buffer consumed / next one produced
+    }
+    if (live && nblk) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ch_->h[q] = h[q];
+      ch_->blk = blk0 + nblk;
+      if (blk0 + nblk == nb && ch_->hex) sha_store_hex(ch_->hex, h);
+    }
+  }
+}
+
+// Initialise n chains in queue slots slot0.. (mod capacity): buffer i starts at
+// base + (i / per) * outer + (i % per) * inner and its hex goes to
+// hex + ((i / per) * hex_outer + i % per) * 64.
+__global__ __launch_bounds__(256) void k_hashq_add(ShaChain* __restrict__ tab, uint32_t mask,
+                                                   uint64_t slot0, uint32_t n,
+                                                   const uint8_t* base, uint32_t per,
+                                                   uint64_t outer, uint64_t inner, uint64_t len,
+                                                   uint8_t* hex, uint64_t hex_outer) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t a = i / per, b = i % per;
+  ShaChain c;
+  c.src = base + a * outer + b * inner;
+  c.len = len;
+  c.blk = 0;
+  c.hex = hex ? hex + (a * hex_outer + b) * 64 : nullptr;
+  const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                          0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+#pragma unroll
+  for (int q = 0; q < 8; ++q) c.h[q] = iv[q];
+  tab[(uint32_t)(slot0 + i) & mask] = c;
+}
+
+namespace {
+int g_sha_mode = 0;  // 0 auto, 1 one wave, 2 two waves per 64 buffers
+}
+void set_sha_mode(int v) { g_sha_mode = v; }
+
+namespace {
+int g_tick_pf = 1;  // hash-queue tick: message blocks loaded ahead by the producer wave (1 or 2)
+}
+void set_tick_prefetch(int v) { g_tick_pf = v == 2 ? 2 : 1; }
+
+
+void launch_sha256_hex(const uint8_t* const* ptrs, const Layout* L, int nshards, uint64_t n,
+                       uint64_t len, uint8_t* hex_out, hipStream_t st) {
+  if (n == 0) return;
+  Layout dummy{};
+  const unsigned g = (unsigned)((n + 63) / 64);
+  // Two waves per group while the groups leave SIMDs idle (latency regime: one serial chain
+  // per buffer); one wave per group once 2 * groups would exceed the chip's 1024 SIMDs.
+  const bool two = g_sha_mode == 2 || (g_sha_mode == 0 && g <= 512);
+  if (two)
+    hipLaunchKernelGGL(k_sha256_2w, dim3(g), dim3(128), 0, st, ptrs, L ? *L : dummy, nshards, n,
+                       len, hex_out);
+  else
+    hipLaunchKernelGGL(k_sha256, dim3(g), dim3(64), 0, st, ptrs, L ? *L : dummy, nshards, n, len,
+                       hex_out);
+}
+
+void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
+                      const uint8_t* base, uint32_t per, uint64_t outer, uint64_t inner,
+                      uint64_t len, uint8_t* hex, uint64_t hex_outer, hipStream_t st) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_hashq_add, dim3((n + 255) / 256), dim3(256), 0, st, tab, mask, slot0, n,
+                     base, per, outer, inner, len, hex, hex_outer);
+}
+
+void launch_sha256_tick(ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,
+                        uint32_t max_blocks, hipStream_t st) {
+  if (n == 0 || max_blocks == 0) return;
+  if (g_tick_pf == 2)
+    hipLaunchKernelGGL(k_sha256_tick<2>, dim3((n + 63) / 64), dim3(128), 0, st, tab, mask, head,
+                       n, max_blocks);
+  else
+    hipLaunchKernelGGL(k_sha256_tick<1>, dim3((n + 63) / 64), dim3(128), 0, st, tab, mask, head,
+                       n, max_blocks);
+}
+
+}  // namespace cec

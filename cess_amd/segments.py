@@ -12,11 +12,11 @@ last segment is zero padded to SEGMENT_SIZE. File hash [build convention]: SHA-2
 concatenated hex segment hashes — a two-level hash, so no serial pass over the whole file
 (one serial SHA-256 stream caps a file at ~2 GB/s).
 
-Pipeline (one GPU): batches of up to 64 segments (1 GiB) go through pinned host buffers and two
+Pipeline (one GPU): batches of up to 64 segments (1 GiB) go through pinned host buffers into
 device slots. Batch i+1's H2D copy and encode overlap the hashing of batch i. Hashes are
-computed where they are cheapest: on the host (OpenSSL SHA-NI via hashlib, threaded) for the
-few long fragments of the CESS geometry (3 x 8 MiB per segment), on the GPU (k_sha256) for wide
-codes with thousands of short fragments per batch.
+computed on the host (OpenSSL SHA-NI via hashlib, threaded) or on the GPU through the hash
+queue (cess_amd.hashq), which keeps a window of batches resident in HBM and hashes all their
+segment and fragment chains together (see SegmentEncoder).
 """
 from __future__ import annotations
 
@@ -81,21 +81,43 @@ def needed_space(seg_list: List[SegmentList],
     return len(seg_list) * (segment_size * 15 // 10)
 
 
-class _Limited(io.RawIOBase):
-    """Read at most `n` bytes from a file object."""
+class _ParallelReader:
+    """File-like source whose readinto() fills a large (pinned) buffer with several threads:
+    numpy copies and os.preadv release the GIL, so one Python thread's memcpy (~5-10 GB/s) does
+    not cap a pipeline that PCIe feeds at ~50 GB/s. Source: a uint8 array or an open fd."""
 
-    def __init__(self, f, n: int):
-        self.f, self.left = f, n
+    def __init__(self, pool: cf.ThreadPoolExecutor, nthreads: int, arr: Optional[np.ndarray]
+                 = None, fd: Optional[int] = None, start: int = 0, stop: int = 0):
+        self.pool, self.nthreads = pool, max(1, nthreads)
+        self.arr, self.fd = arr, fd
+        self.pos, self.stop = start, stop
 
-    def readable(self):
-        return True
+    def _pread(self, mv: memoryview, off: int) -> None:
+        import os
+        got = 0
+        while got < len(mv):
+            n = os.preadv(self.fd, [mv[got:]], off + got)
+            if n <= 0:
+                raise IOError("short read")
+            got += n
 
-    def readinto(self, b):
-        if self.left <= 0:
+    def readinto(self, b) -> int:
+        mv = memoryview(b).cast("B")
+        n = min(len(mv), self.stop - self.pos)
+        if n <= 0:
             return 0
-        mv = memoryview(b)[: self.left]
-        n = self.f.readinto(mv)
-        self.left -= n or 0
+        step = max(4 << 20, -(-n // self.nthreads))
+        futs = []
+        for a in range(0, n, step):
+            e = min(n, a + step)
+            if self.arr is not None:
+                dst = np.frombuffer(mv[a:e], dtype=np.uint8)
+                futs.append(self.pool.submit(np.copyto, dst, self.arr[self.pos + a:self.pos + e]))
+            else:
+                futs.append(self.pool.submit(self._pread, mv[a:e], self.pos + a))
+        for fu in futs:
+            fu.result()
+        self.pos += n
         return n
 
 
@@ -132,11 +154,23 @@ def encode_file_sharded(path: str, rank: int, world: int, group=None, **kw) -> O
 
 
 class SegmentEncoder:
-    """Encode whole files into CESS fragments on one GPU."""
+    """Encode whole files into CESS fragments on one GPU.
+
+    hash_on = "host": SHA-256 on the host (hashlib / OpenSSL SHA-NI, `hash_threads` threads)
+    beside the GPU encode. hash_on = "gpu": every segment and fragment hash on the GPU through
+    the hash queue (cess_amd.hashq): each batch's chains are added after its encode and the
+    queue is ticked once per batch, so `window` batches (window x batch_segments x (k+m+1)
+    chains) hash together and a batch's records land `window` batches after its encode; the
+    window's segments stay resident in HBM until then (288 GB of HBM holds a window of tens of
+    GiB). "auto" picks the GPU when a batch alone has >= 2048 fragments (wide codes) and the
+    host otherwise (small files of the CESS geometry finish sooner on SHA-NI than through the
+    GPU's ~0.5 s per-chain latency for a 16 MiB segment).
+    """
 
     def __init__(self, k: int = geometry.DATA_SHARDS, m: int = geometry.PARITY_SHARDS,
                  segment_size: int = geometry.SEGMENT_SIZE, batch_segments: int = 64,
-                 device: int = 0, hash_on: str = "auto", hash_threads: int = 8):
+                 device: int = 0, hash_on: str = "auto", hash_threads: int = 8,
+                 window: int = 32):
         import torch
         if segment_size % k:
             raise ValueError("segment_size must be a multiple of k")
@@ -148,19 +182,42 @@ class SegmentEncoder:
         frags_per_batch = batch_segments * (k + m)
         self.hash_on = ("gpu" if frags_per_batch >= 2048 else "host") if hash_on == "auto" \
             else hash_on
+        if self.hash_on not in ("gpu", "host"):
+            raise ValueError("hash_on must be 'gpu', 'host' or 'auto'")
         self.pool = cf.ThreadPoolExecutor(max_workers=hash_threads)
+        self.io_threads = 8
+        self.io_pool = cf.ThreadPoolExecutor(max_workers=self.io_threads)
         self.streams = [torch.cuda.Stream(self.dev) for _ in range(2)]
         self.h_data = [torch.empty((batch_segments, k, self.F), dtype=torch.uint8,
                                    pin_memory=True) for _ in range(2)]
         self.h_par = [torch.empty((batch_segments, m, self.F), dtype=torch.uint8,
                                   pin_memory=True) for _ in range(2)]
+        self.W = max(1, window) if self.hash_on == "gpu" else 2
+        # GPU hashing: W + 1 device slots, so the slot a batch reuses was freed one tick
+        # before, and its H2D + encode overlap the current tick
+        nd = self.W + 1 if self.hash_on == "gpu" else 2
         self.d_data = [torch.empty((batch_segments, k, self.F), dtype=torch.uint8,
-                                   device=self.dev) for _ in range(2)]
+                                   device=self.dev) for _ in range(nd)]
         self.d_par = [torch.empty((batch_segments, m, self.F), dtype=torch.uint8,
-                                  device=self.dev) for _ in range(2)]
-        self.d_hex = [torch.empty((batch_segments, k + m, 64), dtype=torch.uint8,
-                                  device=self.dev) for _ in range(2)]
+                                  device=self.dev) for _ in range(nd)]
         self.events = [None, None]
+        if self.hash_on == "gpu":
+            from .hashq import HashQueue, sha256_blocks
+            self.hash_stream = torch.cuda.Stream(self.dev)
+            chains = self.W * batch_segments * (k + m + 1)
+            self.hq = HashQueue(capacity=1 << max(10, (chains - 1).bit_length()), device=device,
+                                stream=self.hash_stream)
+            # a segment chain completes `window` ticks after its add
+            self.tick_blocks = -(-sha256_blocks(segment_size) // self.W)
+            self.d_fhex = [torch.empty((batch_segments, k + m, 64), dtype=torch.uint8,
+                                       device=self.dev) for _ in range(nd)]
+            self.d_shex = [torch.empty((batch_segments, 64), dtype=torch.uint8,
+                                       device=self.dev) for _ in range(nd)]
+            self.h_fhex = [torch.empty((batch_segments, k + m, 64), dtype=torch.uint8,
+                                       pin_memory=True) for _ in range(nd)]
+            self.h_shex = [torch.empty((batch_segments, 64), dtype=torch.uint8,
+                                       pin_memory=True) for _ in range(nd)]
+            self.slot_free = [None] * nd  # event: slot's hashes copied out (slot reusable)
 
     def _read_batch(self, f: BinaryIO, slot: int) -> int:
         """Fill slot's pinned buffer with up to `batch` segments; returns segments read."""
@@ -181,96 +238,167 @@ class SegmentEncoder:
             buf[got:nseg * self.seg] = 0
         return nseg
 
-    def _launch(self, slot: int, nseg: int):
+    def _launch(self, slot: int, dslot: int, nseg: int):
         import torch
         st = self.streams[slot]
         with torch.cuda.stream(st):
-            self.d_data[slot][:nseg].copy_(self.h_data[slot][:nseg], non_blocking=True)
-            self.enc.EncodeBatch(self.d_data[slot], self.d_par[slot], nseg, self.F, stream=st)
+            if self.hash_on == "gpu" and self.slot_free[dslot] is not None:
+                st.wait_event(self.slot_free[dslot])  # batch dslot - W fully hashed
+            self.d_data[dslot][:nseg].copy_(self.h_data[slot][:nseg], non_blocking=True)
+            self.enc.EncodeBatch(self.d_data[dslot], self.d_par[dslot], nseg, self.F, stream=st)
             if self.hash_on == "gpu":
-                self.enc.Sha256Batch(self.d_data[slot], self.d_par[slot], nseg, self.F,
-                                     self.d_hex[slot], stream=st)
-            self.h_par[slot][:nseg].copy_(self.d_par[slot][:nseg], non_blocking=True)
+                ready = torch.cuda.Event()
+                ready.record(st)
+            self.h_par[slot][:nseg].copy_(self.d_par[dslot][:nseg], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(st)
         self.events[slot] = ev
+        if self.hash_on == "gpu":
+            k, m, F = self.k, self.m, self.F
+            self.hash_stream.wait_event(ready)
+            self.hq.add_fragments(self.d_data[dslot], self.d_par[dslot], nseg, k, m, F,
+                                  self.d_fhex[dslot])
+            return self.hq.add_segments(self.d_data[dslot], nseg, k * F, self.d_shex[dslot])
+        return None
+
+    def _copy_hashes(self, dslot: int, nseg: int):
+        """Enqueue the D2H of a completed batch's hex (on the hash stream, after its tick)."""
+        import torch
+        with torch.cuda.stream(self.hash_stream):
+            self.h_fhex[dslot][:nseg].copy_(self.d_fhex[dslot][:nseg], non_blocking=True)
+            self.h_shex[dslot][:nseg].copy_(self.d_shex[dslot][:nseg], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.hash_stream)
+        self.slot_free[dslot] = ev
+        return ev
 
     def _submit_host_hashes(self, slot: int, nseg: int):
-        """Segment hashes (and data-fragment hashes on the host path) need only the host copy:
-        start them as soon as the batch is read, beside the GPU work."""
+        """Host path: segment and data-fragment hashes need only the host copy, so they start
+        as soon as the batch is read, beside the GPU work."""
+        if self.hash_on != "host":
+            return None
         data = self.h_data[slot].numpy()
         seg_futs = [self.pool.submit(sha256_hex, memoryview(data[s].reshape(-1)))
                     for s in range(nseg)]
-        dfuts = None
-        if self.hash_on == "host":
-            dfuts = [[self.pool.submit(sha256_hex, memoryview(data[s, i]))
-                      for i in range(self.k)] for s in range(nseg)]
+        dfuts = [[self.pool.submit(sha256_hex, memoryview(data[s, i])) for i in range(self.k)]
+                 for s in range(nseg)]
         return seg_futs, dfuts
 
-    def _finish(self, slot: int, nseg: int, seg_base: int, futs, out: FileRecord,
-                on_fragment: Optional[Callable]) -> None:
+    def _finish_encode(self, slot: int, nseg: int, seg_base: int, futs,
+                       on_fragment: Optional[Callable]):
+        """Wait for a batch's encode + parity D2H; run the fragment callback; on the host path
+        also collect its hashes (returns the batch's SegmentLists then, else None)."""
         data = self.h_data[slot].numpy()
         k, m = self.k, self.m
-        seg_futs, dfuts = futs
         self.events[slot].synchronize()
         par = self.h_par[slot].numpy()
+        recs = None
         if self.hash_on == "host":
+            seg_futs, dfuts = futs
             pfuts = [[self.pool.submit(sha256_hex, memoryview(par[s, o])) for o in range(m)]
                      for s in range(nseg)]
-            frag = [[f.result() for f in dfuts[s]] + [f.result() for f in pfuts[s]]
+            recs = [SegmentList(seg_futs[s].result(),
+                                [f.result() for f in dfuts[s]] + [f.result() for f in pfuts[s]])
                     for s in range(nseg)]
-        else:
-            hexes = self.d_hex[slot][:nseg].cpu().numpy()
-            frag = [[hexes[s, i].tobytes() for i in range(k + m)] for s in range(nseg)]
-        for s in range(nseg):
-            out.segments.append(SegmentList(seg_futs[s].result(), frag[s]))
-            if on_fragment is not None:
+        if on_fragment is not None:
+            for s in range(nseg):
                 for i in range(k + m):
                     on_fragment(seg_base + s, i, data[s, i] if i < k else par[s, i - k])
+        return recs
+
+    def _gpu_records(self, dslot: int, nseg: int, ev) -> List[SegmentList]:
+        ev.synchronize()
+        fh = self.h_fhex[dslot][:nseg].numpy()
+        sh = self.h_shex[dslot][:nseg].numpy()
+        return [SegmentList(sh[s].tobytes(), [fh[s, i].tobytes() for i in range(self.k + self.m)])
+                for s in range(nseg)]
 
     def encode_range(self, path: str, seg_start: int, seg_stop: int,
                      on_fragment: Optional[Callable[[int, int, np.ndarray], None]] = None
                      ) -> FileRecord:
         """Encode segments [seg_start, seg_stop) of a file (one rank's shard of a file encoded
         across GPUs). `file_hash` of the result covers only this range's segments."""
-        with open(path, "rb") as f:
-            f.seek(seg_start * self.seg)
-            limited = io.BufferedReader(_Limited(f, (seg_stop - seg_start) * self.seg))
-            rec = self.encode_file(limited, on_fragment=on_fragment)
+        import os
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            size = os.fstat(fd).st_size
+            src = _ParallelReader(self.io_pool, self.io_threads, fd=fd, start=seg_start * self.seg,
+                                  stop=min(size, seg_stop * self.seg))
+            rec = self.encode_file(src, on_fragment=on_fragment)
+        finally:
+            os.close(fd)
         return rec
 
     def encode_file(self, src: Union[str, bytes, BinaryIO],
                     on_fragment: Optional[Callable[[int, int, np.ndarray], None]] = None
                     ) -> FileRecord:
-        """Encode a file (path, bytes or binary stream). `on_fragment(seg, idx, bytes)` sees
-        every fragment (e.g. to write it out) before its buffer is reused."""
-        if isinstance(src, bytes):
-            f, close = io.BytesIO(src), True
+        """Encode a file (path, bytes / uint8 array, or binary stream). `on_fragment(seg, idx, bytes)` sees
+        every fragment (e.g. to write it out) before its buffer is reused; on the GPU hash path
+        it runs before the fragment's hash is known."""
+        close_fd = None
+        if isinstance(src, (bytes, bytearray, memoryview, np.ndarray)):
+            arr = np.frombuffer(src, dtype=np.uint8) if not isinstance(src, np.ndarray) \
+                else src.reshape(-1).view(np.uint8)
+            f, close = _ParallelReader(self.io_pool, self.io_threads, arr=arr, stop=arr.size), False
         elif isinstance(src, str):
-            f, close = open(src, "rb"), True
+            import os
+            close_fd = os.open(src, os.O_RDONLY)
+            f = _ParallelReader(self.io_pool, self.io_threads, fd=close_fd,
+                                stop=os.fstat(close_fd).st_size)
+            close = False
         else:
             f, close = src, False
         out = FileRecord(b"", 0)
         self._bytes = 0
+        gpu = self.hash_on == "gpu"
+        inflight = []  # GPU path: [batch no, dslot, nseg, ticket, copy event or None]
         try:
-            pending = None  # (slot, nseg, seg_base)
-            seg_base, slot = 0, 0
+            pending = None  # (slot, nseg, seg_base, futs)
+            seg_base, i = 0, 0
             while True:
+                slot = i & 1
                 nseg = self._read_batch(f, slot)
                 futs = None
                 if nseg:
-                    self._launch(slot, nseg)
+                    dslot = i % len(self.d_data)
+                    if gpu:  # the slot's previous batch must be hashed and copied out first
+                        for b in inflight:
+                            if b[1] == dslot and b[4] is None:
+                                while not self.hq.done(b[3]):
+                                    self.hq.tick(self.tick_blocks)
+                                b[4] = self._copy_hashes(b[1], b[2])
+                    ticket = self._launch(slot, dslot, nseg)
                     futs = self._submit_host_hashes(slot, nseg)
+                    if gpu:
+                        inflight.append([i, dslot, nseg, ticket, None])
+                        self.hq.tick(self.tick_blocks)
+                if gpu and not nseg:
+                    self.hq.finish()
+                if gpu:
+                    for b in inflight:
+                        if b[4] is None and self.hq.done(b[3]):
+                            b[4] = self._copy_hashes(b[1], b[2])
                 if pending is not None:
-                    self._finish(*pending, out, on_fragment)
+                    recs = self._finish_encode(*pending, on_fragment)
+                    if recs is not None:
+                        out.segments.extend(recs)
+                # GPU records in batch order, once their hex copies are enqueued; the slot is
+                # reused W batches later, so wait for the oldest before it is overwritten
+                while gpu and inflight and inflight[0][4] is not None and (
+                        not nseg or len(inflight) >= len(self.d_data) or inflight[0][4].query()):
+                    _, dslot_, nseg_, _, ev = inflight.pop(0)
+                    out.segments.extend(self._gpu_records(dslot_, nseg_, ev))
                 if not nseg:
                     break
                 pending = (slot, nseg, seg_base, futs)
                 seg_base += nseg
-                slot ^= 1
+                i += 1
         finally:
             if close:
                 f.close()
+            if close_fd is not None:
+                import os
+                os.close(close_fd)
         if not out.segments:
             from .reedsolomon import ErrShortData
             raise ErrShortData(ErrShortData.__doc__)
@@ -280,5 +408,7 @@ class SegmentEncoder:
 
     def close(self):
         self.pool.shutdown(wait=True)
+        self.io_pool.shutdown(wait=True)
+        if self.hash_on == "gpu":
+            self.hq.close()
         self.enc.close()
-

@@ -93,6 +93,37 @@ int cec_sha256_batch(cec_codec* codec, const uint8_t* d_data, const uint8_t* d_p
 int cec_sha256_hex(const uint8_t* const* d_bufs, size_t n, size_t len, uint8_t* hex,
                    void* hip_stream);
 
+/* Hash queue: streaming SHA-256 of many long device buffers (fragment and segment hashes).
+ * Chains keep their state in HBM between launches, so one tick advances every live chain of
+ * every batch added so far; a producer that adds a batch per step and ticks once per step hashes
+ * a window of batches at once (one chain per buffer is serial, so the GPU's hash rate is the
+ * number of chains in flight times one wave's issue rate). All work is enqueued on the stream
+ * given at creation; buffers and hex outputs must stay valid until their add is complete.
+ * Completion is tracked on the host from the lengths alone (no read-back): an add is complete
+ * once the ticks enqueued so far cover its blocks, i.e. when the stream reaches that tick. */
+typedef struct cec_hashq cec_hashq;
+/* capacity: maximum live chains, a power of two (64 B of HBM each). */
+int cec_hashq_create(int device, size_t capacity, void* hip_stream, cec_hashq** out);
+/* Synchronises the queue's stream, then frees the table. */
+void cec_hashq_destroy(cec_hashq* q);
+/* Append n chains: buffer i is d_base + (i / per) * outer_stride + (i % per) * inner_stride, len
+ * bytes; its 64 lowercase hex chars go to d_hex + ((i / per) * hex_outer + i % per) * 64
+ * (d_hex NULL: no output). E.g. the fragments of a batch [nseg][k][F]: per = k, outer = k*F,
+ * inner = F; its segment hashes: per = 1, outer = inner = k*F, len = k*F. *ticket (optional)
+ * names the add. CEC_ENOMEM when the ring would overflow (tick first). */
+int cec_hashq_add(cec_hashq* q, const uint8_t* d_base, size_t n, size_t per, size_t outer_stride,
+                  size_t inner_stride, size_t len, uint8_t* d_hex, size_t hex_outer,
+                  uint64_t* ticket);
+/* Advance every live chain by at most max_blocks 64-byte blocks (0 = to completion). */
+int cec_hashq_tick(cec_hashq* q, uint32_t max_blocks);
+/* Tick until every chain added so far is complete (enqueued; synchronise the stream to wait). */
+int cec_hashq_finish(cec_hashq* q);
+/* Host-side status as of the ticks enqueued so far: *done = add `ticket` complete, *live_chains
+ * = chains not yet complete, *blocks_left = most blocks any live chain still needs. Any output
+ * pointer may be NULL. */
+int cec_hashq_status(const cec_hashq* q, uint64_t ticket, int* done, size_t* live_chains,
+                     uint64_t* blocks_left);
+
 /* klauspost Split for one segment (host memory): shard i = seg[i*shard_len, (i+1)*shard_len),
  * zero-padded past seg_len. Requires k*shard_len >= seg_len > 0. */
 int cec_split_segment(const uint8_t* seg, size_t seg_len, int k, uint8_t* const* shards,
@@ -103,14 +134,16 @@ int cec_split_segment(const uint8_t* seg, size_t seg_len, int k, uint8_t* const*
 int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t seg0,
                        uint64_t seed, void* hip_stream);
 
-/* Options (tuning / testing). CT_VARIANT, SHA_MODE and RT_MODE are process-wide kernel choices
- * (the codec argument may be any live handle); FORCE_GENERIC is per codec. */
+/* Options (tuning / testing). CT_VARIANT, SHA_MODE, RT_MODE and TICK_PREFETCH are process-wide
+ * kernel choices (the codec argument may be any live handle); FORCE_GENERIC is per codec. */
 #define CEC_OPT_FORCE_GENERIC 1 /* 1: always use the run-time-coefficient kernel */
 #define CEC_OPT_CT_VARIANT 2    /* compile-time kernel unroll/cache variant, -1 = default */
 #define CEC_OPT_SHA_MODE 3      /* SHA-256 kernel: 0 = auto, 1 = one wave per 64 buffers,
                                    2 = two waves (schedule producer + rounds consumer) */
 #define CEC_OPT_RT_MODE 4       /* run-time-coefficient kernel: 0 = Horner over input groups
                                    when 4 <= inputs <= 32, 1 = always the per-bit mask kernel */
+#define CEC_OPT_TICK_PREFETCH 5  /* hash-queue tick: message blocks the producer wave loads ahead
+                                   (1 or 2) */
 int cec_set_option(cec_codec* codec, int option, int value);
 
 #ifdef __cplusplus

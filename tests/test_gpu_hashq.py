@@ -1,0 +1,143 @@
+"""GPU hash queue (cec_hashq_*): streaming SHA-256 with chain state in HBM, against hashlib and
+the reference's own NIST SHAVS vectors (utils/ring/third_party/NIST/SHAVS, copied as data into
+tests/golden/), through ticks of every size, interleaved adds, unaligned buffers and the
+segment/fragment layouts of SegmentList (c-pallets/file-bank/src/types.rs:13-16)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from tests.conftest import parse_shavs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need a GPU"
+    t.cuda.init()
+    return t
+
+
+@pytest.fixture(scope="module")
+def cess(torch):
+    import cess_amd
+    return cess_amd
+
+
+def hexes(t):
+    return [bytes(r).decode() for r in t.cpu().numpy().reshape(-1, 64)]
+
+
+def test_shavs_through_queue(torch, cess):
+    """Every NIST short/long message as its own chain at an odd device offset, ticked a few
+    blocks at a time while more messages are added."""
+    vecs = parse_shavs("SHA256ShortMsg.rsp") + parse_shavs("SHA256LongMsg.rsp")
+    offs, pos = [], 0
+    for msg, _ in vecs:
+        offs.append(pos + 3)  # 3: every buffer start unaligned
+        pos += len(msg) + 3
+    buf = np.zeros(pos + 64, np.uint8)
+    for (msg, _), o in zip(vecs, offs):
+        buf[o:o + len(msg)] = np.frombuffer(msg, np.uint8)
+    d = torch.from_numpy(buf).cuda()
+    d_hex = torch.zeros((len(vecs), 64), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    with cess.HashQueue(capacity=1024, stream=st) as q:
+        tickets = []
+        for i, ((msg, _), o) in enumerate(zip(vecs, offs)):
+            tickets.append(q.add(d.data_ptr() + o, 1, 1, 0, 0, len(msg), d_hex, 1, i * 64))
+            if i % 7 == 0:
+                q.tick(2)
+        q.finish()
+        assert all(q.done(t) for t in tickets) and q.live_chains == 0
+        torch.cuda.synchronize()
+    got = hexes(d_hex)
+    for (msg, md), g in zip(vecs, got):
+        assert g == md, (len(msg), g, md)
+
+
+@pytest.mark.parametrize("k,m,F", [(2, 1, 65536), (4, 2, 4160), (32, 32, 1000), (2, 1, 56)])
+@pytest.mark.parametrize("max_blocks", [1, 37, 0])
+def test_batch_window(torch, cess, k, m, F, max_blocks):
+    """Fragments + segment hashes of several batches added one per step, one tick per step
+    (a window of batches in flight), then drained: every hex matches hashlib."""
+    nseg, nbatch = 5, 4
+    rng = np.random.default_rng(k * 1000 + F + max_blocks)
+    data = rng.integers(0, 256, (nbatch, nseg, k, F), dtype=np.uint8)
+    par = rng.integers(0, 256, (nbatch, nseg, m, F), dtype=np.uint8)
+    d_data, d_par = torch.from_numpy(data).cuda(), torch.from_numpy(par).cuda()
+    d_fhex = torch.zeros((nbatch, nseg, k + m, 64), dtype=torch.uint8, device="cuda")
+    d_shex = torch.zeros((nbatch, nseg, 64), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    q = cess.HashQueue(capacity=2048, stream=st)
+    tickets = []
+    for b in range(nbatch):
+        t1 = q.add_fragments(d_data[b], d_par[b], nseg, k, m, F, d_fhex[b])
+        t2 = q.add_segments(d_data[b], nseg, k * F, d_shex[b])
+        tickets.append((t1, t2))
+        q.tick(max_blocks)
+        if max_blocks == 0:
+            assert q.done(t1) and q.done(t2)
+    need = cess.sha256_blocks(k * F)
+    if max_blocks and need > max_blocks * nbatch:
+        assert not q.done(tickets[0][1])
+    q.finish()
+    torch.cuda.synchronize()
+    assert q.live_chains == 0 and all(q.done(t) for tt in tickets for t in tt)
+    q.close()
+    fh = np.array(hexes(d_fhex)).reshape(nbatch, nseg, k + m)
+    sh = np.array(hexes(d_shex)).reshape(nbatch, nseg)
+    for b in range(nbatch):
+        for s in range(nseg):
+            assert sh[b, s] == hashlib.sha256(data[b, s].tobytes()).hexdigest()
+            for i in range(k + m):
+                frag = data[b, s, i] if i < k else par[b, s, i - k]
+                assert fh[b, s, i] == hashlib.sha256(frag.tobytes()).hexdigest(), (b, s, i)
+
+
+def test_matches_batch_kernel_full_geometry(torch, cess):
+    """Config-5 geometry (64 segments of 32 x 512 KiB data + 32 parity): the queue's hexes equal
+    the one-shot batch kernel's (k_sha256_2w) for all 4096 fragments; a sample vs hashlib."""
+    k, m, F, nseg = 32, 32, 512 * 1024, 64
+    d_data = torch.empty((nseg, k, F), dtype=torch.uint8, device="cuda")
+    d_par = torch.empty((nseg, m, F), dtype=torch.uint8, device="cuda")
+    cess.fill_synthetic(d_data, k * F, nseg, 0, 0xCE550005)
+    enc = cess.New(k, m)
+    enc.EncodeBatch(d_data, d_par, nseg, F)
+    a = torch.zeros((nseg, k + m, 64), dtype=torch.uint8, device="cuda")
+    b = torch.zeros_like(a)
+    enc.Sha256Batch(d_data, d_par, nseg, F, a)
+    q = cess.HashQueue(capacity=1 << 13, stream=torch.cuda.current_stream())
+    q.add_fragments(d_data, d_par, nseg, k, m, F, b)
+    while q.live_chains:
+        q.tick(1000)
+    torch.cuda.synchronize()
+    q.close()
+    assert torch.equal(a, b)
+    got = hexes(b)
+    for s, i in [(0, 0), (17, 31), (63, 32), (40, 63)]:
+        src = d_data[s, i] if i < k else d_par[s, i - k]
+        assert got[s * (k + m) + i] == hashlib.sha256(src.cpu().numpy().tobytes()).hexdigest()
+
+
+def test_edge_cases(torch, cess):
+    """Empty chains, lengths around the 55/56/64-byte padding boundaries, a full ring."""
+    lens = [0, 1, 55, 56, 57, 63, 64, 65, 119, 120, 128]
+    buf = np.arange(256, dtype=np.uint8)
+    d = torch.from_numpy(buf).cuda()
+    d_hex = torch.zeros((len(lens), 64), dtype=torch.uint8, device="cuda")
+    q = cess.HashQueue(capacity=16, stream=torch.cuda.current_stream())
+    for i, ln in enumerate(lens):
+        q.add(d, 1, 1, 0, 0, ln, d_hex, 1, i * 64)
+    with pytest.raises(cess.CecError):
+        q.add(d, 6, 1, 0, 0, 10, None)  # 11 live + 6 > 16
+    q.tick(1)
+    q.add(d, 5, 1, 1, 1, 10, None)  # 1-block chains completed: room again
+    q.finish()
+    torch.cuda.synchronize()
+    q.close()
+    got = hexes(d_hex)
+    for ln, g in zip(lens, got):
+        assert g == hashlib.sha256(buf[:ln].tobytes()).hexdigest(), ln

@@ -294,18 +294,20 @@ def test_sha256_batch_matches_hashlib(torch, cess, sha_mode):
                 assert hx[s, i].tobytes().decode() == sha(buf)
 
 
-@pytest.mark.parametrize("size,seg,k,m,hash_on", [
-    (3 * (1 << 20) + 12345, 1 << 20, 2, 1, "host"),
-    (5 * (1 << 20) + 7, 1 << 20, 2, 1, "gpu"),
-    (2 * (1 << 20) - 5, 1 << 19, 32, 32, "auto"),
-    (40 * MiB + 3, 16 * MiB, 2, 1, "auto"),
+@pytest.mark.parametrize("size,seg,k,m,hash_on,window", [
+    (3 * (1 << 20) + 12345, 1 << 20, 2, 1, "host", 32),
+    (5 * (1 << 20) + 7, 1 << 20, 2, 1, "gpu", 32),
+    (9 * (1 << 20) + 7, 1 << 20, 2, 1, "gpu", 2),   # device slots reused (5 batches, window 2)
+    (7 * (1 << 19) + 1, 1 << 19, 4, 2, "gpu", 1),
+    (2 * (1 << 20) - 5, 1 << 19, 32, 32, "auto", 32),
+    (40 * MiB + 3, 16 * MiB, 2, 1, "auto", 32),
 ])
-def test_segment_list_pipeline(torch, cess, orc, size, seg, k, m, hash_on):
+def test_segment_list_pipeline(torch, cess, orc, size, seg, k, m, hash_on, window):
     """§8f rank 1: file -> segments -> fragments -> SegmentList, vs the oracle."""
     from cess_amd.segments import SegmentEncoder, check_file_spec, needed_space
     rng = np.random.default_rng(size)
     blob = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
-    se = SegmentEncoder(k, m, seg, batch_segments=2, hash_on=hash_on)
+    se = SegmentEncoder(k, m, seg, batch_segments=2, hash_on=hash_on, window=window)
     frags = {}
     rec = se.encode_file(blob, on_fragment=lambda s, i, b: frags.__setitem__((s, i), sha(b)))
     se.close()

@@ -3,9 +3,8 @@
 bench `value`): a synthetic in-memory file is read through pinned buffers, copied to HBM,
 encoded, parity copied back and every segment/fragment hashed (host SHA-NI or GPU SHA-256).
 
-usage: python tools/e2e_bench.py [--gib 2] [--k 2 --m 1] [--hash auto|host|gpu]"""
+usage: python tools/e2e_bench.py [--gib 2] [--k 2 --m 1] [--hash auto|host|gpu] [--window W]"""
 import argparse
-import io
 import json
 import os
 import sys
@@ -24,6 +23,7 @@ def main():
     ap.add_argument("--m", type=int, default=1)
     ap.add_argument("--hash", default="auto")
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--window", type=int, default=32, help="GPU hash queue window (batches)")
     args = ap.parse_args()
     from cess_amd.segments import SegmentEncoder
     from oracle.c_oracle import load_c_oracle
@@ -32,16 +32,16 @@ def main():
     buf = np.empty(nseg * seg, np.uint8)
     load_c_oracle().orc_fill_synthetic(buf.ctypes.data, seg, nseg, 0, 0xCE550009)
     se = SegmentEncoder(args.k, args.m, seg, batch_segments=64, hash_on=args.hash,
-                        hash_threads=args.threads)
-    se.encode_file(io.BytesIO(buf[: 64 * seg].tobytes()))  # warm-up (allocations, pools)
-    f = io.BytesIO(memoryview(buf))
+                        hash_threads=args.threads, window=args.window)
+    se.encode_file(buf[: 64 * seg])  # warm-up (allocations, pools)
     t0 = time.perf_counter()
-    rec = se.encode_file(f)
+    rec = se.encode_file(buf)  # in-memory file, copied into pinned buffers by 8 threads
     dt = time.perf_counter() - t0
     se.close()
     print(json.dumps({"e2e_GBps_file_bytes": round(nseg * seg / dt / 1e9, 2), "seconds": round(dt, 3),
                       "segments": len(rec.segments), "k": args.k, "m": args.m,
-                      "hash_on": se.hash_on, "threads": args.threads}))
+                      "hash_on": se.hash_on, "threads": args.threads,
+                      "window": args.window if se.hash_on == "gpu" else None}))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,8 @@
+set -u
+cd $GRAFT_REPO_ROOT; OUT=$PWD/gpurun_out/r01s; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_hashq.py tests/test_gpu_parity.py -k "hashq or shavs or window or geometry or edge_cases or segment_list" -x -v --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
+for w in 1 4 16 32; do
+  timeout -k 10 200 python -u bench.py --config 5 --window $w --steps 60 --warmup 5 --no-cpu-baseline > $OUT/c5_w$w.json 2>&1 || { tail $OUT/c5_w$w.json; exit 1; }
+  python -c "import json;d=json.loads(open('$OUT/c5_w$w.json').read().strip().splitlines()[-1]);print('w=$w', d['value'], d['ms_per_step'], d['roofline']['achieved'], d['sha256'])"
+done
