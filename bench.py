@@ -128,6 +128,8 @@ def main() -> None:
     ap.add_argument("--sha-mode", type=int, default=0, help="0 auto, 1 one wave, 2 two waves")
     ap.add_argument("--window", type=int, default=16,
                     help="config 5: batches hashing at once in the GPU hash queue")
+    ap.add_argument("--hash-stream", type=int, default=0,
+                    help="config 5: 1 = hash queue on a second stream, 0 = after the encode")
     ap.add_argument("--tick-pf", type=int, default=0,
                     help="hash-queue tick prefetch depth (1 or 2; 0 = library default)")
     ap.add_argument("--rt-mode", type=int, default=0,
@@ -207,7 +209,9 @@ def main() -> None:
         NB = W + 1
         pipe_par = [d_par] + [torch.empty_like(d_par) for _ in range(NB - 1)]
         pipe_hex = [d_hex] + [torch.empty_like(d_hex) for _ in range(NB - 1)]
-        sha_stream = torch.cuda.Stream(dev)
+        # --hash-stream 1: hash queue on its own stream (ticks overlap the next encode);
+        # 0: one stream, encode then tick (the tick keeps the whole chip)
+        sha_stream = torch.cuda.Stream(dev) if args.hash_stream else stream
         chains = W * nseg * (k + m)
         hq = cess_amd.HashQueue(capacity=1 << max(10, (chains - 1).bit_length()), device=local,
                                 stream=sha_stream)
@@ -238,7 +242,8 @@ def main() -> None:
     def drain():
         if args.config == 5:
             hq.finish()
-            stream.wait_stream(sha_stream)
+            if sha_stream is not stream:
+                stream.wait_stream(sha_stream)
 
     def step_codec():  # the codec kernel alone (config 5's step also hashes)
         if args.config in (3, 6, 7):
@@ -328,8 +333,10 @@ def main() -> None:
                     "window": W, "chains_in_flight": W * nseg * (k + m),
                     "tick_blocks": tick_blocks,
                     "pipeline": f"GPU hash queue: batch i's {nseg * (k + m)} fragment chains "
-                                f"hash over ticks i..i+{W - 1} (one tick per step, on a second "
-                                "stream); the timed region ends with the window drained",
+                                f"hash over ticks i..i+{W - 1} (one tick per step, "
+                                + ("on a second stream" if args.hash_stream else
+                                   "after the step's encode") +
+                                "); the timed region ends with the window drained",
                     "note": "SHA-256 is one sequential chain per fragment: bounded by streams x "
                             "per-wave issue rate, reported apart from the HBM roofline"}
 

@@ -386,7 +386,7 @@ int cec_set_option(cec_codec* c, int option, int value) {
       cec::set_rt_mode(value);
       return CEC_OK;
     case CEC_OPT_TICK_PREFETCH:
-      if (value < 1 || value > 2) return set_err(CEC_EINVAL, "tick prefetch must be 1 or 2");
+      if (value < 0 || value > 3) return set_err(CEC_EINVAL, "tick variant must be 0..3");
       cec::set_tick_prefetch(value);
       return CEC_OK;
   }

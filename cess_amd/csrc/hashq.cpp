@@ -125,9 +125,12 @@ int cec_hashq_tick(cec_hashq* q, uint32_t max_blocks) {
     for (const auto& a : q->adds) most = std::max(most, a.blocks - a.done);
     max_blocks = (uint32_t)std::min<uint64_t>(most, 0xFFFFFFFFull);
   }
+  uint64_t live = 0;
+  for (const auto& a : q->adds)
+    if (a.done < a.blocks) live += a.n;
   HQ_TRY(hipSetDevice(q->device));
   cec::launch_sha256_tick(q->tab, q->cap - 1, q->head, (uint32_t)(q->tail - q->head), max_blocks,
-                          q->stream);
+                          live, q->stream);
   int rc = launched();
   if (rc) return rc;
   for (auto& a : q->adds) a.done += std::min<uint64_t>(max_blocks, a.blocks - a.done);

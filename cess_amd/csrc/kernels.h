@@ -89,9 +89,10 @@ inline uint64_t sha256_blocks(uint64_t len) { return (len >> 6) + ((len & 63) >=
 void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
                       const uint8_t* base, uint32_t per, uint64_t outer, uint64_t inner,
                       uint64_t len, uint8_t* hex, uint64_t hex_outer, hipStream_t st);
-// Advance the n chains in slots head.. by at most max_blocks blocks each.
+// Advance the n chains in slots head.. by at most max_blocks blocks each; `live` (chains not
+// yet complete among them) picks the kernel form.
 void launch_sha256_tick(ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,
-                        uint32_t max_blocks, hipStream_t st);
+                        uint32_t max_blocks, uint64_t live, hipStream_t st);
 
 // Synthetic segment bytes: 64-bit word w of segment s = splitmix64(seed ^ (s << 32) ^ w),
 // little-endian; segments are seg_bytes long and contiguous from `out`.

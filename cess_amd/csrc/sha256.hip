@@ -13,7 +13,9 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // ---------------------------------------------------------------------------------------------
 // SHA-256 (FIPS 180-4), one lane per buffer.
 // ---------------------------------------------------------------------------------------------
-__constant__ uint32_t kSha256K[64] = {
+// Round constants as compile-time literals: after unrolling each becomes an instruction literal,
+// not 64 scalar loads hoisted into SGPRs (which spilled to VGPR lanes).
+static constexpr uint32_t kSha256K[64] = {
     0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
     0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
     0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
@@ -334,6 +336,53 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return v;
 }
 
+// Message block `g` of a chain for the rare cases (unaligned buffer, padding block): the bytes
+// go through this lane's 64-byte LDS stage (final big-endian words) one at a time, so a single load is in flight and the
+// path costs a few VGPRs (64 unrolled byte loads would raise the whole kernel's VGPR count and
+// cut its occupancy). Block g < nfull is message data; the first padding block holds the last
+// r bytes and 0x80; the last block ends with the 64-bit big-endian bit length.
+// `stage` holds the block's 16 words as 4 x u32x4 at a stride of `qstride` u32x4 (1: a lane's
+// own 64 bytes; 64: this lane's column of a [4][64] u32x4 ring buffer).
+__device__ __noinline__ void sha_stage_general(const uint8_t* src, uint64_t g, uint64_t nfull,
+                                               uint32_t r, uint64_t nb, uint64_t len,
+                                               u32x4* stage, uint32_t qstride) {
+  const uint8_t* p = src + (g << 6);
+  const uint32_t nbytes = g < nfull ? 64u : (g == nfull ? r : 0u);
+  const uint32_t mark = g == nfull ? r : 64u;  // where the 0x80 goes (first padding block)
+#pragma unroll 1
+  for (uint32_t j = 0; j < 64; ++j)
+    reinterpret_cast<uint8_t*>(stage + (j >> 4) * qstride)[j & 15] =
+        j < nbytes ? p[j] : (j == mark ? 0x80 : 0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    u32x4 v = stage[q * qstride];
+    v = u32x4{__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z),
+              __builtin_bswap32(v.w)};
+    if (q == 3 && g == nb - 1) {
+      const uint64_t bits = len << 3;
+      v.z = (uint32_t)(bits >> 32);
+      v.w = (uint32_t)bits;
+    }
+    stage[q * qstride] = v;
+  }
+}
+
+// The general block through the stage (the callee never sees `w`, so it stays in registers).
+__device__ __forceinline__ void sha_block_general(uint32_t (&w)[16], const uint8_t* src,
+                                                  uint64_t g, uint64_t nfull, uint32_t r,
+                                                  uint64_t nb, uint64_t len, u32x4* stage,
+                                                  uint32_t qstride) {
+  sha_stage_general(src, g, nfull, r, nb, len, stage, qstride);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const u32x4 v = stage[q * qstride];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+}
+
 #define CEC_SHA_AI __attribute__((always_inline))
 
 template <int PF>
@@ -408,47 +457,10 @@ __global__ __launch_bounds__(128) void k_sha256_tick(ShaChain* __restrict__ tab,
         ++b;
       }
     for (; b < trips; ++b) {
-      const uint64_t g = blk0 + b;
       uint32_t w[16];
-      if (b < nblk && g < nfull) {
-        const uint8_t* p = src + (g << 6);
-        if (al16) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const u32x4 v = *reinterpret_cast<const u32x4*>(p + 16 * q);
-            w[4 * q + 0] = __builtin_bswap32(v.x);
-            w[4 * q + 1] = __builtin_bswap32(v.y);
-            w[4 * q + 2] = __builtin_bswap32(v.z);
-            w[4 * q + 3] = __builtin_bswap32(v.w);
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < 16; ++q)
-            w[q] = (uint32_t)p[4 * q] << 24 | (uint32_t)p[4 * q + 1] << 16 |
-                   (uint32_t)p[4 * q + 2] << 8 | (uint32_t)p[4 * q + 3];
-        }
-      } else if (b < nblk) {
-        // padding block(s): remaining r bytes, 0x80, zeros, 64-bit big-endian bit length
-        const bool first_pad = g == nfull;
-        const uint8_t* p = src + (nfull << 6);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          uint32_t word = 0;
-          if (first_pad) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-              const uint32_t pos = 4 * q + s;
-              const uint32_t byte = pos < r ? p[pos] : (pos == r ? 0x80u : 0u);
-              word |= byte << (24 - 8 * s);
-            }
-          }
-          w[q] = word;
-        }
-        if (g == nb - 1) {
-          const uint64_t bits = len << 3;
-          w[14] = (uint32_t)(bits >> 32);
-          w[15] = (uint32_t)bits;
-        }
+      if (b < nblk) {
+        // staged in the ring buffer this block is about to be written to (consumed at b - 2)
+        sha_block_general(w, src, blk0 + b, nfull, r, nb, len, &ring[b & 1][0][lane], 64);
       } else {
 #pragma unroll
         for (int q = 0; q < 16; ++q) w[q] = 0;
@@ -495,6 +507,66 @@ __global__ __launch_bounds__(128) void k_sha256_tick(ShaChain* __restrict__ tab,
   }
 }
 
+// One-wave tick: each lane expands its own message schedule in registers (no LDS, no barrier).
+// Per block it issues the whole ~1460 VALU ops on one wave instead of splitting them over a
+// producer and a consumer wave, so it loses in the latency regime (few chains: one wave's issue
+// rate is the bound) and can win in the throughput regime (several waves per SIMD interleave,
+// and no barrier ties a consumer to its producer).
+__global__ __launch_bounds__(64) void k_sha256_tick1(ShaChain* __restrict__ tab, uint32_t mask,
+                                                     uint64_t head, uint32_t n,
+                                                     uint32_t max_blocks) {
+  __shared__ u32x4 stage[64][4];  // general-path byte staging
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  ShaChain* ch_ = &tab[(uint32_t)(head + i) & mask];
+  const uint64_t len = ch_->len, blk0 = ch_->blk;
+  const uint64_t nfull = len >> 6;
+  const uint32_t r = (uint32_t)(len & 63);
+  const uint64_t nb = nfull + (r >= 56 ? 2 : 1);
+  const uint64_t rem = nb - blk0;
+  const uint32_t nblk = rem < max_blocks ? (uint32_t)rem : max_blocks;
+  if (nblk == 0) return;
+  const uint8_t* src = ch_->src;
+  uint32_t h[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) h[q] = ch_->h[q];
+  const bool al16 = ((uintptr_t)src & 15) == 0;
+  const uint64_t dat = blk0 < nfull ? nfull - blk0 : 0;
+  const uint32_t nfast = al16 ? (uint32_t)(dat < nblk ? dat : nblk) : 0u;
+  uint32_t w[16];
+  u32x4 nx[4] = {};
+  if (nfast) {
+    const uint8_t* p = src + (blk0 << 6);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+  }
+  // one compression per iteration (a second inlined copy of the rounds doubles the VGPRs)
+  for (uint32_t b = 0; b < nblk; ++b) {
+    const uint64_t g = blk0 + b;
+    if (b < nfast) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w[4 * q + 0] = __builtin_bswap32(nx[q].x);
+        w[4 * q + 1] = __builtin_bswap32(nx[q].y);
+        w[4 * q + 2] = __builtin_bswap32(nx[q].z);
+        w[4 * q + 3] = __builtin_bswap32(nx[q].w);
+      }
+      if (b + 1 < nfast) {
+        const uint8_t* p = src + ((g + 1) << 6);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+      }
+    } else {
+      sha_block_general(w, src, g, nfull, r, nb, len, &stage[threadIdx.x][0], 1);
+    }
+    sha256_block(h, w);
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) ch_->h[q] = h[q];
+  ch_->blk = blk0 + nblk;
+  if (blk0 + nblk == nb && ch_->hex) sha_store_hex(ch_->hex, h);
+}
+
 // Initialise n chains in queue slots slot0.. (mod capacity): buffer i starts at
 // base + (i / per) * outer + (i % per) * inner and its hex goes to
 // hex + ((i / per) * hex_outer + i % per) * 64.
@@ -524,9 +596,10 @@ int g_sha_mode = 0;  // 0 auto, 1 one wave, 2 two waves per 64 buffers
 void set_sha_mode(int v) { g_sha_mode = v; }
 
 namespace {
-int g_tick_pf = 1;  // hash-queue tick: message blocks loaded ahead by the producer wave (1 or 2)
+// hash-queue tick: 0 auto, 1 or 2 = two-wave kernel loading that many blocks ahead, 3 = one-wave
+int g_tick_pf = 0;
 }
-void set_tick_prefetch(int v) { g_tick_pf = v == 2 ? 2 : 1; }
+void set_tick_prefetch(int v) { g_tick_pf = v >= 0 && v <= 3 ? v : 0; }
 
 
 void launch_sha256_hex(const uint8_t* const* ptrs, const Layout* L, int nshards, uint64_t n,
@@ -554,9 +627,16 @@ void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
 }
 
 void launch_sha256_tick(ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,
-                        uint32_t max_blocks, hipStream_t st) {
+                        uint32_t max_blocks, uint64_t live, hipStream_t st) {
   if (n == 0 || max_blocks == 0) return;
-  if (g_tick_pf == 2)
+  // auto (0): the two-wave kernel while live chains are few (one wave's issue rate bounds a
+  // chain), the one-wave kernel once 2^17 live chains give every SIMD several waves (measured
+  // crossover, profiles/r01/sha_scale_*.jsonl)
+  const int v = g_tick_pf ? g_tick_pf : (live >= (1u << 17) ? 3 : 1);
+  if (v == 3)
+    hipLaunchKernelGGL(k_sha256_tick1, dim3((n + 63) / 64), dim3(64), 0, st, tab, mask, head, n,
+                       max_blocks);
+  else if (v == 2)
     hipLaunchKernelGGL(k_sha256_tick<2>, dim3((n + 63) / 64), dim3(128), 0, st, tab, mask, head,
                        n, max_blocks);
   else

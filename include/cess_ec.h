@@ -142,8 +142,9 @@ int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t s
                                    2 = two waves (schedule producer + rounds consumer) */
 #define CEC_OPT_RT_MODE 4       /* run-time-coefficient kernel: 0 = Horner over input groups
                                    when 4 <= inputs <= 32, 1 = always the per-bit mask kernel */
-#define CEC_OPT_TICK_PREFETCH 5  /* hash-queue tick: message blocks the producer wave loads ahead
-                                   (1 or 2) */
+#define CEC_OPT_TICK_PREFETCH 5  /* hash-queue tick kernel: 0 = auto by live chains, 1 or 2 =
+                                   two waves (schedule producer loading 1 or 2 blocks ahead +
+                                   rounds consumer), 3 = one wave per 64 chains */
 int cec_set_option(cec_codec* codec, int option, int value);
 
 #ifdef __cplusplus

@@ -26,11 +26,21 @@ def cess(torch):
     return cess_amd
 
 
+@pytest.fixture(params=[1, 2, 3], ids=["tick2w", "tick2w_pf2", "tick1w"])
+def tick_variant(cess, request):
+    """Every test below runs on each tick kernel (CEC_OPT_TICK_PREFETCH, process-wide)."""
+    enc = cess.New(2, 1)
+    enc.set_option(5, request.param)
+    yield request.param
+    enc.set_option(5, 0)
+    enc.close()
+
+
 def hexes(t):
     return [bytes(r).decode() for r in t.cpu().numpy().reshape(-1, 64)]
 
 
-def test_shavs_through_queue(torch, cess):
+def test_shavs_through_queue(torch, cess, tick_variant):
     """Every NIST short/long message as its own chain at an odd device offset, ticked a few
     blocks at a time while more messages are added."""
     vecs = parse_shavs("SHA256ShortMsg.rsp") + parse_shavs("SHA256LongMsg.rsp")
@@ -60,7 +70,7 @@ def test_shavs_through_queue(torch, cess):
 
 @pytest.mark.parametrize("k,m,F", [(2, 1, 65536), (4, 2, 4160), (32, 32, 1000), (2, 1, 56)])
 @pytest.mark.parametrize("max_blocks", [1, 37, 0])
-def test_batch_window(torch, cess, k, m, F, max_blocks):
+def test_batch_window(torch, cess, k, m, F, max_blocks, tick_variant):
     """Fragments + segment hashes of several batches added one per step, one tick per step
     (a window of batches in flight), then drained: every hex matches hashlib."""
     nseg, nbatch = 5, 4
@@ -97,7 +107,7 @@ def test_batch_window(torch, cess, k, m, F, max_blocks):
                 assert fh[b, s, i] == hashlib.sha256(frag.tobytes()).hexdigest(), (b, s, i)
 
 
-def test_matches_batch_kernel_full_geometry(torch, cess):
+def test_matches_batch_kernel_full_geometry(torch, cess, tick_variant):
     """Config-5 geometry (64 segments of 32 x 512 KiB data + 32 parity): the queue's hexes equal
     the one-shot batch kernel's (k_sha256_2w) for all 4096 fragments; a sample vs hashlib."""
     k, m, F, nseg = 32, 32, 512 * 1024, 64
@@ -122,7 +132,7 @@ def test_matches_batch_kernel_full_geometry(torch, cess):
         assert got[s * (k + m) + i] == hashlib.sha256(src.cpu().numpy().tobytes()).hexdigest()
 
 
-def test_edge_cases(torch, cess):
+def test_edge_cases(torch, cess, tick_variant):
     """Empty chains, lengths around the 55/56/64-byte padding boundaries, a full ring."""
     lens = [0, 1, 55, 56, 57, 63, 64, 65, 119, 120, 128]
     buf = np.arange(256, dtype=np.uint8)

@@ -26,11 +26,21 @@ def main():
     ap.add_argument("--window", type=int, default=32, help="GPU hash queue window (batches)")
     args = ap.parse_args()
     from cess_amd.segments import SegmentEncoder
-    from oracle.c_oracle import load_c_oracle
     seg = 16 << 20
     nseg = int(args.gib * (1 << 30)) // seg
+    # synthetic file bytes: the codec's own splitmix64 generator on the GPU, copied out in 1 GiB
+    # pieces into host memory (the in-memory "file" the pipeline then reads)
+    import torch
+    import cess_amd
     buf = np.empty(nseg * seg, np.uint8)
-    load_c_oracle().orc_fill_synthetic(buf.ctypes.data, seg, nseg, 0, 0xCE550009)
+    piece = 64
+    d = torch.empty(piece * seg, dtype=torch.uint8, device="cuda")
+    hb = torch.from_numpy(buf)
+    for s0 in range(0, nseg, piece):
+        n = min(piece, nseg - s0)
+        cess_amd.fill_synthetic(d, seg, n, s0, 0xCE550009)
+        hb[s0 * seg:(s0 + n) * seg].copy_(d[:n * seg])
+    del d
     se = SegmentEncoder(args.k, args.m, seg, batch_segments=64, hash_on=args.hash,
                         hash_threads=args.threads, window=args.window)
     se.encode_file(buf[: 64 * seg])  # warm-up (allocations, pools)

@@ -17,7 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=256)
     ap.add_argument("--stride", type=int, default=512 * 1024)
-    ap.add_argument("--pf", type=int, default=1)
+    ap.add_argument("--pf", type=int, default=0, help="tick kernel (0 auto, 1/2 two-wave, 3 one-wave)")
     ap.add_argument("--chains", default="4096,16384,32768,65536,98304,131072")
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
@@ -31,6 +31,10 @@ def main():
     buf = torch.empty(nmax * stride, dtype=torch.uint8, device="cuda")
     cess_amd.fill_synthetic(buf, stride, nmax, 0, 7)
     st = torch.cuda.Stream()
+    with cess_amd.HashQueue(capacity=1 << 10, stream=st) as q:  # warm-up (code load, clocks)
+        q.add(buf, 1024, 1, stride, stride, ln, None)
+        q.finish()
+        st.synchronize()
     for n in [int(c) for c in args.chains.split(",")]:
         q = cess_amd.HashQueue(capacity=1 << max(10, (n - 1).bit_length()), stream=st)
         times = []
