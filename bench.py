@@ -126,9 +126,9 @@ def main() -> None:
                     help="segments per GPU (default: the config's; config 5 at 1024 = 16 GiB in "
                          "flight, enough fragments to give every SIMD a SHA-256 wave)")
     ap.add_argument("--sha-mode", type=int, default=0, help="0 auto, 1 one wave, 2 two waves")
-    ap.add_argument("--window", type=int, default=16,
+    ap.add_argument("--window", type=int, default=64,
                     help="config 5: batches hashing at once in the GPU hash queue")
-    ap.add_argument("--hash-stream", type=int, default=0,
+    ap.add_argument("--hash-stream", type=int, default=1,
                     help="config 5: 1 = hash queue on a second stream, 0 = after the encode")
     ap.add_argument("--tick-pf", type=int, default=0,
                     help="hash-queue tick prefetch depth (1 or 2; 0 = library default)")

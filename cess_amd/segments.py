@@ -162,9 +162,10 @@ class SegmentEncoder:
     queue is ticked once per batch, so `window` batches (window x batch_segments x (k+m+1)
     chains) hash together and a batch's records land `window` batches after its encode; the
     window's segments stay resident in HBM until then (288 GB of HBM holds a window of tens of
-    GiB). "auto" picks the GPU when a batch alone has >= 2048 fragments (wide codes) and the
-    host otherwise (small files of the CESS geometry finish sooner on SHA-NI than through the
-    GPU's ~0.5 s per-chain latency for a 16 MiB segment).
+    GiB). "auto" picks the GPU when a batch alone has >= 2048 fragments (wide codes) or the
+    source is known to hold >= AUTO_GPU_BYTES, and the host otherwise (small files of the CESS
+    geometry finish sooner on SHA-NI than through the GPU's ~0.5 s per-chain latency for a
+    16 MiB segment).
     """
 
     def __init__(self, k: int = geometry.DATA_SHARDS, m: int = geometry.PARITY_SHARDS,
@@ -180,10 +181,11 @@ class SegmentEncoder:
         self.dev = torch.device("cuda", device)
         self.enc = New(k, m, device=device)
         frags_per_batch = batch_segments * (k + m)
-        self.hash_on = ("gpu" if frags_per_batch >= 2048 else "host") if hash_on == "auto" \
-            else hash_on
-        if self.hash_on not in ("gpu", "host"):
+        if hash_on not in ("gpu", "host", "auto"):
             raise ValueError("hash_on must be 'gpu', 'host' or 'auto'")
+        self.hash_mode = hash_on
+        self.wide = frags_per_batch >= 2048
+        self.window = max(1, window)
         self.pool = cf.ThreadPoolExecutor(max_workers=hash_threads)
         self.io_threads = 8
         self.io_pool = cf.ThreadPoolExecutor(max_workers=self.io_threads)
@@ -192,31 +194,54 @@ class SegmentEncoder:
                                    pin_memory=True) for _ in range(2)]
         self.h_par = [torch.empty((batch_segments, m, self.F), dtype=torch.uint8,
                                   pin_memory=True) for _ in range(2)]
-        self.W = max(1, window) if self.hash_on == "gpu" else 2
+        self.events = [None, None]
+        self.hash_on = None
+        self.hq = None
+        self._configure("gpu" if hash_on == "gpu" or (hash_on == "auto" and self.wide)
+                        else "host")
+
+    # "auto" hashes on the GPU for wide codes, and for the CESS geometry once the source is known
+    # to be at least this large: a 16 MiB segment chain has ~0.5 s of latency on the GPU, so small
+    # files finish sooner on SHA-NI (measured e2e: 13 GB/s host vs 35 GB/s GPU at 64 GiB, and the
+    # GPU path behind the host below ~8 GiB)
+    AUTO_GPU_BYTES = 8 << 30
+
+    def _configure(self, mode: str) -> None:
+        """(Re)allocate the device slots (and the hash queue) for a hash placement."""
+        import torch
+        if mode == self.hash_on:
+            return
+        if self.hq is not None:
+            self.hq.close()
+            self.hq = None
+        self.d_data = self.d_par = None
+        torch.cuda.synchronize(self.dev)
+        k, m, F, nb = self.k, self.m, self.F, self.batch
+        self.hash_on = mode
+        self.W = self.window if mode == "gpu" else 2
         # GPU hashing: W + 1 device slots, so the slot a batch reuses was freed one tick
         # before, and its H2D + encode overlap the current tick
-        nd = self.W + 1 if self.hash_on == "gpu" else 2
-        self.d_data = [torch.empty((batch_segments, k, self.F), dtype=torch.uint8,
-                                   device=self.dev) for _ in range(nd)]
-        self.d_par = [torch.empty((batch_segments, m, self.F), dtype=torch.uint8,
-                                  device=self.dev) for _ in range(nd)]
-        self.events = [None, None]
-        if self.hash_on == "gpu":
+        nd = self.W + 1 if mode == "gpu" else 2
+        self.d_data = [torch.empty((nb, k, F), dtype=torch.uint8, device=self.dev)
+                       for _ in range(nd)]
+        self.d_par = [torch.empty((nb, m, F), dtype=torch.uint8, device=self.dev)
+                      for _ in range(nd)]
+        if mode == "gpu":
             from .hashq import HashQueue, sha256_blocks
             self.hash_stream = torch.cuda.Stream(self.dev)
-            chains = self.W * batch_segments * (k + m + 1)
-            self.hq = HashQueue(capacity=1 << max(10, (chains - 1).bit_length()), device=device,
-                                stream=self.hash_stream)
+            chains = self.W * nb * (k + m + 1)
+            self.hq = HashQueue(capacity=1 << max(10, (chains - 1).bit_length()),
+                                device=self.dev.index, stream=self.hash_stream)
             # a segment chain completes `window` ticks after its add
-            self.tick_blocks = -(-sha256_blocks(segment_size) // self.W)
-            self.d_fhex = [torch.empty((batch_segments, k + m, 64), dtype=torch.uint8,
-                                       device=self.dev) for _ in range(nd)]
-            self.d_shex = [torch.empty((batch_segments, 64), dtype=torch.uint8,
-                                       device=self.dev) for _ in range(nd)]
-            self.h_fhex = [torch.empty((batch_segments, k + m, 64), dtype=torch.uint8,
-                                       pin_memory=True) for _ in range(nd)]
-            self.h_shex = [torch.empty((batch_segments, 64), dtype=torch.uint8,
-                                       pin_memory=True) for _ in range(nd)]
+            self.tick_blocks = -(-sha256_blocks(self.seg) // self.W)
+            self.d_fhex = [torch.empty((nb, k + m, 64), dtype=torch.uint8, device=self.dev)
+                           for _ in range(nd)]
+            self.d_shex = [torch.empty((nb, 64), dtype=torch.uint8, device=self.dev)
+                           for _ in range(nd)]
+            self.h_fhex = [torch.empty((nb, k + m, 64), dtype=torch.uint8, pin_memory=True)
+                           for _ in range(nd)]
+            self.h_shex = [torch.empty((nb, 64), dtype=torch.uint8, pin_memory=True)
+                           for _ in range(nd)]
             self.slot_free = [None] * nd  # event: slot's hashes copied out (slot reusable)
 
     def _read_batch(self, f: BinaryIO, slot: int) -> int:
@@ -348,6 +373,10 @@ class SegmentEncoder:
             close = False
         else:
             f, close = src, False
+        if self.hash_mode == "auto" and not self.wide:
+            size = f.stop - f.pos if isinstance(f, _ParallelReader) else None
+            self._configure("gpu" if size is not None and size >= self.AUTO_GPU_BYTES
+                            else "host")
         out = FileRecord(b"", 0)
         self._bytes = 0
         gpu = self.hash_on == "gpu"
@@ -409,6 +438,7 @@ class SegmentEncoder:
     def close(self):
         self.pool.shutdown(wait=True)
         self.io_pool.shutdown(wait=True)
-        if self.hash_on == "gpu":
+        if self.hq is not None:
             self.hq.close()
+            self.hq = None
         self.enc.close()

@@ -321,6 +321,23 @@ def test_segment_list_pipeline(torch, cess, orc, size, seg, k, m, hash_on, windo
         assert h.encode() == want[s][1][i]
 
 
+def test_segment_list_auto_placement(torch, cess, orc, monkeypatch):
+    """hash_on="auto" re-places hashing per file by size (host below AUTO_GPU_BYTES, GPU hash
+    queue above) on one encoder, records identical either way."""
+    from cess_amd.segments import SegmentEncoder
+    monkeypatch.setattr(SegmentEncoder, "AUTO_GPU_BYTES", 3 << 20)
+    seg = 1 << 20
+    se = SegmentEncoder(2, 1, seg, batch_segments=2, hash_on="auto", window=2)
+    for size, want_on in [((2 << 20) + 5, "host"), ((7 << 20) + 3, "gpu"), (1 << 20, "host"),
+                          (5 << 20, "gpu")]:
+        blob = np.random.default_rng(size).integers(0, 256, size, dtype=np.uint8)
+        rec = se.encode_file(blob)
+        assert se.hash_on == want_on
+        want = orc.segment_list(blob.tobytes(), 2, 1, seg)
+        assert [(s_.hash, s_.fragment_list) for s_ in rec.segments] == want
+    se.close()
+
+
 def test_degraded_read_single_rank(torch, cess, corc):
     """distributed.degraded_read end to end on one GPU (world 1: every survivor is local, so
     no P2P op is issued; the decode runs through libcessec)."""
