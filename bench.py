@@ -133,7 +133,8 @@ def main() -> None:
     ap.add_argument("--tick-pf", type=int, default=0,
                     help="hash-queue tick prefetch depth (1 or 2; 0 = library default)")
     ap.add_argument("--rt-mode", type=int, default=0,
-                    help="run-time kernel: 0 Horner over input groups (k <= 32), 1 per-bit masks")
+                    help="run-time kernel: 0 Horner over input groups, index-mode XORs (k <= 32), "
+                         "1 per-bit masks, 2 Horner with v_mov table reads")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
@@ -342,12 +343,12 @@ def main() -> None:
 
     tag = f"c{args.config}"
     kernel_name = {2: "k_ct<EncCT<2, 1>>", 3: "k_ct<Dec1CT<2, 1, *>> / k_ct<EncCT<2, 1>>",
-                   4: "k_ct<EncCT<2, 1>>", 5: "k_hg<EncCT<32, 32>, 4>", 6: "k_rth<8>", 7: "k_rth<8>",
-                   8: "k_rth<3>"}[args.config]
+                   4: "k_ct<EncCT<2, 1>>", 5: "k_hg<EncCT<32, 32>, 4>", 6: "k_rthx<8>",
+                   7: "k_rthx<8>", 8: "k_rthx<3>"}[args.config]
     if args.generic:
-        kernel_name = "k_rth" if k <= 32 else "k_rt"
-    if args.rt_mode == 1 and (args.generic or args.config in (6, 7, 8)):
-        kernel_name = "k_rt"
+        kernel_name = "k_rthx" if k <= 32 else "k_rt"
+    if args.rt_mode and (args.generic or args.config in (6, 7, 8)):
+        kernel_name = {1: "k_rt", 2: "k_rth"}[args.rt_mode]
     traffic = load_traffic(tag, bytes_step_gpu, kernel_name)
     out = {
         "metric": METRIC,

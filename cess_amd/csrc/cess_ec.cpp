@@ -382,7 +382,7 @@ int cec_set_option(cec_codec* c, int option, int value) {
       cec::set_sha_mode(value);
       return CEC_OK;
     case CEC_OPT_RT_MODE:
-      if (value < 0 || value > 1) return set_err(CEC_EINVAL, "rt mode out of range");
+      if (value < 0 || value > 2) return set_err(CEC_EINVAL, "rt mode out of range");
       cec::set_rt_mode(value);
       return CEC_OK;
     case CEC_OPT_TICK_PREFETCH:

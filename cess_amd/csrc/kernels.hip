@@ -633,6 +633,18 @@ __device__ __forceinline__ void rt_accumulate(T (&acc)[NOB][U], const cu32* __re
   }
 }
 
+// shard_ptr with the data/parity choice as scalar selects instead of a branch, so the run-time
+// kernels' per-input index loads batch into wide scalar loads ahead of the global loads.
+// (Pointer selects, not integer casts: the address stays in the global space, so the loads are
+// global_load, not flat_load, whose lgkmcnt coupling would serialise them with the index reads.)
+__device__ __forceinline__ uint8_t* shard_ptr_sel(const Layout& L, uint32_t idx, uint32_t seg) {
+  const bool isd = idx < (uint32_t)L.k;
+  uint8_t* const base = isd ? L.data : L.parity;
+  const uint64_t sstr = isd ? L.data_seg_stride : L.par_seg_stride;
+  const uint32_t j = isd ? idx : idx - (uint32_t)L.k;
+  return base + seg * sstr + (uint64_t)j * L.shard_stride;
+}
+
 __device__ __forceinline__ const uint32_t* as_const_ptr(const uint32_t* const* a, uint32_t y) {
   typedef const uint64_t __attribute__((address_space(4))) cu64;
   return (const uint32_t*)(uintptr_t)((const cu64*)(uintptr_t)a)[y];
@@ -710,7 +722,10 @@ __device__ __forceinline__ void rth_column(const cu32* __restrict__ P, LD ld, ST
   for (int g = 0; g < NG; ++g) {
     uint32_t x[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = (uint32_t)(4 * g + i) < nin ? ld(in_idx[4 * g + i]) : 0u;
+    for (int i = 0; i < 4; ++i) {  // unconditional load (unused slots name shard 0), masked
+      const uint32_t v = ld(in_idx[4 * g + i]);
+      x[i] = (uint32_t)(4 * g + i) < nin ? v : 0u;
+    }
     comb[g][0] = 0;
     comb[g][1] = x[0];
     comb[g][2] = x[1];
@@ -767,6 +782,186 @@ __global__ __launch_bounds__(256) void k_rth(Layout L, const uint32_t* __restric
   auto ld = [&](uint32_t sh) CEC_AI -> uint32_t { return shard_ptr(L, (int)sh, seg)[i]; };
   auto st = [&](uint32_t sh, uint32_t val) CEC_AI { shard_ptr(L, (int)sh, seg)[i] = (uint8_t)val; };
   rth_column<NG>(P, ld, st);
+}
+
+// Run-time Horner over input groups with the table reads folded into the XORs (k_rthx): the
+// group tables live in a fixed VGPR range above the compiler's allocation (amdgpu_num_vgpr caps
+// the compiler at RTHX_R registers; the asm blocks own v[RTHX_R, RTHX_R + 16 NG)), so a read of
+// entry idx of group g is the XOR's own source operand v[base_g] under s_set_gpr_idx (SRC0),
+// one VALU op and one SALU op per entry (k_rth: a v_mov under on/off, then the XOR).
+#define RTHX_R 24
+// The tables sit above the compiler's amdgpu_num_vgpr budget, which clang calls "reserved"
+// registers; the kernel descriptor's VGPR count includes them (tools/kres.py shows 24 + 16 NG).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void rthx_table0(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  asm volatile("v_mov_b32 v24, 0\n\tv_mov_b32 v25, %0\n\tv_mov_b32 v26, %1\n\tv_mov_b32 v28, %2\n\tv_mov_b32 v32, %3\n\tv_xor_b32 v27, v26, v25\n\tv_xor_b32 v29, v28, v25\n\tv_xor_b32 v30, v28, v26\n\tv_xor_b32 v31, v30, v25\n\tv_xor_b32 v33, v32, v25\n\tv_xor_b32 v34, v32, v26\n\tv_xor_b32 v35, v34, v25\n\tv_xor_b32 v36, v32, v28\n\tv_xor_b32 v37, v36, v25\n\tv_xor_b32 v38, v36, v26\n\tv_xor_b32 v39, v38, v25" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3)
+               : "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39");
+}
+__device__ __forceinline__ void rthx_table1(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  asm volatile("v_mov_b32 v40, 0\n\tv_mov_b32 v41, %0\n\tv_mov_b32 v42, %1\n\tv_mov_b32 v44, %2\n\tv_mov_b32 v48, %3\n\tv_xor_b32 v43, v42, v41\n\tv_xor_b32 v45, v44, v41\n\tv_xor_b32 v46, v44, v42\n\tv_xor_b32 v47, v46, v41\n\tv_xor_b32 v49, v48, v41\n\tv_xor_b32 v50, v48, v42\n\tv_xor_b32 v51, v50, v41\n\tv_xor_b32 v52, v48, v44\n\tv_xor_b32 v53, v52, v41\n\tv_xor_b32 v54, v52, v42\n\tv_xor_b32 v55, v54, v41" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3)
+               : "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55");
+}
+__device__ __forceinline__ void rthx_table2(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  asm volatile("v_mov_b32 v56, 0\n\tv_mov_b32 v57, %0\n\tv_mov_b32 v58, %1\n\tv_mov_b32 v60, %2\n\tv_mov_b32 v64, %3\n\tv_xor_b32 v59, v58, v57\n\tv_xor_b32 v61, v60, v57\n\tv_xor_b32 v62, v60, v58\n\tv_xor_b32 v63, v62, v57\n\tv_xor_b32 v65, v64, v57\n\tv_xor_b32 v66, v64, v58\n\tv_xor_b32 v67, v66, v57\n\tv_xor_b32 v68, v64, v60\n\tv_xor_b32 v69, v68, v57\n\tv_xor_b32 v70, v68, v58\n\tv_xor_b32 v71, v70, v57" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3)
+               : "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71");
+}
+__device__ __forceinline__ void rthx_table3(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  asm volatile("v_mov_b32 v72, 0\n\tv_mov_b32 v73, %0\n\tv_mov_b32 v74, %1\n\tv_mov_b32 v76, %2\n\tv_mov_b32 v80, %3\n\tv_xor_b32 v75, v74, v73\n\tv_xor_b32 v77, v76, v73\n\tv_xor_b32 v78, v76, v74\n\tv_xor_b32 v79, v78, v73\n\tv_xor_b32 v81, v80, v73\n\tv_xor_b32 v82, v80, v74\n\tv_xor_b32 v83, v82, v73\n\tv_xor_b32 v84, v80, v76\n\tv_xor_b32 v85, v84, v73\n\tv_xor_b32 v86, v84, v74\n\tv_xor_b32 v87, v86, v73" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3)
+               : "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87");
+}
+__device__ __forceinline__ void rthx_table4(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  asm volatile("v_mov_b32 v88, 0\n\tv_mov_b32 v89, %0\n\tv_mov_b32 v90, %1\n\tv_mov_b32 v92, %2\n\tv_mov_b32 v96, %3\n\tv_xor_b32 v91, v90, v89\n\tv_xor_b32 v93, v92, v89\n\tv_xor_b32 v94, v92, v90\n\tv_xor_b32 v95, v94, v89\n\tv_xor_b32 v97, v96, v89\n\tv_xor_b32 v98, v96, v90\n\tv_xor_b32 v99, v98, v89\n\tv_xor_b32 v100, v96, v92\n\tv_xor_b32 v101, v100, v89\n\tv_xor_b32 v102, v100, v90\n\tv_xor_b32 v103, v102, v89" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3)
+               : "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103");
+}
+__device__ __forceinline__ void rthx_table5(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  asm volatile("v_mov_b32 v104, 0\n\tv_mov_b32 v105, %0\n\tv_mov_b32 v106, %1\n\tv_mov_b32 v108, %2\n\tv_mov_b32 v112, %3\n\tv_xor_b32 v107, v106, v105\n\tv_xor_b32 v109, v108, v105\n\tv_xor_b32 v110, v108, v106\n\tv_xor_b32 v111, v110, v105\n\tv_xor_b32 v113, v112, v105\n\tv_xor_b32 v114, v112, v106\n\tv_xor_b32 v115, v114, v105\n\tv_xor_b32 v116, v112, v108\n\tv_xor_b32 v117, v116, v105\n\tv_xor_b32 v118, v116, v106\n\tv_xor_b32 v119, v118, v105" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3)
+               : "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119");
+}
+__device__ __forceinline__ void rthx_table6(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  asm volatile("v_mov_b32 v120, 0\n\tv_mov_b32 v121, %0\n\tv_mov_b32 v122, %1\n\tv_mov_b32 v124, %2\n\tv_mov_b32 v128, %3\n\tv_xor_b32 v123, v122, v121\n\tv_xor_b32 v125, v124, v121\n\tv_xor_b32 v126, v124, v122\n\tv_xor_b32 v127, v126, v121\n\tv_xor_b32 v129, v128, v121\n\tv_xor_b32 v130, v128, v122\n\tv_xor_b32 v131, v130, v121\n\tv_xor_b32 v132, v128, v124\n\tv_xor_b32 v133, v132, v121\n\tv_xor_b32 v134, v132, v122\n\tv_xor_b32 v135, v134, v121" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3)
+               : "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135");
+}
+__device__ __forceinline__ void rthx_table7(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  asm volatile("v_mov_b32 v136, 0\n\tv_mov_b32 v137, %0\n\tv_mov_b32 v138, %1\n\tv_mov_b32 v140, %2\n\tv_mov_b32 v144, %3\n\tv_xor_b32 v139, v138, v137\n\tv_xor_b32 v141, v140, v137\n\tv_xor_b32 v142, v140, v138\n\tv_xor_b32 v143, v142, v137\n\tv_xor_b32 v145, v144, v137\n\tv_xor_b32 v146, v144, v138\n\tv_xor_b32 v147, v146, v137\n\tv_xor_b32 v148, v144, v140\n\tv_xor_b32 v149, v148, v137\n\tv_xor_b32 v150, v148, v138\n\tv_xor_b32 v151, v150, v137" ::"v"(x0), "v"(x1), "v"(x2), "v"(x3)
+               : "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151");
+}
+#pragma clang diagnostic pop
+// y ^= T_g[q[g]] for the NG groups, each a v_xor whose SRC0 is indexed by M0. The SALU write of
+// M0 (s_set_gpr_idx_on / _idx) needs one wait state before the indexed VALU: without the s_nop
+// the XOR read a stale index now and then (10 of 10 RS(32,32) 32-erasure rebuilds had 10^5 wrong
+// bytes, a different set each run; with it 0 of 10, tools/stress_rthx.py). One after _off too,
+// before any VALU that names a VGPR as SRC0.
+#define RTHX_ON "s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\ts_nop 0\n\tv_xor_b32 %0, v24, %0\n\t"
+#define RTHX_IDX(n, reg) "s_set_gpr_idx_idx %" #n "\n\ts_nop 0\n\tv_xor_b32 %0, " reg ", %0\n\t"
+#define RTHX_OFF "s_set_gpr_idx_off\n\ts_nop 0"
+template <int NG>
+__device__ __forceinline__ uint32_t rthx_xor(uint32_t y, const uint32_t (&q)[NG]);
+template <>
+__device__ __forceinline__ uint32_t rthx_xor<1>(uint32_t y, const uint32_t (&q)[1]) {
+  asm volatile(RTHX_ON RTHX_OFF : "+v"(y) : "s"(q[0]));
+  return y;
+}
+template <>
+__device__ __forceinline__ uint32_t rthx_xor<2>(uint32_t y, const uint32_t (&q)[2]) {
+  asm volatile(RTHX_ON RTHX_IDX(2, "v40") RTHX_OFF : "+v"(y) : "s"(q[0]), "s"(q[1]));
+  return y;
+}
+template <>
+__device__ __forceinline__ uint32_t rthx_xor<3>(uint32_t y, const uint32_t (&q)[3]) {
+  asm volatile(RTHX_ON RTHX_IDX(2, "v40") RTHX_IDX(3, "v56") RTHX_OFF
+               : "+v"(y) : "s"(q[0]), "s"(q[1]), "s"(q[2]));
+  return y;
+}
+template <>
+__device__ __forceinline__ uint32_t rthx_xor<4>(uint32_t y, const uint32_t (&q)[4]) {
+  asm volatile(RTHX_ON RTHX_IDX(2, "v40") RTHX_IDX(3, "v56") RTHX_IDX(4, "v72") RTHX_OFF
+               : "+v"(y) : "s"(q[0]), "s"(q[1]), "s"(q[2]), "s"(q[3]));
+  return y;
+}
+template <>
+__device__ __forceinline__ uint32_t rthx_xor<6>(uint32_t y, const uint32_t (&q)[6]) {
+  asm volatile(RTHX_ON RTHX_IDX(2, "v40") RTHX_IDX(3, "v56") RTHX_IDX(4, "v72")
+                   RTHX_IDX(5, "v88") RTHX_IDX(6, "v104") RTHX_OFF
+               : "+v"(y) : "s"(q[0]), "s"(q[1]), "s"(q[2]), "s"(q[3]), "s"(q[4]), "s"(q[5]));
+  return y;
+}
+template <>
+__device__ __forceinline__ uint32_t rthx_xor<8>(uint32_t y, const uint32_t (&q)[8]) {
+  asm volatile(RTHX_ON RTHX_IDX(2, "v40") RTHX_IDX(3, "v56") RTHX_IDX(4, "v72")
+                   RTHX_IDX(5, "v88") RTHX_IDX(6, "v104") RTHX_IDX(7, "v120")
+                       RTHX_IDX(8, "v136") RTHX_OFF
+               : "+v"(y)
+               : "s"(q[0]), "s"(q[1]), "s"(q[2]), "s"(q[3]), "s"(q[4]), "s"(q[5]), "s"(q[6]),
+                 "s"(q[7]));
+  return y;
+}
+#undef RTHX_ON
+#undef RTHX_IDX
+#undef RTHX_OFF
+
+template <int NG, class LD, class ST>
+__device__ __forceinline__ void rthx_column(const cu32* __restrict__ P, LD ld, ST st) {
+  const uint32_t nin = P[0], nout = P[1];
+  const cu32* __restrict__ in_idx = P + 4;
+  const cu32* __restrict__ out_idx = P + 4 + 256;
+  const cu32* __restrict__ ix = P + P[3] + 32;
+  // unused input slots hold shard index 0 (a valid shard), so every load is unconditional and
+  // the index reads batch into wide scalar loads; the value is masked afterwards. Loads run two
+  // groups ahead of the table being built (the asm blocks are ordered; four live inputs per
+  // group keep the compiler inside its RTHX_R registers).
+  uint32_t xs[NG][4];
+  auto load_group = [&](int g) CEC_AI {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t v = ld(in_idx[4 * g + i]);
+      xs[g][i] = (uint32_t)(4 * g + i) < nin ? v : 0u;
+    }
+  };
+  auto build = [&](int g) CEC_AI {
+    const uint32_t* x = xs[g];
+    if (g == 0) rthx_table0(x[0], x[1], x[2], x[3]);
+    if (g == 1) rthx_table1(x[0], x[1], x[2], x[3]);
+    if (g == 2) rthx_table2(x[0], x[1], x[2], x[3]);
+    if (g == 3) rthx_table3(x[0], x[1], x[2], x[3]);
+    if (g == 4) rthx_table4(x[0], x[1], x[2], x[3]);
+    if (g == 5) rthx_table5(x[0], x[1], x[2], x[3]);
+    if (g == 6) rthx_table6(x[0], x[1], x[2], x[3]);
+    if (g == 7) rthx_table7(x[0], x[1], x[2], x[3]);
+  };
+  load_group(0);
+  if constexpr (NG > 1) load_group(1);
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    if (g + 2 < NG) load_group(g + 2);
+    build(g);
+  }
+  for (uint32_t o = 0; o < nout; ++o) {
+    // the row's 8 x NG indices in SGPRs up front: one scalar-load wait per row, not per bit
+    const cu32* __restrict__ q = ix + o * 64;
+    uint32_t iv[8][NG];
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int g = 0; g < NG; ++g) iv[b][g] = q[b * 8 + g];
+    uint32_t y = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; --b) {
+      if (b < 7) y = xt_fast(y);
+      y = rthx_xor<NG>(y, iv[b]);
+    }
+    st(out_idx[o], y);
+  }
+}
+
+template <int NG>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(RTHX_R))) void k_rthx(
+    Layout L, const uint32_t* __restrict__ chunk, const uint32_t* const* __restrict__ per_seg,
+    const uint32_t* __restrict__ seg_list, uint32_t seg0, int vec_ok) {
+  const uint32_t y = seg0 + blockIdx.y;
+  const uint32_t seg = seg_list ? seg_list[y] : y;
+  const cu32* __restrict__ P = as_const(per_seg ? as_const_ptr(per_seg, y) : chunk);
+  if (vec_ok) {
+    const uint64_t nvec = L.len / 4;
+    const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v < nvec) {
+      const uint64_t off = v * 4;
+      auto ld = [&](uint32_t sh) CEC_AI -> uint32_t {
+        return *reinterpret_cast<const uint32_t*>(shard_ptr_sel(L, sh, seg) + off);
+      };
+      auto st = [&](uint32_t sh, uint32_t val) CEC_AI {
+        *reinterpret_cast<uint32_t*>(shard_ptr_sel(L, sh, seg) + off) = val;
+      };
+      rthx_column<NG>(P, ld, st);
+    }
+    if (!(L.len % 4) || blockIdx.x != gridDim.x - 1) return;
+  }
+  const uint64_t i = vec_ok ? (L.len - L.len % 4) + threadIdx.x
+                            : (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= L.len) return;
+  auto ld = [&](uint32_t sh) CEC_AI -> uint32_t { return shard_ptr_sel(L, sh, seg)[i]; };
+  auto st = [&](uint32_t sh, uint32_t val) CEC_AI { shard_ptr_sel(L, sh, seg)[i] = (uint8_t)val; };
+  rthx_column<NG>(P, ld, st);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -974,7 +1169,8 @@ void launch_matvec_rt(const Layout& L, const uint32_t* chunk, const uint32_t* co
 }
 
 namespace {
-int g_rt_mode = 0;  // 0: Horner-over-groups run-time kernel where possible, 1: always k_rt
+int g_rt_mode = 0;  // 0: Horner over input groups with index-mode XORs (k_rthx) where possible,
+                    // 1: always k_rt (per-bit masks), 2: Horner with v_mov table reads (k_rth)
 
 template <int NG>
 void run_rth(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
@@ -985,8 +1181,12 @@ void run_rth(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_
   uint64_t gx = vec_ok ? (L.len / 4 + 255) / 256 : (L.len + 255) / 256;
   if (gx == 0) gx = 1;
   for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) {
-    hipLaunchKernelGGL((k_rth<NG>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, chunk, per_seg,
-                       seg_list, s0, vec_ok);
+    if (g_rt_mode == 0)
+      hipLaunchKernelGGL((k_rthx<NG>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, chunk,
+                         per_seg, seg_list, s0, vec_ok);
+    else
+      hipLaunchKernelGGL((k_rth<NG>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, chunk,
+                         per_seg, seg_list, s0, vec_ok);
   });
 }
 }  // namespace
@@ -995,9 +1195,10 @@ void set_rt_mode(int v) { g_rt_mode = v; }
 
 bool launch_matvec_rth(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
                        int nin_max, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
-  // measured (profiles/r01/rt_modes.txt): faster than k_rt from 4 inputs up (RS(10,4) encode
-  // 3.0 vs 2.7 TB/s, RS(32,32) one-fragment repair 4.0 vs 3.1, 32-erasure rebuild 1.1 vs 0.96);
-  // for 2-3 inputs k_rt's 16-byte columns win (RS(2,1) run-time encode 6.0 vs 2.9 TB/s)
+  // measured (profiles/r01/rt_modes.txt): faster than k_rt from 4 inputs up (k_rthx / k_rth /
+  // k_rt: RS(10,4) encode 3.2 / 3.0 / 2.7 TB/s, RS(32,32) one-fragment repair 4.0 / 4.0 / 3.1,
+  // 32-erasure rebuild 1.76 / 1.1 / 0.96); for 2-3 inputs k_rt's 16-byte columns win (RS(2,1)
+  // run-time encode 6.0 vs 2.9 TB/s)
   if (g_rt_mode == 1 || nin_max > kRthMaxIn || nin_max < 4) return false;
   const int ng = (nin_max + 3) / 4;
   if (ng <= 1) run_rth<1>(L, chunk, per_seg, seg_list, nseg, st);

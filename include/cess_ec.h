@@ -141,7 +141,8 @@ int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t s
 #define CEC_OPT_SHA_MODE 3      /* SHA-256 kernel: 0 = auto, 1 = one wave per 64 buffers,
                                    2 = two waves (schedule producer + rounds consumer) */
 #define CEC_OPT_RT_MODE 4       /* run-time-coefficient kernel: 0 = Horner over input groups
-                                   when 4 <= inputs <= 32, 1 = always the per-bit mask kernel */
+                                   with index-mode table XORs when 4 <= inputs <= 32, 1 = always
+                                   the per-bit mask kernel, 2 = Horner with v_mov table reads */
 #define CEC_OPT_TICK_PREFETCH 5  /* hash-queue tick kernel: 0 = auto by live chains, 1 or 2 =
                                    two waves (schedule producer loading 1 or 2 blocks ahead +
                                    rounds consumer), 3 = one wave per 64 chains */

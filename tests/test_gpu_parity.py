@@ -517,8 +517,9 @@ def test_c_abi_consumer(tmp_path):
 @pytest.mark.parametrize("k,m,ln", [(32, 32, 4096 + 3), (10, 4, 1000), (17, 3, 4099),
                                     (33, 3, 515), (1, 1, 9), (5, 5, 64)])
 def test_runtime_kernels_agree(torch, cess, corc, k, m, ln):
-    """k_rth (Horner over input groups, run-time indices) and k_rt (per-bit masks) against the
-    C oracle: encode and per-segment random-erasure reconstruct, vector body and byte tail."""
+    """k_rth (Horner over input groups, run-time indices), k_rt (per-bit masks) and k_rthx
+    (Horner with index-mode XORs) against the C oracle: encode and per-segment random-erasure
+    reconstruct, vector body and byte tail."""
     nseg = 3
     rng = np.random.default_rng(k * 1000 + ln)
     data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
@@ -529,7 +530,7 @@ def test_runtime_kernels_agree(torch, cess, corc, k, m, ln):
     enc = cess.New(k, m)
     enc.set_option(1, 1)  # run-time coefficients for encode too
     try:
-        for mode in (0, 1):
+        for mode in (0, 1, 2):
             enc.set_option(4, mode)
             d_data = to_dev(torch, data)
             d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")

@@ -1,0 +1,9 @@
+set -u
+cd $GRAFT_REPO_ROOT; OUT=$PWD/gpurun_out/r01zd; mkdir -p $OUT
+timeout -k 10 120 python -u tools/stress_rthx.py --runs 10 || exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+for args in "--config 6" "--config 7" "--config 8" "--config 5 --generic"; do for rt in 0 2; do
+  timeout -k 10 200 python -u bench.py $args --rt-mode $rt --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $OUT/b.json 2>&1 || { tail $OUT/b.json; exit 1; }
+  python -c "import json;d=json.loads(open('$OUT/b.json').read().strip().splitlines()[-1]);print('$args rt=$rt', d['roofline']['achieved'], d['roofline']['launch_ms'], d['config']['kernel'])"
+done; done
