@@ -38,6 +38,19 @@ def sha256_hex(buf) -> bytes:
     return hashlib.sha256(buf).hexdigest().encode()
 
 
+def segment_and_first_fragment_hex(seg2d) -> tuple:
+    """(SHA-256 hex of the whole segment, SHA-256 hex of data fragment 0) from ONE pass over
+    fragment 0. The split is contiguous (fragment i = segment bytes [i*F, (i+1)*F)), so the
+    segment's SHA-256 stream is fragment 0's unpadded stream continued with fragments 1..k-1:
+    the fragment-0 digest is taken from a copy of the running state. For the CESS geometry
+    (k = 2, F = 8 MiB) this hashes 32 MiB per segment instead of 40 MiB."""
+    h = hashlib.sha256(seg2d[0])
+    d0 = h.copy().hexdigest().encode()
+    for i in range(1, len(seg2d)):
+        h.update(seg2d[i])
+    return h.hexdigest().encode(), d0
+
+
 @dataclass
 class SegmentList:
     """types.rs:13-16 — segment hash + fragment hashes in fragment index order."""
@@ -202,9 +215,10 @@ class SegmentEncoder:
 
     # "auto" hashes on the GPU for wide codes, and for the CESS geometry once the source is known
     # to be at least this large: a 16 MiB segment chain has ~0.5 s of latency on the GPU, so small
-    # files finish sooner on SHA-NI (measured e2e: 13 GB/s host vs 35 GB/s GPU at 64 GiB, and the
-    # GPU path behind the host below ~8 GiB)
-    AUTO_GPU_BYTES = 8 << 30
+    # files finish sooner on SHA-NI (measured e2e with the shared segment/fragment-0 stream on the
+    # host: host 16.1 vs GPU 12.8 GB/s at 8 GiB, host 15.1 vs GPU 17.2 at 12 GiB, GPU 34.7 at
+    # 64 GiB; DESIGN.md §5, profiles/r01/e2e_host_shared_stream.txt)
+    AUTO_GPU_BYTES = 10 << 30
 
     def _configure(self, mode: str) -> None:
         """(Re)allocate the device slots (and the hash queue) for a hash placement."""
@@ -303,9 +317,11 @@ class SegmentEncoder:
         if self.hash_on != "host":
             return None
         data = self.h_data[slot].numpy()
-        seg_futs = [self.pool.submit(sha256_hex, memoryview(data[s].reshape(-1)))
+        # segment hash and data fragment 0 share one stream (segment_and_first_fragment_hex)
+        seg_futs = [self.pool.submit(segment_and_first_fragment_hex,
+                                     [memoryview(data[s, i]) for i in range(self.k)])
                     for s in range(nseg)]
-        dfuts = [[self.pool.submit(sha256_hex, memoryview(data[s, i])) for i in range(self.k)]
+        dfuts = [[self.pool.submit(sha256_hex, memoryview(data[s, i])) for i in range(1, self.k)]
                  for s in range(nseg)]
         return seg_futs, dfuts
 
@@ -322,9 +338,11 @@ class SegmentEncoder:
             seg_futs, dfuts = futs
             pfuts = [[self.pool.submit(sha256_hex, memoryview(par[s, o])) for o in range(m)]
                      for s in range(nseg)]
-            recs = [SegmentList(seg_futs[s].result(),
-                                [f.result() for f in dfuts[s]] + [f.result() for f in pfuts[s]])
-                    for s in range(nseg)]
+            recs = []
+            for s in range(nseg):
+                seg_hex, d0_hex = seg_futs[s].result()
+                recs.append(SegmentList(seg_hex, [d0_hex] + [f.result() for f in dfuts[s]]
+                                        + [f.result() for f in pfuts[s]]))
         if on_fragment is not None:
             for s in range(nseg):
                 for i in range(k + m):

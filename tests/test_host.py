@@ -149,3 +149,16 @@ def test_product_matrix_and_plans_match_oracle(plan_dump, orc, k, m):
         assert list(map(int, tok[i_in + 1:i_out])) == surv
         assert list(map(int, tok[i_out + 1:i_coef])) == outs
         assert list(map(int, tok[i_coef + 1:])) == sum(rows, [])
+
+
+@pytest.mark.parametrize("k,flen", [(2, 4096), (2, 1000), (3, 64), (1, 77)])
+def test_segment_hash_shares_fragment0_stream(k, flen):
+    """The host path hashes fragment 0 once for both its own hash and the segment's
+    (segments.segment_and_first_fragment_hex): both digests equal independent SHA-256s."""
+    import hashlib
+    from cess_amd.segments import segment_and_first_fragment_hex
+    rng = np.random.default_rng(k * 1000 + flen)
+    seg = rng.integers(0, 256, size=(k, flen), dtype=np.uint8)
+    seg_hex, d0_hex = segment_and_first_fragment_hex([memoryview(seg[i]) for i in range(k)])
+    assert seg_hex == hashlib.sha256(seg.tobytes()).hexdigest().encode()
+    assert d0_hex == hashlib.sha256(seg[0].tobytes()).hexdigest().encode()
