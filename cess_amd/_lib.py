@@ -35,6 +35,9 @@ SIGNATURES = {
     "cec_hashq_destroy": (None, [c_void_p]),
     "cec_hashq_add": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_size_t,
                               c_size_t, c_void_p, c_size_t, POINTER(c_uint64)]),
+    "cec_hashq_add_prefix": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_size_t,
+                                     c_size_t, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t,
+                                     POINTER(c_uint64)]),
     "cec_hashq_tick": (c_int, [c_void_p, c_uint32]),
     "cec_hashq_finish": (c_int, [c_void_p]),
     "cec_hashq_status": (c_int, [c_void_p, c_uint64, POINTER(c_int), POINTER(c_size_t),

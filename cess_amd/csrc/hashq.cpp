@@ -94,11 +94,14 @@ void cec_hashq_destroy(cec_hashq* q) {
   delete q;
 }
 
-int cec_hashq_add(cec_hashq* q, const uint8_t* d_base, size_t n, size_t per, size_t outer_stride,
-                  size_t inner_stride, size_t len, uint8_t* d_hex, size_t hex_outer,
-                  uint64_t* ticket) {
+int cec_hashq_add_prefix(cec_hashq* q, const uint8_t* d_base, size_t n, size_t per,
+                         size_t outer_stride, size_t inner_stride, size_t len, uint8_t* d_hex,
+                         size_t hex_outer, size_t prefix_len, uint8_t* d_prefix_hex,
+                         size_t prefix_hex_outer, uint64_t* ticket) {
   if (!q || (n && !d_base) || per == 0) return cec::set_error(CEC_EINVAL, "null or per == 0");
   if (n > 0xFFFFFFFFull) return cec::set_error(CEC_EINVAL, "n too large");
+  if (d_prefix_hex && (prefix_len == 0 || (prefix_len & 63) || prefix_len > len))
+    return cec::set_error(CEC_EINVAL, "prefix_len must be a nonzero multiple of 64 <= len");
   if (n == 0) {
     if (ticket) *ticket = 0;
     return CEC_OK;
@@ -107,14 +110,25 @@ int cec_hashq_add(cec_hashq* q, const uint8_t* d_base, size_t n, size_t per, siz
     return cec::set_error(CEC_ENOMEM, "hash queue full: tick until chains complete");
   HQ_TRY(hipSetDevice(q->device));
   cec::launch_hashq_add(q->tab, q->cap - 1, q->tail, (uint32_t)n, d_base, (uint32_t)per,
-                        outer_stride, inner_stride, len, d_hex, hex_outer, q->stream);
+                        outer_stride, inner_stride, len, d_hex, hex_outer,
+                        d_prefix_hex ? prefix_len >> 6 : 0, d_prefix_hex, prefix_hex_outer,
+                        q->stream);
   int rc = launched();
   if (rc) return rc;
+  // the prefix digest is written before the chain completes, so tracking the add by its full
+  // length is conservative for it
   q->adds.push_back({q->tail, n, cec::sha256_blocks(len), 0, q->next_ticket});
   q->tail += n;
   if (ticket) *ticket = q->next_ticket;
   ++q->next_ticket;
   return CEC_OK;
+}
+
+int cec_hashq_add(cec_hashq* q, const uint8_t* d_base, size_t n, size_t per, size_t outer_stride,
+                  size_t inner_stride, size_t len, uint8_t* d_hex, size_t hex_outer,
+                  uint64_t* ticket) {
+  return cec_hashq_add_prefix(q, d_base, n, per, outer_stride, inner_stride, len, d_hex,
+                              hex_outer, 0, nullptr, 0, ticket);
 }
 
 int cec_hashq_tick(cec_hashq* q, uint32_t max_blocks) {

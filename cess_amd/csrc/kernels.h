@@ -70,25 +70,33 @@ bool launch_matvec_rth(const Layout& L, const uint32_t* chunk, const uint32_t* c
 void launch_sha256_hex(const uint8_t* const* ptrs, const Layout* L, int nshards, uint64_t n,
                        uint64_t len, uint8_t* hex_out, hipStream_t st);
 
-// One chain of the streaming SHA-256 queue (hashq.cpp), 64 bytes in HBM. `blk` counts the
+// One chain of the streaming SHA-256 queue (hashq.cpp), 128 bytes in HBM. `blk` counts the
 // 64-byte blocks already compressed into `h`, padding blocks included; the chain is complete
 // when blk == (len >> 6) + ((len & 63) >= 56 ? 2 : 1), and its hex (if `hex` is set) is written
-// by the launch that completes it.
+// by the launch that completes it. Prefix digest: when `pre_blk` > 0 the chain also writes the
+// SHA-256 hex of its first pre_blk * 64 bytes to `pre_hex`, from a copy of `h` taken right after
+// block pre_blk - 1 and one padding block (a segment's chain gives its first fragment's hash).
 struct ShaChain {
   const uint8_t* src;
   uint64_t len;
   uint64_t blk;
   uint8_t* hex;
   uint32_t h[8];
+  uint8_t* pre_hex;
+  uint64_t pre_blk;
+  uint64_t pad_[6];
 };
-static_assert(sizeof(ShaChain) == 64, "ShaChain is one 64-byte record");
+static_assert(sizeof(ShaChain) == 128, "ShaChain is one 128-byte record");
 
 inline uint64_t sha256_blocks(uint64_t len) { return (len >> 6) + ((len & 63) >= 56 ? 2 : 1); }
 
 // Initialise n chains in slots slot0.. of the ring `tab` (capacity mask + 1, a power of two).
+// pre_blk > 0: chain i also writes the hex of its first pre_blk blocks to
+// pre_hex + ((i / per) * pre_hex_outer + i % per) * 64.
 void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
                       const uint8_t* base, uint32_t per, uint64_t outer, uint64_t inner,
-                      uint64_t len, uint8_t* hex, uint64_t hex_outer, hipStream_t st);
+                      uint64_t len, uint8_t* hex, uint64_t hex_outer, uint64_t pre_blk,
+                      uint8_t* pre_hex, uint64_t pre_hex_outer, hipStream_t st);
 // Advance the n chains in slots head.. by at most max_blocks blocks each; `live` (chains not
 // yet complete among them) picks the kernel form.
 void launch_sha256_tick(ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,

@@ -385,6 +385,25 @@ __device__ __forceinline__ void sha_block_general(uint32_t (&w)[16], const uint8
 
 #define CEC_SHA_AI __attribute__((always_inline))
 
+// Prefix digest of a chain (ShaChain::pre_blk): finish a copy of the state after `blocks` whole
+// message blocks with the one padding block of a 64-byte-multiple length, write its hex. Not
+// inlined: it runs once per chain, and a second inlined compression would raise the tick
+// kernels' VGPR counts.
+// The state goes by value (eight VGPR arguments): a pointer would put the caller's h in scratch.
+__device__ __noinline__ void sha_prefix_hex(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
+                                            uint32_t h4, uint32_t h5, uint32_t h6, uint32_t h7,
+                                            uint64_t blocks, uint8_t* __restrict__ hex) {
+  uint32_t h[8] = {h0, h1, h2, h3, h4, h5, h6, h7}, w[16];
+  const uint64_t bits = blocks << 9;
+  w[0] = 0x80000000u;
+#pragma unroll
+  for (int q = 1; q < 14; ++q) w[q] = 0;
+  w[14] = (uint32_t)(bits >> 32);
+  w[15] = (uint32_t)bits;
+  sha256_block(h, w);
+  sha_store_hex(hex, h);
+}
+
 template <int PF>
 __global__ __launch_bounds__(128) void k_sha256_tick(ShaChain* __restrict__ tab, uint32_t mask,
                                                      uint64_t head, uint32_t n,
@@ -471,9 +490,11 @@ __global__ __launch_bounds__(128) void k_sha256_tick(ShaChain* __restrict__ tab,
     __syncthreads();  // matches the consumer's final iteration
   } else {
     uint32_t h[8] = {};
+    uint64_t pre = 0;  // block count after which the prefix digest is due (0: none)
     if (live) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) h[q] = ch_->h[q];
+      pre = ch_->pre_blk;
     }
     __syncthreads();  // block 0 produced
     for (uint32_t b = 0; b < trips; ++b) {
@@ -495,6 +516,8 @@ __global__ __launch_bounds__(128) void k_sha256_tick(ShaChain* __restrict__ tab,
           }
         }
         h[0] += a; h[1] += bb; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+        if (blk0 + b + 1 == pre)
+          sha_prefix_hex(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], pre, ch_->pre_hex);
       }
       __syncthreads();  // this buffer consumed / next one produced
     }
@@ -527,6 +550,7 @@ __global__ __launch_bounds__(64) void k_sha256_tick1(ShaChain* __restrict__ tab,
   const uint32_t nblk = rem < max_blocks ? (uint32_t)rem : max_blocks;
   if (nblk == 0) return;
   const uint8_t* src = ch_->src;
+  const uint64_t pre = ch_->pre_blk;
   uint32_t h[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) h[q] = ch_->h[q];
@@ -560,6 +584,8 @@ __global__ __launch_bounds__(64) void k_sha256_tick1(ShaChain* __restrict__ tab,
       sha_block_general(w, src, g, nfull, r, nb, len, &stage[threadIdx.x][0], 1);
     }
     sha256_block(h, w);
+    if (g + 1 == pre)
+      sha_prefix_hex(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], pre, ch_->pre_hex);
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) ch_->h[q] = h[q];
@@ -574,7 +600,9 @@ __global__ __launch_bounds__(256) void k_hashq_add(ShaChain* __restrict__ tab, u
                                                    uint64_t slot0, uint32_t n,
                                                    const uint8_t* base, uint32_t per,
                                                    uint64_t outer, uint64_t inner, uint64_t len,
-                                                   uint8_t* hex, uint64_t hex_outer) {
+                                                   uint8_t* hex, uint64_t hex_outer,
+                                                   uint64_t pre_blk, uint8_t* pre_hex,
+                                                   uint64_t pre_hex_outer) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const uint32_t a = i / per, b = i % per;
@@ -583,6 +611,10 @@ __global__ __launch_bounds__(256) void k_hashq_add(ShaChain* __restrict__ tab, u
   c.len = len;
   c.blk = 0;
   c.hex = hex ? hex + (a * hex_outer + b) * 64 : nullptr;
+  c.pre_blk = pre_hex ? pre_blk : 0;
+  c.pre_hex = pre_hex ? pre_hex + (a * pre_hex_outer + b) * 64 : nullptr;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) c.pad_[q] = 0;
   const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                           0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
 #pragma unroll
@@ -620,10 +652,12 @@ void launch_sha256_hex(const uint8_t* const* ptrs, const Layout* L, int nshards,
 
 void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
                       const uint8_t* base, uint32_t per, uint64_t outer, uint64_t inner,
-                      uint64_t len, uint8_t* hex, uint64_t hex_outer, hipStream_t st) {
+                      uint64_t len, uint8_t* hex, uint64_t hex_outer, uint64_t pre_blk,
+                      uint8_t* pre_hex, uint64_t pre_hex_outer, hipStream_t st) {
   if (n == 0) return;
   hipLaunchKernelGGL(k_hashq_add, dim3((n + 255) / 256), dim3(256), 0, st, tab, mask, slot0, n,
-                     base, per, outer, inner, len, hex, hex_outer);
+                     base, per, outer, inner, len, hex, hex_outer, pre_blk, pre_hex,
+                     pre_hex_outer);
 }
 
 void launch_sha256_tick(ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,

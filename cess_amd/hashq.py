@@ -57,14 +57,20 @@ class HashQueue:
         self.close()
 
     def add(self, d_base, n: int, per: int, outer_stride: int, inner_stride: int, length: int,
-            d_hex=None, hex_outer: int = 0, hex_offset: int = 0) -> int:
+            d_hex=None, hex_outer: int = 0, hex_offset: int = 0, prefix_len: int = 0,
+            d_prefix_hex=None, prefix_hex_outer: int = 0, prefix_hex_offset: int = 0) -> int:
         """Append n chains (buffer i at base + (i // per) * outer + (i % per) * inner, `length`
-        bytes; hex at d_hex + hex_offset + ((i // per) * hex_outer + i % per) * 64). Returns the
-        add's ticket."""
+        bytes; hex at d_hex + hex_offset + ((i // per) * hex_outer + i % per) * 64). With
+        d_prefix_hex, chain i also writes the hex of its first prefix_len bytes (a multiple of 64)
+        at d_prefix_hex + prefix_hex_offset + ((i // per) * prefix_hex_outer + i % per) * 64
+        (cec_hashq_add_prefix). Returns the add's ticket."""
         t = c_uint64()
         hexp = None if d_hex is None else _dev_ptr(d_hex) + hex_offset
-        check(_lib.load().cec_hashq_add(self._h, _dev_ptr(d_base), n, per, outer_stride,
-                                        inner_stride, length, hexp, hex_outer, byref(t)),
+        prep = None if d_prefix_hex is None else _dev_ptr(d_prefix_hex) + prefix_hex_offset
+        check(_lib.load().cec_hashq_add_prefix(self._h, _dev_ptr(d_base), n, per, outer_stride,
+                                               inner_stride, length, hexp, hex_outer,
+                                               prefix_len if prep else 0, prep,
+                                               prefix_hex_outer, byref(t)),
               "HashQueue.add")
         return t.value
 
@@ -86,6 +92,31 @@ class HashQueue:
         """Hash nseg contiguous segments (SegmentList.hash) into d_hex[nseg][64]."""
         stride = seg_len if seg_stride is None else seg_stride
         return self.add(d_data, nseg, 1, stride, stride, seg_len, d_hex, 1, 0)
+
+    def add_segment_lists(self, d_data, d_parity, nseg: int, k: int, m: int, shard_len: int,
+                          d_seg_hex, d_frag_hex) -> int:
+        """Every hash of a batch's SegmentLists ([nseg][k][len] data, [nseg][m][len] parity):
+        segment hashes into d_seg_hex[nseg][64], fragment hashes into d_frag_hex[nseg][k+m][64].
+        Data fragment 0's hash is the prefix digest of its segment's chain, so fragment 0 is
+        hashed once (k*len + (k-1)*len + m*len bytes per segment instead of (2k+m)*len).
+        Needs shard_len % 64 == 0 (else fragment 0 gets its own chain). Returns the ticket of
+        the segment chains, the longest of the batch (the batch is done when they are)."""
+        n_sh = k + m
+        seg = k * shard_len
+        if shard_len % 64 == 0:
+            t = self.add(d_data, nseg, 1, seg, seg, seg, d_seg_hex, 1, 0, shard_len,
+                         d_frag_hex, n_sh, 0)
+            if k > 1:
+                # data fragments 1..k-1: base shifted by one fragment, per = k - 1
+                self.add(_dev_ptr(d_data) + shard_len, nseg * (k - 1), k - 1, seg, shard_len,
+                         shard_len, d_frag_hex, n_sh, 64)
+        else:
+            t = self.add(d_data, nseg, 1, seg, seg, seg, d_seg_hex, 1, 0)
+            self.add(d_data, nseg * k, k, seg, shard_len, shard_len, d_frag_hex, n_sh, 0)
+        if m:
+            self.add(d_parity, nseg * m, m, m * shard_len, shard_len, shard_len, d_frag_hex,
+                     n_sh, k * 64)
+        return t
 
     def tick(self, max_blocks: int = 0) -> None:
         """Advance every live chain by at most max_blocks blocks (0: to completion)."""

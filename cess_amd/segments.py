@@ -295,9 +295,9 @@ class SegmentEncoder:
         if self.hash_on == "gpu":
             k, m, F = self.k, self.m, self.F
             self.hash_stream.wait_event(ready)
-            self.hq.add_fragments(self.d_data[dslot], self.d_par[dslot], nseg, k, m, F,
-                                  self.d_fhex[dslot])
-            return self.hq.add_segments(self.d_data[dslot], nseg, k * F, self.d_shex[dslot])
+            # segment chains also give data fragment 0's hash (prefix digest, cec_hashq_add_prefix)
+            return self.hq.add_segment_lists(self.d_data[dslot], self.d_par[dslot], nseg, k, m, F,
+                                             self.d_shex[dslot], self.d_fhex[dslot])
         return None
 
     def _copy_hashes(self, dslot: int, nseg: int):

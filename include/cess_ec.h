@@ -102,7 +102,7 @@ int cec_sha256_hex(const uint8_t* const* d_bufs, size_t n, size_t len, uint8_t* 
  * Completion is tracked on the host from the lengths alone (no read-back): an add is complete
  * once the ticks enqueued so far cover its blocks, i.e. when the stream reaches that tick. */
 typedef struct cec_hashq cec_hashq;
-/* capacity: maximum live chains, a power of two (64 B of HBM each). */
+/* capacity: maximum live chains, a power of two (128 B of HBM each). */
 int cec_hashq_create(int device, size_t capacity, void* hip_stream, cec_hashq** out);
 /* Synchronises the queue's stream, then frees the table. */
 void cec_hashq_destroy(cec_hashq* q);
@@ -114,6 +114,15 @@ void cec_hashq_destroy(cec_hashq* q);
 int cec_hashq_add(cec_hashq* q, const uint8_t* d_base, size_t n, size_t per, size_t outer_stride,
                   size_t inner_stride, size_t len, uint8_t* d_hex, size_t hex_outer,
                   uint64_t* ticket);
+/* cec_hashq_add where chain i also emits the hex of its first prefix_len bytes (a nonzero
+ * multiple of 64, <= len) to d_prefix_hex + ((i / per) * prefix_hex_outer + i % per) * 64.
+ * The segment's chain thus yields data fragment 0's hash on the way (the split is contiguous,
+ * fragment 0 = the segment's first F bytes): 32 instead of 40 MiB hashed per CESS segment.
+ * Both outputs are final once the add is complete. d_prefix_hex NULL = cec_hashq_add. */
+int cec_hashq_add_prefix(cec_hashq* q, const uint8_t* d_base, size_t n, size_t per,
+                         size_t outer_stride, size_t inner_stride, size_t len, uint8_t* d_hex,
+                         size_t hex_outer, size_t prefix_len, uint8_t* d_prefix_hex,
+                         size_t prefix_hex_outer, uint64_t* ticket);
 /* Advance every live chain by at most max_blocks 64-byte blocks (0 = to completion). */
 int cec_hashq_tick(cec_hashq* q, uint32_t max_blocks);
 /* Tick until every chain added so far is complete (enqueued; synchronise the stream to wait). */

@@ -70,9 +70,12 @@ def test_shavs_through_queue(torch, cess, tick_variant):
 
 @pytest.mark.parametrize("k,m,F", [(2, 1, 65536), (4, 2, 4160), (32, 32, 1000), (2, 1, 56)])
 @pytest.mark.parametrize("max_blocks", [1, 37, 0])
-def test_batch_window(torch, cess, k, m, F, max_blocks, tick_variant):
+@pytest.mark.parametrize("combined", [False, True], ids=["separate", "prefix"])
+def test_batch_window(torch, cess, k, m, F, max_blocks, combined, tick_variant):
     """Fragments + segment hashes of several batches added one per step, one tick per step
-    (a window of batches in flight), then drained: every hex matches hashlib."""
+    (a window of batches in flight), then drained: every hex matches hashlib. "prefix": one
+    add_segment_lists per batch, fragment 0's hash from the segment chain's prefix digest
+    (F % 64 == 0; F = 1000 and 56 take the separate-chain fallback)."""
     nseg, nbatch = 5, 4
     rng = np.random.default_rng(k * 1000 + F + max_blocks)
     data = rng.integers(0, 256, (nbatch, nseg, k, F), dtype=np.uint8)
@@ -84,8 +87,12 @@ def test_batch_window(torch, cess, k, m, F, max_blocks, tick_variant):
     q = cess.HashQueue(capacity=2048, stream=st)
     tickets = []
     for b in range(nbatch):
-        t1 = q.add_fragments(d_data[b], d_par[b], nseg, k, m, F, d_fhex[b])
-        t2 = q.add_segments(d_data[b], nseg, k * F, d_shex[b])
+        if combined:
+            t1 = t2 = q.add_segment_lists(d_data[b], d_par[b], nseg, k, m, F, d_shex[b],
+                                          d_fhex[b])
+        else:
+            t1 = q.add_fragments(d_data[b], d_par[b], nseg, k, m, F, d_fhex[b])
+            t2 = q.add_segments(d_data[b], nseg, k * F, d_shex[b])
         tickets.append((t1, t2))
         q.tick(max_blocks)
         if max_blocks == 0:
@@ -105,6 +112,44 @@ def test_batch_window(torch, cess, k, m, F, max_blocks, tick_variant):
             for i in range(k + m):
                 frag = data[b, s, i] if i < k else par[b, s, i - k]
                 assert fh[b, s, i] == hashlib.sha256(frag.tobytes()).hexdigest(), (b, s, i)
+
+
+@pytest.mark.parametrize("max_blocks", [1, 5, 0])
+def test_prefix_digest(torch, cess, max_blocks, tick_variant):
+    """cec_hashq_add_prefix: chains of different lengths whose prefix ends at the first
+    block, mid-chain, at the last whole block and at the full (64-multiple) length; ticks of
+    1, 5 and all blocks put the prefix boundary inside, at the start and at the end of a tick."""
+    cases = [(64 * 9, 64), (64 * 9, 64 * 5), (64 * 9 + 57, 64 * 9), (64 * 12, 64 * 12),
+             (64 * 20 + 3, 64 * 10)]
+    rng = np.random.default_rng(77 + max_blocks)
+    st = torch.cuda.current_stream()
+    q = cess.HashQueue(capacity=64, stream=st)
+    bufs, outs = [], []
+    for n, (length, plen) in enumerate(cases):
+        data = rng.integers(0, 256, (3, length), dtype=np.uint8)
+        d = torch.from_numpy(data).cuda()
+        hx = torch.zeros((3, 64), dtype=torch.uint8, device="cuda")
+        px = torch.zeros((3, 64), dtype=torch.uint8, device="cuda")
+        q.add(d, 3, 1, length, length, length, hx, 1, 0, plen, px, 1, 0)
+        q.tick(max_blocks)
+        bufs.append((data, plen))
+        outs.append((hx, px, d))  # d stays alive until the chains are done
+    q.finish()
+    torch.cuda.synchronize()
+    q.close()
+    for (data, plen), (hx, px, _) in zip(bufs, outs):
+        for i in range(3):
+            assert hexes(hx)[i] == hashlib.sha256(data[i].tobytes()).hexdigest()
+            assert hexes(px)[i] == hashlib.sha256(data[i, :plen].tobytes()).hexdigest(), plen
+
+
+def test_prefix_rejects_bad_length(torch, cess):
+    d = torch.zeros(1024, dtype=torch.uint8, device="cuda")
+    hx = torch.zeros((1, 64), dtype=torch.uint8, device="cuda")
+    with cess.HashQueue(capacity=16) as q:
+        for plen in (63, 2048):
+            with pytest.raises(Exception):
+                q.add(d, 1, 1, 0, 0, 1024, hx, 1, 0, plen, hx, 1, 0)
 
 
 def test_matches_batch_kernel_full_geometry(torch, cess, tick_variant):
