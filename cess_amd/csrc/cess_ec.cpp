@@ -5,6 +5,7 @@
 // host-buffer API. Multi-GPU sharding lives above this library (one codec per device).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -154,6 +155,9 @@ struct cec_codec {
   size_t ps_ptrs_bytes = 0;
   std::vector<std::pair<std::string, std::pair<size_t, size_t>>> ps_ct;
   std::vector<PsLaunch> ps_rt;
+  // RS(2,1), every segment a single erasure: offset/count of the tagged list (segment |
+  // erased << 30) in ps_list for one mixed-pattern launch (count 0: none)
+  size_t ps_mixed_off = 0, ps_mixed_count = 0;
 
   ~cec_codec() {
     (void)hipSetDevice(device);
@@ -434,6 +438,7 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
     c->ps_valid = false;
     c->ps_ct.clear();
     c->ps_rt.clear();
+    c->ps_mixed_count = 0;
     std::unordered_map<std::string, std::vector<uint32_t>> groups;
     for (size_t s = 0; s < nseg; ++s) groups[pkey.substr(s * n, n)].push_back((uint32_t)s);
     bool all_ct = !c->force_generic;
@@ -449,12 +454,21 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
     std::vector<uint32_t> hl;
     std::vector<const uint32_t*> hp;
     if (all_ct) {
+      std::vector<uint32_t> tagged;
       for (auto& g : groups) {
         const Program* p = nullptr;
         get_decode(c, reinterpret_cast<const uint8_t*>(g.first.data()), data_only != 0, &p);
         if (!p->nout) continue;
         c->ps_ct.push_back({g.first, {hl.size(), g.second.size()}});
         hl.insert(hl.end(), g.second.begin(), g.second.end());
+        for (uint32_t sg : g.second) tagged.push_back(sg | ((uint32_t)p->single << 30));
+      }
+      if (c->k == 2 && c->m == 1 && c->ps_ct.size() > 1 && nseg < (1u << 30)) {
+        std::sort(tagged.begin(), tagged.end(),
+                  [](uint32_t a, uint32_t b) { return (a & 0x3FFFFFFFu) < (b & 0x3FFFFFFFu); });
+        c->ps_mixed_off = hl.size();
+        c->ps_mixed_count = tagged.size();
+        hl.insert(hl.end(), tagged.begin(), tagged.end());
       }
     } else {
       size_t maxchunks = 0;
@@ -494,6 +508,10 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
     c->ps_key = std::move(pkey);
     c->ps_valid = true;
   }
+  if (c->ps_mixed_count &&
+      cec::launch_decode1_mixed(c->k, c->m, L, c->ps_list + c->ps_mixed_off,
+                                (uint32_t)c->ps_mixed_count, st))
+    return check_launch();
   for (const auto& w : c->ps_ct) {
     const Program* p = nullptr;
     int rc = get_decode(c, reinterpret_cast<const uint8_t*>(w.first.data()), data_only != 0, &p);

@@ -48,6 +48,10 @@ bool launch_encode_ct(int k, int m, const Layout& L, const uint32_t* seg_list, u
 // erased shard index and `data_only` drops a parity output.
 bool launch_decode_ct(int k, int m, int missing, const Layout& L, const uint32_t* seg_list,
                       uint32_t nseg, hipStream_t st);
+// RS(2,1) single erasures, a different one per segment, in one launch: tagged[i] = segment |
+// (erased index << 30) for the nseg segments of the launch. False if not applicable.
+bool launch_decode1_mixed(int k, int m, const Layout& L, const uint32_t* tagged, uint32_t nseg,
+                          hipStream_t st);
 
 // Whether a compile-time single-erasure decode kernel exists for (k, m, missing).
 bool has_decode_ct(int k, int m, int missing);

@@ -506,11 +506,10 @@ __global__ __launch_bounds__(BS) void k_hg(Layout L, const uint32_t* __restrict_
   if ((L.len % 4) && blockIdx.x == gridDim.x - 1) ct_tail<P, 4>(L, seg);
 }
 
-template <class P, int U, bool NT, class TV = u32x4, int PF = 1, bool WIN = false, int BS = 256>
-__global__ __launch_bounds__(BS) void k_ct(Layout L, const uint32_t* __restrict__ seg_list,
-                                            uint32_t seg0) {
+// One workgroup's tile (blockIdx.x) of segment `seg`; k_ct and the mixed-pattern kernel below.
+template <class P, int U, bool NT, class TV, int PF, bool WIN, int BS>
+__device__ __forceinline__ void ct_tile(const Layout& L, uint32_t seg) {
   constexpr int VB = sizeof(TV);  // bytes per lane per shard per column
-  const uint32_t seg = seg_list ? seg_list[seg0 + blockIdx.y] : seg0 + blockIdx.y;
   const uint64_t nvec = L.len / VB;
   const uint64_t base = (uint64_t)blockIdx.x * (BS * U) + threadIdx.x;
   // Shard pointers are recomputed per use (scalar base + index * stride): holding 2 * (NI + NO)
@@ -535,6 +534,28 @@ __global__ __launch_bounds__(BS) void k_ct(Layout L, const uint32_t* __restrict_
     });
   }
   if ((L.len % VB) && blockIdx.x == gridDim.x - 1) ct_tail<P, VB>(L, seg);
+}
+
+template <class P, int U, bool NT, class TV = u32x4, int PF = 1, bool WIN = false, int BS = 256>
+__global__ __launch_bounds__(BS) void k_ct(Layout L, const uint32_t* __restrict__ seg_list,
+                                            uint32_t seg0) {
+  const uint32_t seg = seg_list ? seg_list[seg0 + blockIdx.y] : seg0 + blockIdx.y;
+  ct_tile<P, U, NT, TV, PF, WIN, BS>(L, seg);
+}
+
+// RS(2,1) degraded read with a different single erasure per segment, in one launch: entry
+// seg | (erased << 30) of the tagged list picks the compile-time rebuild for the workgroup row
+// (a wave-uniform branch), where one launch per erasure pattern over a third of the batch each
+// paid three ramp-ups and drains per batch.
+template <bool NT, int BS>
+__global__ __launch_bounds__(BS) void k_ct_dec1_mixed21(Layout L,
+                                                        const uint32_t* __restrict__ tagged,
+                                                        uint32_t seg0) {
+  const uint32_t w = tagged[seg0 + blockIdx.y];
+  const uint32_t seg = w & 0x3FFFFFFFu, e = w >> 30;
+  if (e == 0) ct_tile<Dec1CT<2, 1, 0>, 1, NT, u32x4, 1, false, BS>(L, seg);
+  else if (e == 1) ct_tile<Dec1CT<2, 1, 1>, 1, NT, u32x4, 1, false, BS>(L, seg);
+  else ct_tile<EncCT<2, 1>, 1, NT, u32x4, 1, false, BS>(L, seg);
 }
 
 // Persistent grid-stride variant: a fixed grid walks the flattened (segment, tile) space.
@@ -1111,6 +1132,19 @@ bool launch_encode_ct(int k, int m, const Layout& L, const uint32_t* seg_list, u
   if (k == 2 && m == 1) { run_ct_variant<EncCT<2, 1>>(L, seg_list, nseg, st); return true; }
   if (k == 32 && m == 32) { run_wide_variant<EncCT<32, 32>>(L, seg_list, nseg, st); return true; }
   return false;
+}
+
+bool launch_decode1_mixed(int k, int m, const Layout& L, const uint32_t* tagged, uint32_t nseg,
+                          hipStream_t st) {
+  // the r01 default variant only (a variant set for a sweep keeps the per-pattern launches)
+  if (k != 2 || m != 1 || g_ct_variant != -1 || !layout_vec16_ok(L)) return false;
+  uint64_t gx = (L.len / 16 + 255) / 256;
+  if (gx == 0) gx = 1;
+  for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {
+    hipLaunchKernelGGL((k_ct_dec1_mixed21<true, 256>), dim3((unsigned)gx, ny), dim3(256), 0, st,
+                       L, tagged, s0);
+  });
+  return true;
 }
 
 bool launch_decode_ct(int k, int m, int missing, const Layout& L, const uint32_t* seg_list,

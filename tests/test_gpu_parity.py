@@ -120,7 +120,8 @@ def test_reconstruct_too_few(cess):
 
 
 @pytest.mark.parametrize("k,m,ln,nseg", [(2, 1, 4096, 9), (4, 2, 1000, 7), (32, 32, 4096, 5),
-                                         (10, 4, 4099, 6), (2, 1, 1, 3)])
+                                         (10, 4, 4099, 6), (2, 1, 1, 3), (2, 1, 4099, 8),
+                                         (2, 1, (1 << 16) + 16, 2)])
 @pytest.mark.parametrize("generic", [0, 1])
 def test_reconstruct_batch_per_segment(torch, cess, corc, k, m, ln, nseg, generic):
     rng = np.random.default_rng(k * 1000 + ln)
