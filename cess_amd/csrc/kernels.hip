@@ -368,6 +368,21 @@ __device__ __forceinline__ uint32_t xt_fast2(uint32_t x) {
   return __builtin_amdgcn_bitop3_b32((x ^ t) + a2, v, 0x1d1d1d1du, 0x78);
 }
 
+// xtime in the bit-reversed representation (each byte's bits mirrored: v_bfrev_b32 of a dword
+// mirrors its bytes and reverses their order, which the byte-wise arithmetic does not see).
+// Multiplying by 2 is then a RIGHT shift, a full-rate op LLVM leaves alone, and the reduction
+// constant 0x1D becomes 0xB8: r' = ((r >> 1) & 0x7F) ^ (r0 ? 0xB8 : 0). The mask comes from
+// w = 0x80 - r0 (0x80 or 0x7F), and w & 0xB8 is the wanted term XOR a constant 0x80 in every
+// byte. xt_rev omits that constant: xtime is GF(2)-linear, so the omission adds a data-independent
+// error e = 1 ^ 2 ^ ... ^ 2^(n-1) = 2^n - 1 (original representation) after n xtimes, removed
+// once per output. 5 full-rate ops, no inline asm (xt_fast: 6 ops + a hazard s_nop).
+__device__ __forceinline__ uint32_t xt_rev(uint32_t r) {
+  const uint32_t t = r & 0x01010101u;
+  const uint32_t s = (r >> 1) & 0x7f7f7f7fu;
+  const uint32_t w = 0x80808080u - t;
+  return __builtin_amdgcn_bitop3_b32(s, w, 0xb8b8b8b8u, 0x78);  // s ^ (w & 0xB8)
+}
+
 // Output row o of a wide code is evaluated by Horner's rule over coefficient bits,
 //   y = 2*y ^ S_b,   S_b = XOR of x_j over inputs j whose coefficient c[o][j] has bit b set,
 // with S_b read from per-group tables: inputs are split into groups of G = 4 and every XOR
@@ -416,10 +431,27 @@ constexpr int ctz_c(unsigned v) {
   return b;
 }
 
-// FL bit 1: xt_fast2 instead of xt_fast; bit 2: scheduling barrier between output rows.
+// FL bit 1: xt_fast2 instead of xt_fast; bit 2: scheduling barrier between output rows; bit 3:
+// bit-reversed representation (inputs v_bfrev'd on load, xt_rev, outputs reversed back and
+// corrected by 2^top - 1 per byte).
 template <class P, int G, int FL, class LD, class ST>
-__device__ __forceinline__ void ct_column_hgroup(LD ld, ST st) {
+__device__ __forceinline__ void ct_column_hgroup(LD ld_, ST st_) {
   using H = HGroup<P, G>;
+  constexpr bool REV = (FL & 8) != 0;
+  auto ld = [&](auto J) CEC_AI -> uint32_t {
+    if constexpr (REV) return __builtin_bitreverse32(ld_(J));
+    else return ld_(J);
+  };
+  auto st = [&](auto O, uint32_t y) CEC_AI {
+    if constexpr (REV) {
+      constexpr int top = P::v.hb_row[(int)O];
+      constexpr uint32_t corr = top > 0 ? ((1u << top) - 1u) * 0x01010101u : 0u;
+      if constexpr (corr) st_(O, __builtin_bitreverse32(y) ^ corr);
+      else st_(O, __builtin_bitreverse32(y));
+    } else {
+      st_(O, y);
+    }
+  };
   uint32_t comb[H::NG][1 << G];
   static_for<H::NG>([&](auto Gi) CEC_AI {
     constexpr int g = Gi;
@@ -450,7 +482,8 @@ __device__ __forceinline__ void ct_column_hgroup(LD ld, ST st) {
           else
             y = comb[tl.g[0]][tl.v[0]];
         } else {
-          if constexpr (FL & 2) y = xt_fast2(y);
+          if constexpr (REV) y = xt_rev(y);
+          else if constexpr (FL & 2) y = xt_fast2(y);
           else y = xt_fast(y);
         }
         constexpr int s0 = b == top ? (tl.n >= 3 ? 3 : tl.n) : 0;
@@ -1118,6 +1151,8 @@ void run_wide_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, 
     case 14: run_hg<P, 4, 4>(L, seg_list, nseg, st); break;
     case 15: run_hg<P, 4, 0, 128>(L, seg_list, nseg, st); break;
     case 16: run_hg<P, 4, 0, 512>(L, seg_list, nseg, st); break;
+    case 17: run_hg<P, 4, 8>(L, seg_list, nseg, st); break;
+    case 18: run_hg<P, 3, 8>(L, seg_list, nseg, st); break;
     case 10: run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st); break;  // r01 default
     default: run_hg<P, 4, 0>(L, seg_list, nseg, st); break;  // r01 sweep: 3.11 -> 5.26 TB/s
   }
