@@ -342,7 +342,7 @@ def main() -> None:
                             "per-wave issue rate, reported apart from the HBM roofline"}
 
     tag = f"c{args.config}"
-    kernel_name = {2: "k_ct<EncCT<2, 1>>", 3: "k_ct<Dec1CT<2, 1, *>> / k_ct<EncCT<2, 1>>",
+    kernel_name = {2: "k_ct<EncCT<2, 1>>", 3: "k_ct_dec1_mixed21 (Dec1CT<2, 1, e> / EncCT<2, 1> per segment)",
                    4: "k_ct<EncCT<2, 1>>", 5: "k_hg<EncCT<32, 32>, 4>", 6: "k_rthx<8>",
                    7: "k_rthx<8>", 8: "k_rthx<3>"}[args.config]
     if args.generic:
