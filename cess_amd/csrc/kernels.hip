@@ -368,6 +368,17 @@ __device__ __forceinline__ uint32_t xt_fast2(uint32_t x) {
   return __builtin_amdgcn_bitop3_b32((x ^ t) + a2, v, 0x1d1d1d1du, 0x78);
 }
 
+// xt_fast with the sign-bit mask in an SGPR (`c80`, set once per kernel by an s_mov in asm, so
+// LLVM cannot fold it back into a literal): the two 32-bit literals per xtime (0x80808080 and
+// the canonicalised 0x7f7f7f7f) make 8-byte instructions; SGPR operands keep them at 4 bytes.
+// The straight-line k_hg body is ~17 KB and a CU pair fetches it for 8 SIMDs, so instruction
+// bytes per VALU op are a co-limiter (SQ_WAIT_INST_ANY rose with a literal-heavier xtime).
+__device__ __forceinline__ uint32_t xt_fast_sc(uint32_t x, uint32_t c80, uint32_t c7f) {
+  const uint32_t t = x & c80;
+  const uint32_t v = t - (t >> 7);
+  return __builtin_amdgcn_bitop3_b32(add_self(x & c7f), v, 0x1d1d1d1du, 0x78);  // a ^ (b & c)
+}
+
 // xtime in the bit-reversed representation (each byte's bits mirrored: v_bfrev_b32 of a dword
 // mirrors its bytes and reverses their order, which the byte-wise arithmetic does not see).
 // Multiplying by 2 is then a RIGHT shift, a full-rate op LLVM leaves alone, and the reduction
@@ -433,11 +444,16 @@ constexpr int ctz_c(unsigned v) {
 
 // FL bit 1: xt_fast2 instead of xt_fast; bit 2: scheduling barrier between output rows; bit 3:
 // bit-reversed representation (inputs v_bfrev'd on load, xt_rev, outputs reversed back and
-// corrected by 2^top - 1 per byte).
+// corrected by 2^top - 1 per byte); bit 4: xt_fast_sc (mask constant in an SGPR).
 template <class P, int G, int FL, class LD, class ST>
 __device__ __forceinline__ void ct_column_hgroup(LD ld_, ST st_) {
   using H = HGroup<P, G>;
   constexpr bool REV = (FL & 8) != 0;
+  uint32_t c80 = 0x80808080u, c7f = 0x7f7f7f7fu;
+  if constexpr ((FL & 16) != 0) {
+    asm volatile("s_mov_b32 %0, 0x80808080" : "=s"(c80));
+    asm volatile("s_mov_b32 %0, 0x7f7f7f7f" : "=s"(c7f));
+  }
   auto ld = [&](auto J) CEC_AI -> uint32_t {
     if constexpr (REV) return __builtin_bitreverse32(ld_(J));
     else return ld_(J);
@@ -483,6 +499,7 @@ __device__ __forceinline__ void ct_column_hgroup(LD ld_, ST st_) {
             y = comb[tl.g[0]][tl.v[0]];
         } else {
           if constexpr (REV) y = xt_rev(y);
+          else if constexpr (FL & 16) y = xt_fast_sc(y, c80, c7f);
           else if constexpr (FL & 2) y = xt_fast2(y);
           else y = xt_fast(y);
         }
@@ -1153,6 +1170,8 @@ void run_wide_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, 
     case 16: run_hg<P, 4, 0, 512>(L, seg_list, nseg, st); break;
     case 17: run_hg<P, 4, 8>(L, seg_list, nseg, st); break;
     case 18: run_hg<P, 3, 8>(L, seg_list, nseg, st); break;
+    case 19: run_hg<P, 4, 16>(L, seg_list, nseg, st); break;
+    case 20: run_hg<P, 4, 17>(L, seg_list, nseg, st); break;
     case 10: run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st); break;  // r01 default
     default: run_hg<P, 4, 0>(L, seg_list, nseg, st); break;  // r01 sweep: 3.11 -> 5.26 TB/s
   }

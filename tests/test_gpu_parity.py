@@ -161,7 +161,7 @@ def test_ct_variants_identical(torch, cess, corc, k, m, ln):
     want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
     d_data = to_dev(torch, data)
     enc = cess.New(k, m)
-    for v in range(-1, 19):
+    for v in range(-1, 21):
         enc.set_option(2, v)
         d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
         enc.EncodeBatch(d_data, d_par, nseg, ln)
