@@ -175,14 +175,15 @@ def main() -> None:
     d_data = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
     d_par = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
     cess_amd.fill_synthetic(d_data, k * F, nseg, seg0, SEED0 + args.config, stream=stream)
-    enc = cess_amd.New(k, m, device=local)
+    # kernel variants (--variant / --sweep) live in the tuning build of the library only
+    tuning = bool(args.sweep) or args.variant != -1
+    enc = cess_amd.New(k, m, device=local, tuning=tuning)
     if args.generic:
         enc.set_option(1, 1)
-    enc.set_option(2, args.variant)
+    if tuning:
+        enc.set_option(2, args.variant)
     enc.set_option(3, args.sha_mode)
     enc.set_option(4, args.rt_mode)
-    if args.tick_pf:
-        enc.set_option(5, args.tick_pf)
     enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)  # valid parity for config 3
 
     present = None
@@ -216,6 +217,8 @@ def main() -> None:
         chains = W * nseg * (k + m)
         hq = cess_amd.HashQueue(capacity=1 << max(10, (chains - 1).bit_length()), device=local,
                                 stream=sha_stream)
+        if args.tick_pf:
+            hq.set_option(1, args.tick_pf)
         tick_blocks = -(-cess_amd.sha256_blocks(F) // W)
         ev_enc = [torch.cuda.Event() for _ in range(NB)]
         ev_free = [torch.cuda.Event() for _ in range(NB)]

@@ -8,6 +8,9 @@ from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint32, c_uint
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CESS_EC_LIB", os.path.join(_HERE, "libcessec.so"))
+# tuning build of the same library: every kernel variant of the sweeps (CEC_OPT_CT_VARIANT);
+# used only by bench.py --sweep and the variant tests, never by the product path
+TUNE_LIB_PATH = os.path.join(_HERE, "libcessec_tune.so")
 
 # exported symbols and their (restype, argtypes); tests check this against include/cess_ec.h
 SIGNATURES = {
@@ -31,6 +34,7 @@ SIGNATURES = {
     "cec_split_segment": (c_int, [c_void_p, c_size_t, c_int, POINTER(c_void_p), c_size_t]),
     "cec_fill_synthetic": (c_int, [c_void_p, c_size_t, c_size_t, c_uint64, c_uint64, c_void_p]),
     "cec_set_option": (c_int, [c_void_p, c_int, c_int]),
+    "cec_get_stat": (c_int, [c_void_p, c_int, POINTER(c_uint64)]),
     "cec_hashq_create": (c_int, [c_int, c_size_t, c_void_p, POINTER(c_void_p)]),
     "cec_hashq_destroy": (None, [c_void_p]),
     "cec_hashq_add": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_size_t,
@@ -42,6 +46,7 @@ SIGNATURES = {
     "cec_hashq_finish": (c_int, [c_void_p]),
     "cec_hashq_status": (c_int, [c_void_p, c_uint64, POINTER(c_int), POINTER(c_size_t),
                                  POINTER(c_uint64)]),
+    "cec_hashq_set_option": (c_int, [c_void_p, c_int, c_int]),
 }
 
 CEC_OK = 0
@@ -53,25 +58,35 @@ CEC_ENOMEM = -5
 CEC_ENCCL = -6
 CEC_ESHORTDATA = -7
 CEC_ENODEV = -8
+CEC_ESEGCOUNT = -9
+CEC_ECALLBACK = -10
 
 CEC_OPT_FORCE_GENERIC = 1
 CEC_OPT_CT_VARIANT = 2
+CEC_OPT_SHA_MODE = 3
+CEC_OPT_RT_MODE = 4
+CEC_OPT_DECODE_CACHE = 6
+CEC_STAT_DECODE_CACHED = 1
+CEC_STAT_RETIRED_PENDING = 2
+CEC_HQOPT_TICK = 1
 
-_lib = None
+_libs = {}
 
 
-def load() -> ctypes.CDLL:
-    """Load libcessec once; raises OSError with a build hint when it is missing."""
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise OSError(f"libcessec not found at {LIB_PATH}: build it with "
+def load(tuning: bool = False) -> ctypes.CDLL:
+    """Load libcessec (or its tuning build) once; raises OSError with a build hint when it is
+    missing."""
+    path = TUNE_LIB_PATH if tuning else LIB_PATH
+    lib = _libs.get(path)
+    if lib is None:
+        if not os.path.exists(path):
+            raise OSError(f"libcessec not found at {path}: build it with "
                           "`python -c 'import __graft_entry__ as g; g.build()'` "
                           "or `make -C cess_amd/csrc`")
-        lib = ctypes.CDLL(LIB_PATH)
+        lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        _lib = lib
-    return _lib
+        _libs[path] = lib
+    return lib

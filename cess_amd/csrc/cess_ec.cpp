@@ -1,15 +1,26 @@
 // libcessec host side: the C ABI of include/cess_ec.h over the HIP kernels in kernels.hip.
 //
 // Owns, per codec: the (k+m) x k encode matrix (gf256.h), the run-time coefficient programs in
-// HBM (encode + one per erasure pattern, cached), a HIP stream and a staging area in HBM for the
-// host-buffer API. Multi-GPU sharding lives above this library (one codec per device).
+// HBM (encode + one per erasure pattern in an LRU cache), the plan of the last per-segment
+// reconstruct, the kernel selection (KernelOpts), a private HIP stream for uploads and a staging
+// area in HBM for the host-buffer API. Multi-GPU sharding lives above this library (one codec
+// per device).
+//
+// Lifetime of device blocks (coefficient programs, per-segment plans): a block can still be read
+// by kernels enqueued on any caller stream after the host has dropped it (an evicted pattern, a
+// replaced plan). Blocks come from a per-codec DevPool and are never freed in place: dropping the
+// last reference retires the block, and a retired block is reused or freed only once every
+// launch enqueued before the retirement has completed. Each call that launches kernels reading
+// pool blocks records a mark event on its stream; a block retired after mark n waits for marks
+// 1..n (host-side event queries, no device-wide synchronisation).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <list>
 #include <memory>
-#include <mutex>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -19,15 +30,9 @@
 #include "gf256.h"
 #include "kernels.h"
 
-namespace cec {
-void set_ct_variant(int v);
-void set_sha_mode(int v);
-void set_rt_mode(int v);
-void set_tick_prefetch(int v);
-}
-
 namespace {
 
+using cec::KernelOpts;
 using cec::Layout;
 using BigMat = cec::Mat<cec::kMaxShards, cec::kMaxShards>;
 using WorkMat = cec::Mat<cec::kMaxShards, 2 * cec::kMaxShards>;
@@ -48,10 +53,109 @@ int set_err(int code, const std::string& msg) {
                      std::string(#expr) + ": " + hipGetErrorString(_e));                \
   } while (0)
 
+// ---- device block pool with stream-ordered retirement -------------------------------------
+class DevPool {
+ public:
+  ~DevPool() { drain(); }
+
+  // A block of at least `bytes` (size classes of powers of two from 4 KiB).
+  int alloc(size_t bytes, void** out) {
+    collect();
+    const int c = cls(bytes);
+    if ((size_t)c < free_.size() && !free_[c].empty()) {
+      *out = free_[c].back();
+      free_[c].pop_back();
+      return CEC_OK;
+    }
+    HIP_TRY(hipMalloc(out, (size_t)1 << c));
+    return CEC_OK;
+  }
+  // The last reference to a block was dropped; kernels enqueued so far may still read it.
+  void retire(void* p, size_t bytes) {
+    if (p) dead_.push_back({seq_, p, cls(bytes)});
+  }
+  // Record the completion point of the launches just enqueued on `st`.
+  int mark(hipStream_t st) {
+    hipEvent_t ev = nullptr;
+    if (!evpool_.empty()) {
+      ev = evpool_.back();
+      evpool_.pop_back();
+    } else {
+      HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    hipError_t e = hipEventRecord(ev, st);
+    if (e != hipSuccess) {
+      evpool_.push_back(ev);
+      return set_err(CEC_EHIP, std::string("hipEventRecord: ") + hipGetErrorString(e));
+    }
+    marks_.push_back({++seq_, ev});
+    // bound the backlog of a producer that never synchronises
+    while (marks_.size() > 1024) {
+      (void)hipEventSynchronize(marks_.front().ev);
+      collect();
+    }
+    return CEC_OK;
+  }
+  // Move retired blocks whose readers have completed to the free lists.
+  void collect() {
+    while (!marks_.empty() && hipEventQuery(marks_.front().ev) == hipSuccess) {
+      done_ = marks_.front().seq;
+      evpool_.push_back(marks_.front().ev);
+      marks_.pop_front();
+    }
+    if (marks_.empty()) done_ = seq_;
+    while (!dead_.empty() && dead_.front().tag <= done_) {
+      const Dead& d = dead_.front();
+      if ((size_t)d.c >= free_.size()) free_.resize(d.c + 1);
+      free_[d.c].push_back(d.p);
+      dead_.pop_front();
+    }
+  }
+  // Wait for every mark and free every block (codec destruction).
+  void drain() {
+    for (auto& m : marks_) {
+      (void)hipEventSynchronize(m.ev);
+      evpool_.push_back(m.ev);
+    }
+    marks_.clear();
+    done_ = seq_;
+    collect();
+    for (auto& fl : free_)
+      for (void* p : fl) (void)hipFree(p);
+    free_.clear();
+    for (hipEvent_t e : evpool_) (void)hipEventDestroy(e);
+    evpool_.clear();
+  }
+  size_t pending() const { return dead_.size(); }
+
+ private:
+  static int cls(size_t bytes) {
+    int c = 12;
+    while (((size_t)1 << c) < bytes) ++c;
+    return c;
+  }
+  struct Dead {
+    uint64_t tag;
+    void* p;
+    int c;
+  };
+  struct Mark {
+    uint64_t seq;
+    hipEvent_t ev;
+  };
+  std::vector<std::vector<void*>> free_;
+  std::deque<Dead> dead_;  // in retirement order, so tags are non-decreasing
+  std::deque<Mark> marks_;
+  std::vector<hipEvent_t> evpool_;
+  uint64_t seq_ = 0;   // marks recorded
+  uint64_t done_ = 0;  // every mark <= done_ has completed
+};
+
 // A run-time program: chunks of up to kRtMaxOut outputs, each a device block in the layout of
 // kernels.h (header, input indices, output indices, coefficients [nin][nob]).
 struct RtChunk {
   uint32_t* dev = nullptr;
+  size_t bytes = 0;
   int nin = 0, nout = 0, nob = 0;
 };
 
@@ -62,26 +166,30 @@ struct Program {
   uint8_t in_idx[cec::kMaxShards] = {};   // survivors read (host copy)
   uint8_t out_idx[cec::kMaxShards] = {};  // shards written (host copy)
 };
+using ProgPtr = std::shared_ptr<const Program>;
 
-void free_program(Program& p) {
-  for (auto& c : p.chunks)
-    if (c.dev) (void)hipFree(c.dev);
-  p.chunks.clear();
-}
-
-// Upload coefficient rows for outputs out_idx[o] (coef[o][j]) as run-time chunks.
-int build_program(const uint8_t* in_idx, int nin, const uint8_t* out_idx, int nout,
-                  const BigMat& coef, Program& prog) {
-  prog.nout = nout;
-  prog.single = nout == 1 ? out_idx[0] : -1;
-  std::memcpy(prog.in_idx, in_idx, nin);
-  std::memcpy(prog.out_idx, out_idx, nout);
+// Upload coefficient rows for outputs out_idx[o] (coef[o][j]) as run-time chunks. The chunk
+// blocks come from `pool` and go back to it (retired) when the last ProgPtr is dropped. Uploads
+// run on `upload` and are complete when this returns.
+int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int nin,
+                  const uint8_t* out_idx, int nout, const BigMat& coef, ProgPtr* out) {
+  DevPool* pp = &pool;
+  std::shared_ptr<Program> prog(new Program, [pp](Program* p) {
+    for (auto& c : p->chunks) pp->retire(c.dev, c.bytes);
+    delete p;
+  });
+  prog->nout = nout;
+  prog->single = nout == 1 ? out_idx[0] : -1;
+  std::memcpy(prog->in_idx, in_idx, nin);
+  std::memcpy(prog->out_idx, out_idx, nout);
+  std::vector<std::vector<uint32_t>> hosts;
   for (int o0 = 0; o0 < nout; o0 += cec::kRtMaxOut) {
     RtChunk c;
     c.nin = nin;
     c.nout = std::min(cec::kRtMaxOut, nout - o0);
     c.nob = cec::rt_bucket(c.nout);
-    std::vector<uint32_t> h(cec::rt_chunk_bytes(nin, c.nob) / sizeof(uint32_t), 0u);
+    hosts.emplace_back(cec::rt_chunk_bytes(nin, c.nob) / sizeof(uint32_t), 0u);
+    std::vector<uint32_t>& h = hosts.back();
     h[0] = (uint32_t)nin;
     h[1] = (uint32_t)c.nout;
     h[2] = (uint32_t)c.nob;
@@ -119,53 +227,86 @@ int build_program(const uint8_t* in_idx, int nin, const uint8_t* out_idx, int no
             if (coef.v[o0 + o][j] >> b & 1) ix[((size_t)o * 8 + b) * 8 + j / 4] |= 1u << (j % 4);
       }
     }
-    HIP_TRY(hipMalloc(&c.dev, h.size() * sizeof(uint32_t)));
-    prog.chunks.push_back(c);
-    HIP_TRY(hipMemcpy(c.dev, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c.bytes = h.size() * sizeof(uint32_t);
+    void* d = nullptr;
+    int rc = pool.alloc(c.bytes, &d);
+    if (rc) return rc;  // prog's deleter retires the chunks built so far
+    c.dev = static_cast<uint32_t*>(d);
+    prog->chunks.push_back(c);
+    HIP_TRY(hipMemcpyAsync(c.dev, h.data(), c.bytes, hipMemcpyHostToDevice, upload));
   }
+  // the block may be a reused one whose readers have completed; the upload must land before
+  // any caller-stream launch that reads it, and the host vectors die here
+  HIP_TRY(hipStreamSynchronize(upload));
+  *out = std::move(prog);
   return CEC_OK;
 }
 
 // One multi-pattern run-time launch of the per-segment reconstruct path.
 struct PsLaunch {
   int nob = 0, nin = 0;
-  size_t off = 0, count = 0;  // into the cached segment-list / chunk-pointer arrays
+  size_t off = 0, count = 0;  // into the plan's segment-list / chunk-pointer arrays
 };
+
+// Plan of one per-segment reconstruct call (cached for a repeated pattern array): either
+// compile-time launches per pattern (ct: program, offset, count into list), one mixed-pattern
+// RS(2,1) launch, or multi-pattern run-time launches (rt: segment list + per-segment chunk
+// pointers). `progs` holds every program whose device chunks the arrays point at.
+struct PsPlan {
+  std::string key;
+  std::vector<ProgPtr> progs;
+  std::vector<std::string> keys;  // decode-cache keys of the patterns (LRU touch on reuse)
+  uint32_t* list = nullptr;
+  size_t list_bytes = 0;
+  void* ptrs = nullptr;  // const uint32_t* [count] per run-time launch
+  size_t ptrs_bytes = 0;
+  std::vector<std::pair<ProgPtr, std::pair<size_t, size_t>>> ct;
+  std::vector<PsLaunch> rt;
+  size_t mixed_off = 0, mixed_count = 0;  // tagged list (segment | erased << 30), count 0: none
+};
+
+constexpr size_t kDefaultDecodeCache = 4096;
 
 }  // namespace
 
 struct cec_codec {
   int k = 0, m = 0, device = 0;
   std::unique_ptr<BigMat> E;
-  hipStream_t stream = nullptr;
-  Program encode;
-  std::unordered_map<std::string, Program> decode_cache;
+  hipStream_t stream = nullptr;  // private: uploads and the host-buffer API
+  KernelOpts opts;
   bool force_generic = false;
+  DevPool pool;  // declared before every holder of pool blocks: destroyed after them
+  ProgPtr encode;
+  // decode programs by erasure pattern (n presence flags + data_only), least recently used last
+  struct Entry {
+    ProgPtr prog;
+    std::list<std::string>::iterator lru;
+  };
+  std::unordered_map<std::string, Entry> decode_cache;
+  std::list<std::string> lru;
+  size_t cache_cap = kDefaultDecodeCache;
+  std::unique_ptr<PsPlan> ps;
   // staging for the host-buffer API: [n][stride]
   uint8_t* stage = nullptr;
   size_t stage_bytes = 0;
-  // cached plan of the last per-segment reconstruct call: either compile-time launches per
-  // pattern (ps_ct: pattern key, offset, count into ps_list) or multi-pattern run-time
-  // launches (ps_rt: segment list + per-segment chunk pointers)
-  std::string ps_key;
-  bool ps_valid = false;
-  uint32_t* ps_list = nullptr;
-  size_t ps_list_bytes = 0;
-  uint8_t* ps_ptrs = nullptr;  // const uint32_t* [count] per launch
-  size_t ps_ptrs_bytes = 0;
-  std::vector<std::pair<std::string, std::pair<size_t, size_t>>> ps_ct;
-  std::vector<PsLaunch> ps_rt;
-  // RS(2,1), every segment a single erasure: offset/count of the tagged list (segment |
-  // erased << 30) in ps_list for one mixed-pattern launch (count 0: none)
-  size_t ps_mixed_off = 0, ps_mixed_count = 0;
 
+  void drop_plan() {
+    if (!ps) return;
+    pool.retire(ps->list, ps->list_bytes);
+    pool.retire(ps->ptrs, ps->ptrs_bytes);
+    ps.reset();
+  }
   ~cec_codec() {
     (void)hipSetDevice(device);
-    free_program(encode);
-    for (auto& kv : decode_cache) free_program(kv.second);
+    // the encode program is never retired while the codec lives and batch encodes are not
+    // marked: let every queued launch finish before its blocks go
+    (void)hipDeviceSynchronize();
+    drop_plan();
+    decode_cache.clear();
+    lru.clear();
+    encode.reset();
+    pool.drain();
     if (stage) (void)hipFree(stage);
-    if (ps_list) (void)hipFree(ps_list);
-    if (ps_ptrs) (void)hipFree(ps_ptrs);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -189,16 +330,19 @@ Layout batch_layout(const cec_codec* c, const uint8_t* d_data, const uint8_t* d_
   return L;
 }
 
-void launch_chunk(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
-                  int nin, int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
-  if (nin <= cec::kRthMaxIn && cec::launch_matvec_rth(L, chunk, per_seg, nin, seg_list, nseg, st))
+void launch_chunk(const KernelOpts& o, const Layout& L, const uint32_t* chunk,
+                  const uint32_t* const* per_seg, int nin, int nob, const uint32_t* seg_list,
+                  uint32_t nseg, hipStream_t st) {
+  if (nin <= cec::kRthMaxIn &&
+      cec::launch_matvec_rth(o, L, chunk, per_seg, nin, seg_list, nseg, st))
     return;
   cec::launch_matvec_rt(L, chunk, per_seg, nob, seg_list, nseg, st);
 }
 
-void run_program(const Program& p, const Layout& L, const uint32_t* seg_list, uint32_t nseg,
-                 hipStream_t st) {
-  for (const auto& c : p.chunks) launch_chunk(L, c.dev, nullptr, c.nin, c.nob, seg_list, nseg, st);
+void run_program(const KernelOpts& o, const Program& p, const Layout& L, const uint32_t* seg_list,
+                 uint32_t nseg, hipStream_t st) {
+  for (const auto& c : p.chunks)
+    launch_chunk(o, L, c.dev, nullptr, c.nin, c.nob, seg_list, nseg, st);
 }
 
 int check_launch() {
@@ -210,20 +354,28 @@ int check_launch() {
 int do_encode(cec_codec* c, const Layout& L, const uint32_t* seg_list, uint32_t nseg,
               hipStream_t st) {
   if (nseg == 0 || L.len == 0) return CEC_OK;
-  if (c->force_generic || !cec::launch_encode_ct(c->k, c->m, L, seg_list, nseg, st))
-    run_program(c->encode, L, seg_list, nseg, st);
+  if (c->force_generic || !cec::launch_encode_ct(c->opts, c->k, c->m, L, seg_list, nseg, st))
+    run_program(c->opts, *c->encode, L, seg_list, nseg, st);
   return check_launch();
 }
 
-// Decode program for one erasure pattern (cached).
-int get_decode(cec_codec* c, const uint8_t* present, bool data_only, const Program** out) {
-  const int n = c->k + c->m;
+std::string pattern_key(const uint8_t* present, int n, bool data_only) {
   std::string key(n + 1, '\0');
   for (int i = 0; i < n; ++i) key[i] = present[i] ? 1 : 0;
   key[n] = data_only ? 1 : 0;
+  return key;
+}
+
+// Decode program for one erasure pattern (LRU-cached). Nothing is evicted here: the caller
+// evicts after its launches are enqueued and marked (evict_decode), so a program resolved
+// earlier in the same call is never dropped under it.
+int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* out) {
+  const int n = c->k + c->m;
+  std::string key = pattern_key(present, n, data_only);
   auto it = c->decode_cache.find(key);
   if (it != c->decode_cache.end()) {
-    *out = &it->second;
+    c->lru.splice(c->lru.begin(), c->lru, it->second.lru);
+    *out = it->second.prog;
     return CEC_OK;
   }
   auto plan = std::make_unique<BigPlan>();
@@ -234,32 +386,35 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, const Progr
   for (int i = 0; i < n; ++i) flags[i] = key[i];
   if (cec::gf_decode_plan(c->k, c->m, flags, data_only, *c->E, *plan, *sub, *inv, *work) != 0)
     return set_err(CEC_ETOOFEW, "fewer than k shards present");
-  if (c->decode_cache.size() >= 4096) {
-    // Drain users of the cached device coefficients before freeing them.
-    (void)hipDeviceSynchronize();
-    for (auto& kv : c->decode_cache) free_program(kv.second);
-    c->decode_cache.clear();
-    c->ps_valid = false;  // its chunk pointers referred to the freed programs
-  }
-  Program prog;
+  ProgPtr prog;
   if (plan->nout > 0) {
-    int rc = build_program(plan->in_idx, c->k, plan->out_idx, plan->nout, plan->coef, prog);
-    if (rc) {
-      free_program(prog);
-      return rc;
-    }
+    int rc = build_program(c->pool, c->stream, plan->in_idx, c->k, plan->out_idx, plan->nout,
+                           plan->coef, &prog);
+    if (rc) return rc;
+  } else {
+    prog = std::make_shared<const Program>();
   }
-  auto res = c->decode_cache.emplace(key, std::move(prog));
-  *out = &res.first->second;
+  c->lru.push_front(key);
+  c->decode_cache.emplace(std::move(key), cec_codec::Entry{prog, c->lru.begin()});
+  *out = std::move(prog);
   return CEC_OK;
+}
+
+// Drop least recently used patterns beyond the cap. A dropped program that a cached per-segment
+// plan still uses stays alive through the plan; device blocks are retired, not freed.
+void evict_decode(cec_codec* c) {
+  while (c->decode_cache.size() > c->cache_cap && !c->lru.empty()) {
+    c->decode_cache.erase(c->lru.back());
+    c->lru.pop_back();
+  }
 }
 
 int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* seg_list,
               uint32_t nseg, hipStream_t st) {
   if (p.nout == 0 || nseg == 0 || L.len == 0) return CEC_OK;
   if (c->force_generic || p.single < 0 ||
-      !cec::launch_decode_ct(c->k, c->m, p.single, L, seg_list, nseg, st))
-    run_program(p, L, seg_list, nseg, st);
+      !cec::launch_decode_ct(c->opts, c->k, c->m, p.single, L, seg_list, nseg, st))
+    run_program(c->opts, p, L, seg_list, nseg, st);
   return check_launch();
 }
 
@@ -289,6 +444,130 @@ Layout stage_layout(cec_codec* c, size_t len) {
   return L;
 }
 
+// Build the plan of a per-segment reconstruct for the pattern array `pkey` (nseg * n flags +
+// data_only + force_generic) into *out; device arrays are uploaded and complete on return.
+int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_only,
+                  std::unique_ptr<PsPlan>* out) {
+  const int n = c->k + c->m;
+  auto plan = std::make_unique<PsPlan>();
+  plan->key = pkey;
+  // group segments by pattern, in first-appearance order (deterministic launch order)
+  std::unordered_map<std::string, size_t> gidx;
+  std::vector<std::pair<std::string, std::vector<uint32_t>>> groups;
+  for (size_t s = 0; s < nseg; ++s) {
+    std::string k = pkey.substr(s * n, n);
+    auto it = gidx.find(k);
+    if (it == gidx.end()) {
+      it = gidx.emplace(k, groups.size()).first;
+      groups.push_back({k, {}});
+    }
+    groups[it->second].second.push_back((uint32_t)s);
+  }
+  bool all_ct = !c->force_generic;
+  std::vector<std::pair<ProgPtr, const std::vector<uint32_t>*>> progs;
+  for (auto& g : groups) {
+    ProgPtr p;
+    int rc = get_decode(c, reinterpret_cast<const uint8_t*>(g.first.data()), data_only, &p);
+    if (rc) return rc;
+    plan->keys.push_back(pattern_key(reinterpret_cast<const uint8_t*>(g.first.data()), n,
+                                     data_only));
+    if (!p->nout) continue;
+    progs.push_back({p, &g.second});
+    plan->progs.push_back(p);
+    if (p->single < 0 || !cec::has_decode_ct(c->k, c->m, p->single)) all_ct = false;
+  }
+  std::vector<uint32_t> hl;
+  std::vector<const uint32_t*> hp;
+  if (all_ct) {
+    std::vector<uint32_t> tagged;
+    for (auto& pr : progs) {
+      plan->ct.push_back({pr.first, {hl.size(), pr.second->size()}});
+      hl.insert(hl.end(), pr.second->begin(), pr.second->end());
+      for (uint32_t sg : *pr.second) tagged.push_back(sg | ((uint32_t)pr.first->single << 30));
+    }
+    if (c->k == 2 && c->m == 1 && plan->ct.size() > 1 && nseg < (1u << 30)) {
+      std::sort(tagged.begin(), tagged.end(),
+                [](uint32_t a, uint32_t b) { return (a & 0x3FFFFFFFu) < (b & 0x3FFFFFFFu); });
+      plan->mixed_off = hl.size();
+      plan->mixed_count = tagged.size();
+      hl.insert(hl.end(), tagged.begin(), tagged.end());
+    }
+  } else {
+    size_t maxchunks = 0;
+    for (auto& pr : progs) maxchunks = std::max(maxchunks, pr.first->chunks.size());
+    for (size_t ci = 0; ci < maxchunks; ++ci) {
+      std::vector<std::pair<int, std::vector<std::pair<uint32_t, const uint32_t*>>>> byb;
+      int nin_max = 0;
+      for (auto& pr : progs)
+        if (ci < pr.first->chunks.size()) {
+          const RtChunk& ch = pr.first->chunks[ci];
+          nin_max = std::max(nin_max, ch.nin);
+          auto it = std::find_if(byb.begin(), byb.end(),
+                                 [&](const auto& b) { return b.first == ch.nob; });
+          if (it == byb.end()) it = byb.insert(byb.end(), {ch.nob, {}});
+          for (uint32_t sg : *pr.second) it->second.push_back({sg, ch.dev});
+        }
+      for (auto& b : byb) {
+        PsLaunch l;
+        l.nob = b.first;
+        l.nin = nin_max;
+        l.off = hl.size();
+        l.count = b.second.size();
+        for (auto& e : b.second) {
+          hl.push_back(e.first);
+          hp.push_back(e.second);
+        }
+        plan->rt.push_back(l);
+      }
+    }
+  }
+  void* d = nullptr;
+  plan->list_bytes = std::max<size_t>(hl.size(), 1) * sizeof(uint32_t);
+  int rc = c->pool.alloc(plan->list_bytes, &d);
+  if (rc) return rc;
+  plan->list = static_cast<uint32_t*>(d);
+  plan->ptrs_bytes = std::max<size_t>(hp.size(), 1) * sizeof(void*);
+  rc = c->pool.alloc(plan->ptrs_bytes, &plan->ptrs);
+  if (rc) {
+    c->pool.retire(plan->list, plan->list_bytes);
+    return rc;
+  }
+  hipError_t e = hipSuccess;
+  if (!hl.empty())
+    e = hipMemcpyAsync(plan->list, hl.data(), hl.size() * sizeof(uint32_t),
+                       hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess && !hp.empty())
+    e = hipMemcpyAsync(plan->ptrs, hp.data(), hp.size() * sizeof(void*), hipMemcpyHostToDevice,
+                       c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    c->pool.retire(plan->list, plan->list_bytes);
+    c->pool.retire(plan->ptrs, plan->ptrs_bytes);
+    return set_err(CEC_EHIP, std::string("plan upload: ") + hipGetErrorString(e));
+  }
+  *out = std::move(plan);
+  return CEC_OK;
+}
+
+int launch_ps_plan(cec_codec* c, const PsPlan& p, const Layout& L, hipStream_t st) {
+  if (p.mixed_count &&
+      cec::launch_decode1_mixed(c->opts, c->k, c->m, L, p.list + p.mixed_off,
+                                (uint32_t)p.mixed_count, st))
+    return check_launch();
+  for (const auto& w : p.ct) {
+    int rc = do_decode(c, *w.first, L, p.list + w.second.first, (uint32_t)w.second.second, st);
+    if (rc) return rc;
+  }
+  const uint32_t* const* ptrs = static_cast<const uint32_t* const*>(p.ptrs);
+  for (const auto& l : p.rt) {
+    launch_chunk(c->opts, L, nullptr, ptrs + l.off, l.nin, l.nob, p.list + l.off,
+                 (uint32_t)l.count, st);
+    int rc = check_launch();
+    if (rc) return rc;
+  }
+  return CEC_OK;
+}
+
 }  // namespace
 
 namespace cec {
@@ -298,7 +577,13 @@ int set_error(int code, const std::string& msg) { return set_err(code, msg); }
 
 extern "C" {
 
-const char* cec_version(void) { return "cessec 0.1.0 gfx950"; }
+const char* cec_version(void) {
+#ifdef CEC_TUNING
+  return "cessec 0.2.0 gfx950 tuning";
+#else
+  return "cessec 0.2.0 gfx950";
+#endif
+}
 
 const char* cec_strerror(int code) {
   switch (code) {
@@ -311,6 +596,8 @@ const char* cec_strerror(int code) {
     case CEC_ENCCL: return "RCCL error";
     case CEC_ESHORTDATA: return "not enough data to fill the number of requested shards";
     case CEC_ENODEV: return "no GPU device";
+    case CEC_ESEGCOUNT: return "file exceeds SegmentCount segments";
+    case CEC_ECALLBACK: return "callback failed";
   }
   return "unknown error";
 }
@@ -355,7 +642,7 @@ int cec_create(int k, int m, int device, cec_codec** out) {
       out_idx[o] = (uint8_t)(k + o);
       for (int j = 0; j < k; ++j) par->v[o][j] = c->E->v[k + o][j];
     }
-    int rc = build_program(in_idx, k, out_idx, m, *par, c->encode);
+    int rc = build_program(c->pool, c->stream, in_idx, k, out_idx, m, *par, &c->encode);
     if (rc) return rc;
   }
   *out = c.release();
@@ -372,29 +659,42 @@ int cec_matrix(const cec_codec* c, uint8_t* out) {
 }
 
 int cec_set_option(cec_codec* c, int option, int value) {
+  if (!c) return set_err(CEC_EINVAL, "null codec");
   switch (option) {
     case CEC_OPT_FORCE_GENERIC:
-      if (!c) return set_err(CEC_EINVAL, "null codec");
       c->force_generic = value != 0;
       return CEC_OK;
     case CEC_OPT_CT_VARIANT:
-      if (value < -1 || value > 31) return set_err(CEC_EINVAL, "variant out of range");
-      cec::set_ct_variant(value);
+      if (value < -1 || value > cec::max_ct_variant())
+        return set_err(CEC_EINVAL, cec::max_ct_variant() == 0
+                                       ? "kernel variants need the tuning build (libcessec_tune)"
+                                       : "variant out of range");
+      c->opts.ct_variant = value == 0 && cec::max_ct_variant() == 0 ? -1 : value;
       return CEC_OK;
     case CEC_OPT_SHA_MODE:
       if (value < 0 || value > 2) return set_err(CEC_EINVAL, "sha mode out of range");
-      cec::set_sha_mode(value);
+      c->opts.sha_mode = value;
       return CEC_OK;
     case CEC_OPT_RT_MODE:
       if (value < 0 || value > 2) return set_err(CEC_EINVAL, "rt mode out of range");
-      cec::set_rt_mode(value);
+      c->opts.rt_mode = value;
       return CEC_OK;
-    case CEC_OPT_TICK_PREFETCH:
-      if (value < 0 || value > 3) return set_err(CEC_EINVAL, "tick variant must be 0..3");
-      cec::set_tick_prefetch(value);
+    case CEC_OPT_DECODE_CACHE:
+      if (value < 1) return set_err(CEC_EINVAL, "decode cache capacity must be >= 1");
+      c->cache_cap = (size_t)value;
+      evict_decode(c);
       return CEC_OK;
   }
   return set_err(CEC_EINVAL, "unknown option");
+}
+
+int cec_get_stat(const cec_codec* c, int stat, uint64_t* value) {
+  if (!c || !value) return set_err(CEC_EINVAL, "null");
+  switch (stat) {
+    case CEC_STAT_DECODE_CACHED: *value = c->decode_cache.size(); return CEC_OK;
+    case CEC_STAT_RETIRED_PENDING: *value = c->pool.pending(); return CEC_OK;
+  }
+  return set_err(CEC_EINVAL, "unknown stat");
 }
 
 int cec_encode_batch(cec_codec* c, const uint8_t* d_data, uint8_t* d_parity, size_t nseg,
@@ -417,116 +717,43 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
   hipStream_t st = pick_stream(c, hip_stream);
   const int n = c->k + c->m;
   Layout L = batch_layout(c, d_data, d_parity, shard_len);
+  int rc = CEC_OK;
   if (!per_segment) {
-    const Program* p = nullptr;
-    int rc = get_decode(c, present, data_only != 0, &p);
+    ProgPtr p;
+    rc = get_decode(c, present, data_only != 0, &p);
     if (rc) return rc;
-    return do_decode(c, *p, L, nullptr, (uint32_t)nseg, st);
-  }
-  // Per-segment patterns. Segments are grouped by pattern once and the grouping is cached for a
-  // repeated pattern array (degraded-read bench and repair loops pass the same map each call).
-  //  * every pattern has a compile-time single-erasure kernel (RS(2,1)): one launch per
-  //    pattern over its segment list;
-  //  * otherwise: one multi-pattern run-time launch per (chunk index, bucket), each segment's
-  //    workgroup row reading its own pattern's chunk, so a batch where every segment has a
-  //    different erasure map is still one full-grid launch.
-  std::string pkey(reinterpret_cast<const char*>(present), nseg * n);
-  for (auto& ch : pkey) ch = ch ? 1 : 0;
-  pkey.push_back(data_only ? 1 : 0);
-  pkey.push_back(c->force_generic ? 1 : 0);
-  if (c->ps_key != pkey || !c->ps_valid) {
-    c->ps_valid = false;
-    c->ps_ct.clear();
-    c->ps_rt.clear();
-    c->ps_mixed_count = 0;
-    std::unordered_map<std::string, std::vector<uint32_t>> groups;
-    for (size_t s = 0; s < nseg; ++s) groups[pkey.substr(s * n, n)].push_back((uint32_t)s);
-    bool all_ct = !c->force_generic;
-    std::vector<std::pair<const Program*, const std::vector<uint32_t>*>> progs;
-    for (auto& g : groups) {
-      const Program* p = nullptr;
-      int rc = get_decode(c, reinterpret_cast<const uint8_t*>(g.first.data()), data_only != 0, &p);
+    rc = do_decode(c, *p, L, nullptr, (uint32_t)nseg, st);
+  } else {
+    // Per-segment patterns. Segments are grouped by pattern once and the plan is cached for a
+    // repeated pattern array (degraded-read bench and repair loops pass the same map each
+    // call):
+    //  * every pattern has a compile-time single-erasure kernel (RS(2,1)): one mixed-pattern
+    //    launch (or one launch per pattern over its segment list);
+    //  * otherwise: one multi-pattern run-time launch per (chunk index, bucket), each segment's
+    //    workgroup row reading its own pattern's chunk, so a batch where every segment has a
+    //    different erasure map is still one full-grid launch.
+    std::string pkey(reinterpret_cast<const char*>(present), nseg * n);
+    for (auto& ch : pkey) ch = ch ? 1 : 0;
+    pkey.push_back(data_only ? 1 : 0);
+    pkey.push_back(c->force_generic ? 1 : 0);
+    if (!c->ps || c->ps->key != pkey) {
+      std::unique_ptr<PsPlan> plan;
+      rc = build_ps_plan(c, pkey, nseg, data_only != 0, &plan);
       if (rc) return rc;
-      if (!p->nout) continue;
-      progs.push_back({p, &g.second});
-      if (p->single < 0 || !cec::has_decode_ct(c->k, c->m, p->single)) all_ct = false;
-    }
-    std::vector<uint32_t> hl;
-    std::vector<const uint32_t*> hp;
-    if (all_ct) {
-      std::vector<uint32_t> tagged;
-      for (auto& g : groups) {
-        const Program* p = nullptr;
-        get_decode(c, reinterpret_cast<const uint8_t*>(g.first.data()), data_only != 0, &p);
-        if (!p->nout) continue;
-        c->ps_ct.push_back({g.first, {hl.size(), g.second.size()}});
-        hl.insert(hl.end(), g.second.begin(), g.second.end());
-        for (uint32_t sg : g.second) tagged.push_back(sg | ((uint32_t)p->single << 30));
-      }
-      if (c->k == 2 && c->m == 1 && c->ps_ct.size() > 1 && nseg < (1u << 30)) {
-        std::sort(tagged.begin(), tagged.end(),
-                  [](uint32_t a, uint32_t b) { return (a & 0x3FFFFFFFu) < (b & 0x3FFFFFFFu); });
-        c->ps_mixed_off = hl.size();
-        c->ps_mixed_count = tagged.size();
-        hl.insert(hl.end(), tagged.begin(), tagged.end());
-      }
+      c->drop_plan();  // the old plan's arrays are retired: launches already enqueued keep them
+      c->ps = std::move(plan);
     } else {
-      size_t maxchunks = 0;
-      for (auto& pr : progs) maxchunks = std::max(maxchunks, pr.first->chunks.size());
-      for (size_t ci = 0; ci < maxchunks; ++ci) {
-        std::unordered_map<int, std::vector<std::pair<uint32_t, const uint32_t*>>> byb;
-        int nin_max = 0;
-        for (auto& pr : progs)
-          if (ci < pr.first->chunks.size()) {
-            nin_max = std::max(nin_max, pr.first->chunks[ci].nin);
-            for (uint32_t sg : *pr.second)
-              byb[pr.first->chunks[ci].nob].push_back({sg, pr.first->chunks[ci].dev});
-          }
-        for (auto& b : byb) {
-          PsLaunch l;
-          l.nob = b.first;
-          l.nin = nin_max;
-          l.off = hl.size();
-          l.count = b.second.size();
-          for (auto& e : b.second) {
-            hl.push_back(e.first);
-            hp.push_back(e.second);
-          }
-          c->ps_rt.push_back(l);
-        }
+      for (const auto& key : c->ps->keys) {  // the reused plan's patterns stay recently used
+        auto it = c->decode_cache.find(key);
+        if (it != c->decode_cache.end()) c->lru.splice(c->lru.begin(), c->lru, it->second.lru);
       }
     }
-    int rc = ensure(reinterpret_cast<uint8_t**>(&c->ps_list), &c->ps_list_bytes,
-                    std::max<size_t>(hl.size(), 1) * sizeof(uint32_t));
-    if (rc) return rc;
-    rc = ensure(&c->ps_ptrs, &c->ps_ptrs_bytes, std::max<size_t>(hp.size(), 1) * sizeof(void*));
-    if (rc) return rc;
-    if (!hl.empty())
-      HIP_TRY(hipMemcpy(c->ps_list, hl.data(), hl.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    if (!hp.empty())
-      HIP_TRY(hipMemcpy(c->ps_ptrs, hp.data(), hp.size() * sizeof(void*), hipMemcpyHostToDevice));
-    c->ps_key = std::move(pkey);
-    c->ps_valid = true;
+    rc = launch_ps_plan(c, *c->ps, L, st);
   }
-  if (c->ps_mixed_count &&
-      cec::launch_decode1_mixed(c->k, c->m, L, c->ps_list + c->ps_mixed_off,
-                                (uint32_t)c->ps_mixed_count, st))
-    return check_launch();
-  for (const auto& w : c->ps_ct) {
-    const Program* p = nullptr;
-    int rc = get_decode(c, reinterpret_cast<const uint8_t*>(w.first.data()), data_only != 0, &p);
-    if (rc) return rc;
-    rc = do_decode(c, *p, L, c->ps_list + w.second.first, (uint32_t)w.second.second, st);
-    if (rc) return rc;
-  }
-  const uint32_t* const* ptrs = reinterpret_cast<const uint32_t* const*>(c->ps_ptrs);
-  for (const auto& l : c->ps_rt) {
-    launch_chunk(L, nullptr, ptrs + l.off, l.nin, l.nob, c->ps_list + l.off, (uint32_t)l.count,
-                 st);
-    int rc = check_launch();
-    if (rc) return rc;
-  }
-  return CEC_OK;
+  // completion point of these launches; only then may evicted programs be retired
+  int mrc = c->pool.mark(st);
+  evict_decode(c);
+  return rc ? rc : mrc;
 }
 
 int cec_sha256_batch(cec_codec* c, const uint8_t* d_data, const uint8_t* d_parity, size_t nseg,
@@ -539,8 +766,8 @@ int cec_sha256_batch(cec_codec* c, const uint8_t* d_data, const uint8_t* d_parit
     nsh = c->k;
     L.parity = nullptr;
   }
-  cec::launch_sha256_hex(nullptr, &L, nsh, (uint64_t)nseg * nsh, shard_len, d_hex,
-                         pick_stream(c, hip_stream));
+  cec::launch_sha256_hex(c->opts.sha_mode, nullptr, &L, nsh, (uint64_t)nseg * nsh, shard_len,
+                         d_hex, pick_stream(c, hip_stream));
   return check_launch();
 }
 
@@ -560,7 +787,7 @@ int cec_sha256_hex(const uint8_t* const* d_bufs, size_t n, size_t len, uint8_t* 
   int rc = CEC_OK;
   do {
     if ((e = hipMemcpyAsync(dptrs, d_bufs, n * sizeof(void*), hipMemcpyHostToDevice, st))) break;
-    cec::launch_sha256_hex(dptrs, nullptr, 1, n, len, dhex, st);
+    cec::launch_sha256_hex(0, dptrs, nullptr, 1, n, len, dhex, st);
     if ((e = hipGetLastError())) break;
     if ((e = hipMemcpyAsync(hex, dhex, n * 64, hipMemcpyDeviceToHost, st))) break;
     e = hipStreamSynchronize(st);
@@ -628,7 +855,7 @@ int cec_reconstruct(cec_codec* c, uint8_t* const* shards, const uint8_t* present
   if (shard_len == 0) return set_err(CEC_ESHARDLEN, "zero shard length");
   const int n = c->k + c->m;
   HIP_TRY(hipSetDevice(c->device));
-  const Program* p = nullptr;
+  ProgPtr p;
   int rc = get_decode(c, present, data_only != 0, &p);
   if (rc) return rc;
   if (p->nout == 0) return CEC_OK;
@@ -652,6 +879,7 @@ int cec_reconstruct(cec_codec* c, uint8_t* const* shards, const uint8_t* present
                            c->stream));
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
+  evict_decode(c);  // the launch above has completed
   return CEC_OK;
 }
 

@@ -33,6 +33,7 @@ struct cec_hashq {
   };
   std::deque<Add> adds;  // adds not yet complete, in slot order
   uint64_t next_ticket = 1;
+  int tick_mode = 0;  // CEC_HQOPT_TICK
 };
 
 namespace {
@@ -143,7 +144,7 @@ int cec_hashq_tick(cec_hashq* q, uint32_t max_blocks) {
   for (const auto& a : q->adds)
     if (a.done < a.blocks) live += a.n;
   HQ_TRY(hipSetDevice(q->device));
-  cec::launch_sha256_tick(q->tab, q->cap - 1, q->head, (uint32_t)(q->tail - q->head), max_blocks,
+  cec::launch_sha256_tick(q->tick_mode, q->tab, q->cap - 1, q->head, (uint32_t)(q->tail - q->head), max_blocks,
                           live, q->stream);
   int rc = launched();
   if (rc) return rc;
@@ -179,6 +180,16 @@ int cec_hashq_status(const cec_hashq* q, uint64_t ticket, int* done, size_t* liv
   if (live_chains) *live_chains = (size_t)live;
   if (blocks_left) *blocks_left = left;
   return CEC_OK;
+}
+
+int cec_hashq_set_option(cec_hashq* q, int option, int value) {
+  if (!q) return cec::set_error(CEC_EINVAL, "null");
+  if (option == CEC_HQOPT_TICK) {
+    if (value < 0 || value > 3) return cec::set_error(CEC_EINVAL, "tick kernel must be 0..3");
+    q->tick_mode = value;
+    return CEC_OK;
+  }
+  return cec::set_error(CEC_EINVAL, "unknown hash queue option");
 }
 
 }  // extern "C"

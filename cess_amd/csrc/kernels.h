@@ -40,18 +40,30 @@ inline size_t rt_chunk_bytes(int nin, int nob) {
 // True when every shard start and the shard length allow 16-byte vector access.
 bool layout_vec16_ok(const Layout& L);
 
+// Kernel selection of one codec (cec_set_option). Held per codec, passed to every launcher: no
+// process-wide state, so distinct codecs on distinct threads stay independent.
+struct KernelOpts {
+  int ct_variant = -1;  // compile-time kernel variant: -1 = default; others only in tuning
+                        // builds (libcessec_tune.so, -DCEC_TUNING)
+  int rt_mode = 0;      // run-time kernel: 0 Horner + index-mode XORs (4..32 inputs), 1 per-bit
+                        // masks, 2 Horner + v_mov table reads
+  int sha_mode = 0;     // one-shot SHA-256: 0 auto, 1 one wave, 2 two waves per 64 buffers
+};
+// Highest ct_variant this build instantiates (0 in the product library: default only).
+int max_ct_variant();
+
 // Compile-time-coefficient kernels. Return false if no specialised kernel exists for the
 // request (caller then uses the run-time kernel).
-bool launch_encode_ct(int k, int m, const Layout& L, const uint32_t* seg_list, uint32_t nseg,
-                      hipStream_t st);
+bool launch_encode_ct(const KernelOpts& o, int k, int m, const Layout& L,
+                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
 // Decode for a single erasure of RS(k, m) codes that have a specialised plan; `missing` is the
 // erased shard index and `data_only` drops a parity output.
-bool launch_decode_ct(int k, int m, int missing, const Layout& L, const uint32_t* seg_list,
-                      uint32_t nseg, hipStream_t st);
+bool launch_decode_ct(const KernelOpts& o, int k, int m, int missing, const Layout& L,
+                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
 // RS(2,1) single erasures, a different one per segment, in one launch: tagged[i] = segment |
 // (erased index << 30) for the nseg segments of the launch. False if not applicable.
-bool launch_decode1_mixed(int k, int m, const Layout& L, const uint32_t* tagged, uint32_t nseg,
-                          hipStream_t st);
+bool launch_decode1_mixed(const KernelOpts& o, int k, int m, const Layout& L,
+                          const uint32_t* tagged, uint32_t nseg, hipStream_t st);
 
 // Whether a compile-time single-erasure decode kernel exists for (k, m, missing).
 bool has_decode_ct(int k, int m, int missing);
@@ -65,14 +77,15 @@ void launch_matvec_rt(const Layout& L, const uint32_t* chunk, const uint32_t* co
                       int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
 // Same product from the chunks' Horner sections (every chunk of the launch has nin <= nin_max
 // <= kRthMaxIn). Returns false (nothing launched) if the form is disabled by the variant knob.
-bool launch_matvec_rth(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
-                       int nin_max, const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
+bool launch_matvec_rth(const KernelOpts& o, const Layout& L, const uint32_t* chunk,
+                       const uint32_t* const* per_seg, int nin_max, const uint32_t* seg_list,
+                       uint32_t nseg, hipStream_t st);
 
 // SHA-256 of `n` equal-length buffers, written as 64 lowercase hex characters each into
 // `hex_out` (device, n * 64 bytes). If `ptrs` is null, buffer i is shard (i % nshards) of
 // segment (i / nshards) in layout L.
-void launch_sha256_hex(const uint8_t* const* ptrs, const Layout* L, int nshards, uint64_t n,
-                       uint64_t len, uint8_t* hex_out, hipStream_t st);
+void launch_sha256_hex(int sha_mode, const uint8_t* const* ptrs, const Layout* L, int nshards,
+                       uint64_t n, uint64_t len, uint8_t* hex_out, hipStream_t st);
 
 // One chain of the streaming SHA-256 queue (hashq.cpp), 128 bytes in HBM. `blk` counts the
 // 64-byte blocks already compressed into `h`, padding blocks included; the chain is complete
@@ -101,9 +114,10 @@ void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
                       const uint8_t* base, uint32_t per, uint64_t outer, uint64_t inner,
                       uint64_t len, uint8_t* hex, uint64_t hex_outer, uint64_t pre_blk,
                       uint8_t* pre_hex, uint64_t pre_hex_outer, hipStream_t st);
-// Advance the n chains in slots head.. by at most max_blocks blocks each; `live` (chains not
-// yet complete among them) picks the kernel form.
-void launch_sha256_tick(ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,
+// Advance the n chains in slots head.. by at most max_blocks blocks each; tick_mode 0 lets `live`
+// (chains not yet complete among them) pick the kernel form, 1 or 2 = two waves with that many
+// blocks prefetched, 3 = one wave per 64 chains.
+void launch_sha256_tick(int tick_mode, ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,
                         uint32_t max_blocks, uint64_t live, hipStream_t st);
 
 // Synthetic segment bytes: 64-bit word w of segment s = splitmix64(seed ^ (s << 32) ^ w),

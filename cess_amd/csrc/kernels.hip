@@ -902,7 +902,11 @@ __device__ __forceinline__ void rthx_table7(uint32_t x0, uint32_t x1, uint32_t x
 // M0 (s_set_gpr_idx_on / _idx) needs one wait state before the indexed VALU: without the s_nop
 // the XOR read a stale index now and then (10 of 10 RS(32,32) 32-erasure rebuilds had 10^5 wrong
 // bytes, a different set each run; with it 0 of 10, tools/stress_rthx.py). One after _off too,
-// before any VALU that names a VGPR as SRC0.
+// // before any VALU that names a VGPR as SRC0. Every block clobbers M0 (declared: clang warns that
+// M0 is a reserved register it does not preserve; no other instruction of k_rthx uses M0, which
+// tests/test_host.py checks on the shipped code object along with the wait states).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 #define RTHX_ON "s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\ts_nop 0\n\tv_xor_b32 %0, v24, %0\n\t"
 #define RTHX_IDX(n, reg) "s_set_gpr_idx_idx %" #n "\n\ts_nop 0\n\tv_xor_b32 %0, " reg ", %0\n\t"
 #define RTHX_OFF "s_set_gpr_idx_off\n\ts_nop 0"
@@ -910,31 +914,31 @@ template <int NG>
 __device__ __forceinline__ uint32_t rthx_xor(uint32_t y, const uint32_t (&q)[NG]);
 template <>
 __device__ __forceinline__ uint32_t rthx_xor<1>(uint32_t y, const uint32_t (&q)[1]) {
-  asm volatile(RTHX_ON RTHX_OFF : "+v"(y) : "s"(q[0]));
+  asm volatile(RTHX_ON RTHX_OFF : "+v"(y) : "s"(q[0]) : "m0");
   return y;
 }
 template <>
 __device__ __forceinline__ uint32_t rthx_xor<2>(uint32_t y, const uint32_t (&q)[2]) {
-  asm volatile(RTHX_ON RTHX_IDX(2, "v40") RTHX_OFF : "+v"(y) : "s"(q[0]), "s"(q[1]));
+  asm volatile(RTHX_ON RTHX_IDX(2, "v40") RTHX_OFF : "+v"(y) : "s"(q[0]), "s"(q[1]) : "m0");
   return y;
 }
 template <>
 __device__ __forceinline__ uint32_t rthx_xor<3>(uint32_t y, const uint32_t (&q)[3]) {
   asm volatile(RTHX_ON RTHX_IDX(2, "v40") RTHX_IDX(3, "v56") RTHX_OFF
-               : "+v"(y) : "s"(q[0]), "s"(q[1]), "s"(q[2]));
+               : "+v"(y) : "s"(q[0]), "s"(q[1]), "s"(q[2]) : "m0");
   return y;
 }
 template <>
 __device__ __forceinline__ uint32_t rthx_xor<4>(uint32_t y, const uint32_t (&q)[4]) {
   asm volatile(RTHX_ON RTHX_IDX(2, "v40") RTHX_IDX(3, "v56") RTHX_IDX(4, "v72") RTHX_OFF
-               : "+v"(y) : "s"(q[0]), "s"(q[1]), "s"(q[2]), "s"(q[3]));
+               : "+v"(y) : "s"(q[0]), "s"(q[1]), "s"(q[2]), "s"(q[3]) : "m0");
   return y;
 }
 template <>
 __device__ __forceinline__ uint32_t rthx_xor<6>(uint32_t y, const uint32_t (&q)[6]) {
   asm volatile(RTHX_ON RTHX_IDX(2, "v40") RTHX_IDX(3, "v56") RTHX_IDX(4, "v72")
                    RTHX_IDX(5, "v88") RTHX_IDX(6, "v104") RTHX_OFF
-               : "+v"(y) : "s"(q[0]), "s"(q[1]), "s"(q[2]), "s"(q[3]), "s"(q[4]), "s"(q[5]));
+               : "+v"(y) : "s"(q[0]), "s"(q[1]), "s"(q[2]), "s"(q[3]), "s"(q[4]), "s"(q[5]) : "m0");
   return y;
 }
 template <>
@@ -944,9 +948,10 @@ __device__ __forceinline__ uint32_t rthx_xor<8>(uint32_t y, const uint32_t (&q)[
                        RTHX_IDX(8, "v136") RTHX_OFF
                : "+v"(y)
                : "s"(q[0]), "s"(q[1]), "s"(q[2]), "s"(q[3]), "s"(q[4]), "s"(q[5]), "s"(q[6]),
-                 "s"(q[7]));
+                 "s"(q[7]) : "m0");
   return y;
 }
+#pragma clang diagnostic pop
 #undef RTHX_ON
 #undef RTHX_IDX
 #undef RTHX_OFF
@@ -1103,30 +1108,36 @@ void run_ct(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_
   }
 }
 
-int g_ct_variant = -1;  // -1: default; set by cec_set_option(CEC_OPT_CT_VARIANT)
-
+// Kernel variants for tuning sweeps (bench.py --sweep) exist only in the tuning build
+// (libcessec_tune.so, -DCEC_TUNING); the product library instantiates the default of each.
 template <class P>
-void run_ct_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
-  switch (g_ct_variant) {
-    case 0: run_ct<P, 1, false>(L, seg_list, nseg, st); break;
-    case 1: run_ct<P, 2, false>(L, seg_list, nseg, st); break;
-    case 2: run_ct<P, 4, false>(L, seg_list, nseg, st); break;
-    case 3: run_ct<P, 1, true>(L, seg_list, nseg, st); break;
-    case 4: run_ct<P, 2, true>(L, seg_list, nseg, st); break;
-    case 5: run_ct<P, 4, true>(L, seg_list, nseg, st); break;
-    case 6: run_ct<P, 1, true, u32x4, 1, false, 512>(L, seg_list, nseg, st); break;
-    case 7: run_ct<P, 1, true, u32x4, 1, false, 128>(L, seg_list, nseg, st); break;
-    case 8: run_ct<P, 1, true, u32x4, 1, false, 1024>(L, seg_list, nseg, st); break;
+void run_ct_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_list,
+                    uint32_t nseg, hipStream_t st) {
+#ifdef CEC_TUNING
+  switch (o.ct_variant) {
+    case 0: run_ct<P, 1, false>(L, seg_list, nseg, st); return;
+    case 1: run_ct<P, 2, false>(L, seg_list, nseg, st); return;
+    case 2: run_ct<P, 4, false>(L, seg_list, nseg, st); return;
+    case 3: run_ct<P, 1, true>(L, seg_list, nseg, st); return;
+    case 4: run_ct<P, 2, true>(L, seg_list, nseg, st); return;
+    case 5: run_ct<P, 4, true>(L, seg_list, nseg, st); return;
+    case 6: run_ct<P, 1, true, u32x4, 1, false, 512>(L, seg_list, nseg, st); return;
+    case 7: run_ct<P, 1, true, u32x4, 1, false, 128>(L, seg_list, nseg, st); return;
+    case 8: run_ct<P, 1, true, u32x4, 1, false, 1024>(L, seg_list, nseg, st); return;
     case 9: case 10: case 11: {
-      if (!layout_vec16_ok(L) || (L.len & 15)) { run_ct<P, 1, true>(L, seg_list, nseg, st); break; }
+      if (!layout_vec16_ok(L) || (L.len & 15)) break;
       const uint64_t tiles = (L.len / 16 + 255) / 256;
-      const unsigned grid = g_ct_variant == 9 ? 2048 : g_ct_variant == 10 ? 4096 : 8192;
+      const unsigned grid = o.ct_variant == 9 ? 2048 : o.ct_variant == 10 ? 4096 : 8192;
       hipLaunchKernelGGL((k_ct_persist<P, true, 256>), dim3(grid), dim3(256), 0, st, L, seg_list,
                          nseg, tiles);
-      break;
+      return;
     }
-    default: run_ct<P, 1, true>(L, seg_list, nseg, st); break;  // r01 sweep winner
+    default: break;
   }
+#else
+  (void)o;
+#endif
+  run_ct<P, 1, true>(L, seg_list, nseg, st);  // r01 sweep winner: one 16-B column, nontemporal
 }
 
 // Horner-over-groups kernel; needs 4-byte-aligned shards and 32-bit lane offsets (else the
@@ -1147,51 +1158,61 @@ void run_hg(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_
   });
 }
 
-// Wide codes: nibble-window / streaming forms (per-lane width, prefetch depth) and the Horner
-// form over input groups.
+// Wide codes: Horner over input groups by default; the tuning build adds the nibble-window /
+// streaming forms (per-lane width, prefetch depth) and the k_hg flag variants.
 template <class P>
-void run_wide_variant(const Layout& L, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
-  switch (g_ct_variant) {
-    case 0: run_ct<P, 1, false, u32x4, 1>(L, seg_list, nseg, st); break;
-    case 1: run_ct<P, 1, false, u32x4, 2>(L, seg_list, nseg, st); break;
-    case 2: run_ct<P, 1, false, u32x2, 2>(L, seg_list, nseg, st); break;
-    case 3: run_ct<P, 1, false, u32x2, 4>(L, seg_list, nseg, st); break;
-    case 4: run_ct<P, 1, true, u32x2, 4>(L, seg_list, nseg, st); break;
-    case 5: run_ct<P, 1, false, u32x2, 8>(L, seg_list, nseg, st); break;
-    case 6: run_ct<P, 1, false, u32x2, 2, true>(L, seg_list, nseg, st); break;
-    case 7: run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st); break;
-    case 8: run_ct<P, 1, false, u32x2, 4, true>(L, seg_list, nseg, st); break;
-    case 9: run_ct<P, 1, false, u32x4, 2, true>(L, seg_list, nseg, st); break;
-    case 11: run_hg<P, 3, 0>(L, seg_list, nseg, st); break;
-    case 12: run_hg<P, 4, 1>(L, seg_list, nseg, st); break;
-    case 13: run_hg<P, 4, 2>(L, seg_list, nseg, st); break;
-    case 14: run_hg<P, 4, 4>(L, seg_list, nseg, st); break;
-    case 15: run_hg<P, 4, 0, 128>(L, seg_list, nseg, st); break;
-    case 16: run_hg<P, 4, 0, 512>(L, seg_list, nseg, st); break;
-    case 17: run_hg<P, 4, 8>(L, seg_list, nseg, st); break;
-    case 18: run_hg<P, 3, 8>(L, seg_list, nseg, st); break;
-    case 19: run_hg<P, 4, 16>(L, seg_list, nseg, st); break;
-    case 20: run_hg<P, 4, 17>(L, seg_list, nseg, st); break;
-    case 10: run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st); break;  // r01 default
-    default: run_hg<P, 4, 0>(L, seg_list, nseg, st); break;  // r01 sweep: 3.11 -> 5.26 TB/s
+void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_list,
+                      uint32_t nseg, hipStream_t st) {
+#ifdef CEC_TUNING
+  switch (o.ct_variant) {
+    case 0: run_ct<P, 1, false, u32x4, 1>(L, seg_list, nseg, st); return;
+    case 1: run_ct<P, 1, false, u32x4, 2>(L, seg_list, nseg, st); return;
+    case 2: run_ct<P, 1, false, u32x2, 2>(L, seg_list, nseg, st); return;
+    case 3: run_ct<P, 1, false, u32x2, 4>(L, seg_list, nseg, st); return;
+    case 4: run_ct<P, 1, true, u32x2, 4>(L, seg_list, nseg, st); return;
+    case 5: run_ct<P, 1, false, u32x2, 8>(L, seg_list, nseg, st); return;
+    case 6: run_ct<P, 1, false, u32x2, 2, true>(L, seg_list, nseg, st); return;
+    case 7: run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st); return;
+    case 8: run_ct<P, 1, false, u32x2, 4, true>(L, seg_list, nseg, st); return;
+    case 9: run_ct<P, 1, false, u32x4, 2, true>(L, seg_list, nseg, st); return;
+    case 10: run_ct<P, 1, false, uint32_t, 4, true>(L, seg_list, nseg, st); return;
+    case 11: run_hg<P, 3, 0>(L, seg_list, nseg, st); return;
+    case 12: run_hg<P, 4, 1>(L, seg_list, nseg, st); return;
+    case 13: run_hg<P, 4, 2>(L, seg_list, nseg, st); return;
+    case 14: run_hg<P, 4, 4>(L, seg_list, nseg, st); return;
+    case 15: run_hg<P, 4, 0, 128>(L, seg_list, nseg, st); return;
+    case 16: run_hg<P, 4, 0, 512>(L, seg_list, nseg, st); return;
+    case 17: run_hg<P, 4, 8>(L, seg_list, nseg, st); return;
+    case 18: run_hg<P, 3, 8>(L, seg_list, nseg, st); return;
+    case 19: run_hg<P, 4, 16>(L, seg_list, nseg, st); return;
+    case 20: run_hg<P, 4, 17>(L, seg_list, nseg, st); return;
+    default: break;
   }
+#else
+  (void)o;
+#endif
+  run_hg<P, 4, 0>(L, seg_list, nseg, st);  // r01 sweep: 3.11 -> 5.26 TB/s
 }
 
 }  // namespace
 
-void set_ct_variant(int v) { g_ct_variant = v; }
+#ifdef CEC_TUNING
+int max_ct_variant() { return 20; }
+#else
+int max_ct_variant() { return 0; }
+#endif
 
-bool launch_encode_ct(int k, int m, const Layout& L, const uint32_t* seg_list, uint32_t nseg,
-                      hipStream_t st) {
-  if (k == 2 && m == 1) { run_ct_variant<EncCT<2, 1>>(L, seg_list, nseg, st); return true; }
-  if (k == 32 && m == 32) { run_wide_variant<EncCT<32, 32>>(L, seg_list, nseg, st); return true; }
+bool launch_encode_ct(const KernelOpts& o, int k, int m, const Layout& L,
+                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  if (k == 2 && m == 1) { run_ct_variant<EncCT<2, 1>>(o, L, seg_list, nseg, st); return true; }
+  if (k == 32 && m == 32) { run_wide_variant<EncCT<32, 32>>(o, L, seg_list, nseg, st); return true; }
   return false;
 }
 
-bool launch_decode1_mixed(int k, int m, const Layout& L, const uint32_t* tagged, uint32_t nseg,
-                          hipStream_t st) {
-  // the r01 default variant only (a variant set for a sweep keeps the per-pattern launches)
-  if (k != 2 || m != 1 || g_ct_variant != -1 || !layout_vec16_ok(L)) return false;
+bool launch_decode1_mixed(const KernelOpts& o, int k, int m, const Layout& L,
+                          const uint32_t* tagged, uint32_t nseg, hipStream_t st) {
+  // the default variant only (a variant set for a sweep keeps the per-pattern launches)
+  if (k != 2 || m != 1 || o.ct_variant != -1 || !layout_vec16_ok(L)) return false;
   uint64_t gx = (L.len / 16 + 255) / 256;
   if (gx == 0) gx = 1;
   for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {
@@ -1201,13 +1222,13 @@ bool launch_decode1_mixed(int k, int m, const Layout& L, const uint32_t* tagged,
   return true;
 }
 
-bool launch_decode_ct(int k, int m, int missing, const Layout& L, const uint32_t* seg_list,
-                      uint32_t nseg, hipStream_t st) {
+bool launch_decode_ct(const KernelOpts& o, int k, int m, int missing, const Layout& L,
+                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
   if (k == 2 && m == 1) {
     switch (missing) {
-      case 0: run_ct_variant<Dec1CT<2, 1, 0>>(L, seg_list, nseg, st); return true;
-      case 1: run_ct_variant<Dec1CT<2, 1, 1>>(L, seg_list, nseg, st); return true;
-      case 2: run_ct_variant<EncCT<2, 1>>(L, seg_list, nseg, st); return true;
+      case 0: run_ct_variant<Dec1CT<2, 1, 0>>(o, L, seg_list, nseg, st); return true;
+      case 1: run_ct_variant<Dec1CT<2, 1, 1>>(o, L, seg_list, nseg, st); return true;
+      case 2: run_ct_variant<EncCT<2, 1>>(o, L, seg_list, nseg, st); return true;
     }
   }
   return false;
@@ -1257,11 +1278,10 @@ void launch_matvec_rt(const Layout& L, const uint32_t* chunk, const uint32_t* co
 }
 
 namespace {
-int g_rt_mode = 0;  // 0: Horner over input groups with index-mode XORs (k_rthx) where possible,
-                    // 1: always k_rt (per-bit masks), 2: Horner with v_mov table reads (k_rth)
-
+// rt_mode 0: Horner over input groups with index-mode XORs (k_rthx) where possible,
+// 1: always k_rt (per-bit masks), 2: Horner with v_mov table reads (k_rth)
 template <int NG>
-void run_rth(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
+void run_rth(int rt_mode, const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
              const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
   const uintptr_t bits = (uintptr_t)L.data | (uintptr_t)L.parity | L.shard_stride |
                          L.data_seg_stride | L.par_seg_stride;
@@ -1269,7 +1289,7 @@ void run_rth(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_
   uint64_t gx = vec_ok ? (L.len / 4 + 255) / 256 : (L.len + 255) / 256;
   if (gx == 0) gx = 1;
   for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) {
-    if (g_rt_mode == 0)
+    if (rt_mode == 0)
       hipLaunchKernelGGL((k_rthx<NG>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, chunk,
                          per_seg, seg_list, s0, vec_ok);
     else
@@ -1279,22 +1299,21 @@ void run_rth(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_
 }
 }  // namespace
 
-void set_rt_mode(int v) { g_rt_mode = v; }
-
-bool launch_matvec_rth(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
-                       int nin_max, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+bool launch_matvec_rth(const KernelOpts& o, const Layout& L, const uint32_t* chunk,
+                       const uint32_t* const* per_seg, int nin_max, const uint32_t* seg_list,
+                       uint32_t nseg, hipStream_t st) {
   // measured (profiles/r01/rt_modes.txt): faster than k_rt from 4 inputs up (k_rthx / k_rth /
   // k_rt: RS(10,4) encode 3.2 / 3.0 / 2.7 TB/s, RS(32,32) one-fragment repair 4.0 / 4.0 / 3.1,
   // 32-erasure rebuild 1.76 / 1.1 / 0.96); for 2-3 inputs k_rt's 16-byte columns win (RS(2,1)
   // run-time encode 6.0 vs 2.9 TB/s)
-  if (g_rt_mode == 1 || nin_max > kRthMaxIn || nin_max < 4) return false;
+  if (o.rt_mode == 1 || nin_max > kRthMaxIn || nin_max < 4) return false;
   const int ng = (nin_max + 3) / 4;
-  if (ng <= 1) run_rth<1>(L, chunk, per_seg, seg_list, nseg, st);
-  else if (ng == 2) run_rth<2>(L, chunk, per_seg, seg_list, nseg, st);
-  else if (ng == 3) run_rth<3>(L, chunk, per_seg, seg_list, nseg, st);
-  else if (ng == 4) run_rth<4>(L, chunk, per_seg, seg_list, nseg, st);
-  else if (ng <= 6) run_rth<6>(L, chunk, per_seg, seg_list, nseg, st);
-  else run_rth<8>(L, chunk, per_seg, seg_list, nseg, st);
+  if (ng <= 1) run_rth<1>(o.rt_mode, L, chunk, per_seg, seg_list, nseg, st);
+  else if (ng == 2) run_rth<2>(o.rt_mode, L, chunk, per_seg, seg_list, nseg, st);
+  else if (ng == 3) run_rth<3>(o.rt_mode, L, chunk, per_seg, seg_list, nseg, st);
+  else if (ng == 4) run_rth<4>(o.rt_mode, L, chunk, per_seg, seg_list, nseg, st);
+  else if (ng <= 6) run_rth<6>(o.rt_mode, L, chunk, per_seg, seg_list, nseg, st);
+  else run_rth<8>(o.rt_mode, L, chunk, per_seg, seg_list, nseg, st);
   return true;
 }
 

@@ -622,26 +622,14 @@ __global__ __launch_bounds__(256) void k_hashq_add(ShaChain* __restrict__ tab, u
   tab[(uint32_t)(slot0 + i) & mask] = c;
 }
 
-namespace {
-int g_sha_mode = 0;  // 0 auto, 1 one wave, 2 two waves per 64 buffers
-}
-void set_sha_mode(int v) { g_sha_mode = v; }
-
-namespace {
-// hash-queue tick: 0 auto, 1 or 2 = two-wave kernel loading that many blocks ahead, 3 = one-wave
-int g_tick_pf = 0;
-}
-void set_tick_prefetch(int v) { g_tick_pf = v >= 0 && v <= 3 ? v : 0; }
-
-
-void launch_sha256_hex(const uint8_t* const* ptrs, const Layout* L, int nshards, uint64_t n,
-                       uint64_t len, uint8_t* hex_out, hipStream_t st) {
+void launch_sha256_hex(int sha_mode, const uint8_t* const* ptrs, const Layout* L, int nshards,
+                       uint64_t n, uint64_t len, uint8_t* hex_out, hipStream_t st) {
   if (n == 0) return;
   Layout dummy{};
   const unsigned g = (unsigned)((n + 63) / 64);
   // Two waves per group while the groups leave SIMDs idle (latency regime: one serial chain
   // per buffer); one wave per group once 2 * groups would exceed the chip's 1024 SIMDs.
-  const bool two = g_sha_mode == 2 || (g_sha_mode == 0 && g <= 512);
+  const bool two = sha_mode == 2 || (sha_mode != 1 && g <= 512);
   if (two)
     hipLaunchKernelGGL(k_sha256_2w, dim3(g), dim3(128), 0, st, ptrs, L ? *L : dummy, nshards, n,
                        len, hex_out);
@@ -660,13 +648,13 @@ void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
                      pre_hex_outer);
 }
 
-void launch_sha256_tick(ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,
+void launch_sha256_tick(int tick_mode, ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,
                         uint32_t max_blocks, uint64_t live, hipStream_t st) {
   if (n == 0 || max_blocks == 0) return;
   // auto (0): the two-wave kernel while live chains are few (one wave's issue rate bounds a
   // chain), the one-wave kernel once 2^17 live chains give every SIMD several waves (measured
   // crossover, profiles/r01/sha_scale_*.jsonl)
-  const int v = g_tick_pf ? g_tick_pf : (live >= (1u << 17) ? 3 : 1);
+  const int v = tick_mode >= 1 && tick_mode <= 3 ? tick_mode : (live >= (1u << 17) ? 3 : 1);
   if (v == 3)
     hipLaunchKernelGGL(k_sha256_tick1, dim3((n + 63) / 64), dim3(64), 0, st, tab, mask, head, n,
                        max_blocks);

@@ -118,6 +118,11 @@ class HashQueue:
                      n_sh, k * 64)
         return t
 
+    def set_option(self, option: int, value: int) -> None:
+        """cec_hashq_set_option (CEC_HQOPT_TICK: 0 auto, 1/2 two-wave prefetch depth, 3 one
+        wave)."""
+        check(_lib.load().cec_hashq_set_option(self._h, option, value), "HashQueue.set_option")
+
     def tick(self, max_blocks: int = 0) -> None:
         """Advance every live chain by at most max_blocks blocks (0: to completion)."""
         check(_lib.load().cec_hashq_tick(self._h, max_blocks), "HashQueue.tick")

@@ -129,9 +129,11 @@ def _stream_handle(stream) -> Optional[int]:
 
 
 class Encoder:
-    """One codec bound to one GPU (klauspost Encoder)."""
+    """One codec bound to one GPU (klauspost Encoder). `tuning=True` binds the tuning build of
+    the library (kernel variants for sweeps; never the product path)."""
 
-    def __init__(self, data_shards: int, parity_shards: int, device: int = 0):
+    def __init__(self, data_shards: int, parity_shards: int, device: int = 0,
+                 tuning: bool = False):
         if data_shards <= 0 or parity_shards < 0:
             raise ErrInvShardNum(ErrInvShardNum.__doc__)
         if data_shards + parity_shards > 256:
@@ -141,14 +143,15 @@ class Encoder:
         self.Shards = data_shards + parity_shards
         self.device = device
         self._h = c_void_p()
+        self._lib = None
         if parity_shards > 0:
-            lib = _lib.load()
-            check(lib.cec_create(data_shards, parity_shards, device, byref(self._h)), "New")
+            self._lib = _lib.load(tuning)
+            check(self._lib.cec_create(data_shards, parity_shards, device, byref(self._h)), "New")
 
     # -- lifetime ----------------------------------------------------------------------------
     def close(self) -> None:
         if self._h:
-            _lib.load().cec_destroy(self._h)
+            self._lib.cec_destroy(self._h)
             self._h = c_void_p()
 
     def __del__(self):
@@ -169,11 +172,17 @@ class Encoder:
         out = np.zeros((self.Shards, self.DataShards), dtype=np.uint8)
         if self.ParityShards == 0:
             return np.eye(self.DataShards, dtype=np.uint8)
-        check(_lib.load().cec_matrix(self._h, out.ctypes.data_as(POINTER(c_uint8))), "matrix")
+        check(self._lib.cec_matrix(self._h, out.ctypes.data_as(POINTER(c_uint8))), "matrix")
         return out
 
     def set_option(self, option: int, value: int) -> None:
-        check(_lib.load().cec_set_option(self._h, option, value), "set_option")
+        """cec_set_option on this codec only (CEC_OPT_*)."""
+        check(self._lib.cec_set_option(self._h, option, value), "set_option")
+
+    def stat(self, which: int) -> int:
+        v = ctypes.c_uint64()
+        check(self._lib.cec_get_stat(self._h, which, byref(v)), "stat")
+        return v.value
 
     def _check_shards(self, shards, nil_ok: bool) -> int:
         size = next((len(s) for s in shards if _present(s)), 0)
@@ -194,7 +203,7 @@ class Encoder:
         if self.ParityShards == 0:
             return
         arrs = [_as_u8(s) for s in shards]
-        check(_lib.load().cec_encode(self._h, _ptr_array(arrs), size), "Encode")
+        check(self._lib.cec_encode(self._h, _ptr_array(arrs), size), "Encode")
 
     def Verify(self, shards: Sequence) -> bool:
         if len(shards) != self.Shards:
@@ -204,7 +213,7 @@ class Encoder:
             return True
         arrs = [_as_u8(s) for s in shards]
         ok = c_int(0)
-        check(_lib.load().cec_verify(self._h, _ptr_array(arrs), size, byref(ok)), "Verify")
+        check(self._lib.cec_verify(self._h, _ptr_array(arrs), size, byref(ok)), "Verify")
         return bool(ok.value)
 
     def _reconstruct(self, shards: List, data_only: bool) -> None:
@@ -221,7 +230,7 @@ class Encoder:
                 shards[i] = np.zeros(size, dtype=np.uint8)
         arrs = [_as_u8(s) if _present(s) else np.zeros(size, dtype=np.uint8) for s in shards]
         flags = (c_uint8 * self.Shards)(*[1 if p else 0 for p in present])
-        check(_lib.load().cec_reconstruct(self._h, _ptr_array(arrs), flags, size,
+        check(self._lib.cec_reconstruct(self._h, _ptr_array(arrs), flags, size,
                                           1 if data_only else 0), "Reconstruct")
         for i in range(self.Shards):
             if not present[i] and (i < self.DataShards or not data_only):
@@ -266,7 +275,7 @@ class Encoder:
     # -- HBM-resident batches ----------------------------------------------------------------
     def EncodeBatch(self, d_data, d_parity, nseg: int, shard_len: int, stream=None) -> None:
         """Enqueue encode of nseg segments ([nseg][k][len] -> [nseg][m][len]) on `stream`."""
-        check(_lib.load().cec_encode_batch(self._h, _dev_ptr(d_data), _dev_ptr(d_parity), nseg,
+        check(self._lib.cec_encode_batch(self._h, _dev_ptr(d_data), _dev_ptr(d_parity), nseg,
                                            shard_len, _stream_handle(stream)), "EncodeBatch")
 
     def ReconstructBatch(self, d_data, d_parity, nseg: int, shard_len: int, present,
@@ -278,7 +287,7 @@ class Encoder:
             raise ValueError("present must be (nseg, k+m)")
         if not per_segment and p.shape != (self.Shards,):
             raise ValueError("present must have k+m flags")
-        check(_lib.load().cec_reconstruct_batch(
+        check(self._lib.cec_reconstruct_batch(
             self._h, _dev_ptr(d_data), _dev_ptr(d_parity), nseg, shard_len,
             p.ctypes.data_as(POINTER(c_uint8)), per_segment, 1 if data_only else 0,
             _stream_handle(stream)), "ReconstructBatch")
@@ -286,14 +295,14 @@ class Encoder:
     def Sha256Batch(self, d_data, d_parity, nseg: int, shard_len: int, d_hex,
                     stream=None) -> None:
         """Hex SHA-256 of every shard into d_hex ([nseg][k+m][64] bytes, device)."""
-        check(_lib.load().cec_sha256_batch(
+        check(self._lib.cec_sha256_batch(
             self._h, _dev_ptr(d_data), 0 if d_parity is None else _dev_ptr(d_parity), nseg,
             shard_len, _dev_ptr(d_hex), _stream_handle(stream)), "Sha256Batch")
 
 
-def New(data_shards: int, parity_shards: int, device: int = 0) -> Encoder:
+def New(data_shards: int, parity_shards: int, device: int = 0, tuning: bool = False) -> Encoder:
     """klauspost reedsolomon.New(dataShards, parityShards) on a GPU."""
-    return Encoder(data_shards, parity_shards, device)
+    return Encoder(data_shards, parity_shards, device, tuning)
 
 
 def fill_synthetic(d_out, seg_bytes: int, nseg: int, seg0: int, seed: int, stream=None) -> None:

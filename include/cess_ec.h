@@ -43,6 +43,8 @@ extern "C" {
 #define CEC_ENCCL (-6)      /* RCCL error (multi-GPU paths) */
 #define CEC_ESHORTDATA (-7) /* split of an empty segment (klauspost ErrShortData) */
 #define CEC_ENODEV (-8)     /* no usable GPU */
+#define CEC_ESEGCOUNT (-9)  /* more segments than the chain's SegmentCount bound (1000) */
+#define CEC_ECALLBACK (-10) /* a pipeline callback returned an error */
 
 typedef struct cec_codec cec_codec;
 
@@ -132,6 +134,10 @@ int cec_hashq_finish(cec_hashq* q);
  * pointer may be NULL. */
 int cec_hashq_status(const cec_hashq* q, uint64_t ticket, int* done, size_t* live_chains,
                      uint64_t* blocks_left);
+/* Queue options. CEC_HQOPT_TICK: tick kernel, 0 = auto by live chains, 1 or 2 = two waves
+ * (schedule producer loading 1 or 2 blocks ahead + rounds consumer), 3 = one wave per 64 chains. */
+#define CEC_HQOPT_TICK 1
+int cec_hashq_set_option(cec_hashq* q, int option, int value);
 
 /* klauspost Split for one segment (host memory): shard i = seg[i*shard_len, (i+1)*shard_len),
  * zero-padded past seg_len. Requires k*shard_len >= seg_len > 0. */
@@ -143,19 +149,23 @@ int cec_split_segment(const uint8_t* seg, size_t seg_len, int k, uint8_t* const*
 int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t seg0,
                        uint64_t seed, void* hip_stream);
 
-/* Options (tuning / testing). CT_VARIANT, SHA_MODE, RT_MODE and TICK_PREFETCH are process-wide
- * kernel choices (the codec argument may be any live handle); FORCE_GENERIC is per codec. */
+/* Options, per codec (distinct codecs never affect each other). */
 #define CEC_OPT_FORCE_GENERIC 1 /* 1: always use the run-time-coefficient kernel */
-#define CEC_OPT_CT_VARIANT 2    /* compile-time kernel unroll/cache variant, -1 = default */
-#define CEC_OPT_SHA_MODE 3      /* SHA-256 kernel: 0 = auto, 1 = one wave per 64 buffers,
-                                   2 = two waves (schedule producer + rounds consumer) */
+#define CEC_OPT_CT_VARIANT 2    /* compile-time kernel variant for tuning sweeps: -1 = default;
+                                   other values need the tuning build (libcessec_tune.so) */
+#define CEC_OPT_SHA_MODE 3      /* cec_sha256_batch kernel: 0 = auto, 1 = one wave per 64
+                                   buffers, 2 = two waves (schedule producer + rounds consumer) */
 #define CEC_OPT_RT_MODE 4       /* run-time-coefficient kernel: 0 = Horner over input groups
                                    with index-mode table XORs when 4 <= inputs <= 32, 1 = always
                                    the per-bit mask kernel, 2 = Horner with v_mov table reads */
-#define CEC_OPT_TICK_PREFETCH 5  /* hash-queue tick kernel: 0 = auto by live chains, 1 or 2 =
-                                   two waves (schedule producer loading 1 or 2 blocks ahead +
-                                   rounds consumer), 3 = one wave per 64 chains */
+#define CEC_OPT_DECODE_CACHE 6  /* capacity (>= 1) of the decode-program LRU cache, one entry
+                                   per erasure pattern (default 4096) */
 int cec_set_option(cec_codec* codec, int option, int value);
+/* Counters (tests / monitoring). */
+#define CEC_STAT_DECODE_CACHED 1   /* erasure patterns in the decode cache */
+#define CEC_STAT_RETIRED_PENDING 2 /* device blocks retired but possibly still read by queued
+                                      kernels (released once those complete) */
+int cec_get_stat(const cec_codec* codec, int stat, uint64_t* value);
 
 #ifdef __cplusplus
 }

@@ -155,12 +155,13 @@ def test_reconstruct_batch_per_segment(torch, cess, corc, k, m, ln, nseg, generi
 @pytest.mark.parametrize("k,m,ln", [(2, 1, (1 << 16) + 48), (32, 32, (1 << 14) + 4),
                                     (32, 32, 3000 * 4 + 7), (32, 32, 5)])
 def test_ct_variants_identical(torch, cess, corc, k, m, ln):
+    """Every kernel variant of the tuning build (libcessec_tune.so) is bit-exact too."""
     nseg = 4
     rng = np.random.default_rng(7)
     data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
     want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
     d_data = to_dev(torch, data)
-    enc = cess.New(k, m)
+    enc = cess.New(k, m, tuning=True)
     for v in range(-1, 21):
         enc.set_option(2, v)
         d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
@@ -249,15 +250,27 @@ def test_full_geometry_rs3232(torch, cess, corc):
 
 
 @pytest.fixture(params=[1, 2], ids=["sha1wave", "sha2wave"])
-def sha_mode(request, cess):
-    """Run a SHA-256 test with each kernel form (CEC_OPT_SHA_MODE), then restore auto."""
-    enc = cess.New(2, 1)
-    enc.set_option(3, request.param)
-    yield request.param
-    enc.set_option(3, 0)
+def sha_mode(request):
+    """Run a SHA-256 test with each kernel form (CEC_OPT_SHA_MODE on the test's codec)."""
+    return request.param
 
 
 def test_sha256_shavs_on_gpu(torch, cess, sha_mode):
+    """The reference's NIST SHAVS vectors through cec_sha256_batch (one buffer per launch)."""
+    vecs = parse_shavs("SHA256ShortMsg.rsp") + parse_shavs("SHA256LongMsg.rsp")
+    enc = cess.New(1, 1)
+    enc.set_option(3, sha_mode)
+    d_hex = torch.zeros((1, 1, 64), dtype=torch.uint8, device="cuda")
+    for msg, md in vecs:
+        b = torch.from_numpy(np.frombuffer(msg, np.uint8).copy() if msg else
+                             np.zeros(1, np.uint8)).cuda()
+        enc.Sha256Batch(b, None, 1, len(msg), d_hex)
+        torch.cuda.synchronize()
+        assert bytes(d_hex.cpu().numpy().reshape(64)).decode() == md, len(msg)
+
+
+def test_sha256_shavs_pointer_api(torch, cess):
+    """cec_sha256_hex (device pointer array, auto kernel) on the SHAVS vectors."""
     vecs = parse_shavs("SHA256ShortMsg.rsp") + parse_shavs("SHA256LongMsg.rsp")
     bufs = [torch.from_numpy(np.frombuffer(msg, np.uint8).copy() if msg else
                              np.zeros(1, np.uint8)).cuda() for msg, _ in vecs]
@@ -268,7 +281,9 @@ def test_sha256_shavs_on_gpu(torch, cess, sha_mode):
 
 @pytest.mark.parametrize("length", [0, 1, 55, 56, 63, 64, 119, 120, 1000, 4096 + 17])
 def test_sha256_many_unaligned(torch, cess, sha_mode, length):
-    """130 buffers (three 64-lane groups, the last partial) at odd and 16-byte-aligned starts."""
+    """130 buffers (three 64-lane groups, the last partial): back to back in the batch layout
+    (odd lengths put every start at a different misalignment) with the chosen kernel form, and
+    at odd / 16-byte-aligned starts through the pointer API."""
     n = 130
     rng = np.random.default_rng(length)
     pool = rng.integers(0, 256, n * (length + 32), dtype=np.uint8)
@@ -277,6 +292,14 @@ def test_sha256_many_unaligned(torch, cess, sha_mode, length):
     got = cess.sha256_hex_device([d_pool.data_ptr() + o for o in offs], length)
     for j, o in enumerate(offs):
         assert got[j].decode() == sha(pool[o:o + length]), j
+    enc = cess.New(1, 1)
+    enc.set_option(3, sha_mode)
+    d_hex = torch.zeros((n, 1, 64), dtype=torch.uint8, device="cuda")
+    enc.Sha256Batch(d_pool, None, n, length, d_hex)
+    torch.cuda.synchronize()
+    hx = d_hex.cpu().numpy().reshape(n, 64)
+    for j in range(n):
+        assert hx[j].tobytes().decode() == sha(pool[j * length:(j + 1) * length]), j
 
 
 def test_sha256_batch_matches_hashlib(torch, cess, sha_mode):
@@ -549,3 +572,64 @@ def test_runtime_kernels_agree(torch, cess, corc, k, m, ln):
     finally:
         enc.set_option(4, 0)
 
+
+
+@pytest.mark.parametrize("k,m,ln", [(32, 32, 4096 + 4), (10, 4, 1000)])
+def test_decode_cache_eviction(torch, cess, corc, k, m, ln):
+    """The decode-program LRU cache at capacity 8 (CEC_OPT_DECODE_CACHE) under per-segment
+    ReconstructBatch calls with 24 distinct erasure patterns each: programs resolved early in a
+    call stay valid while later patterns push the cache past its cap, and retired device blocks
+    are reused only after the launches that read them (bit-exact vs the C oracle every call)."""
+    nseg, ncall = 24, 3
+    n = k + m
+    rng = np.random.default_rng(k * 7 + ln)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    par = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    enc = cess.New(k, m)
+    enc.set_option(6, 8)
+    for call in range(ncall):
+        present = np.ones((nseg, n), np.uint8)
+        seen = set()
+        for s in range(nseg):
+            while True:
+                e = rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False)
+                key = tuple(sorted(e.tolist()))
+                if key not in seen:
+                    seen.add(key)
+                    break
+            present[s, list(key)] = 0
+        d_data = to_dev(torch, data * present[:, :k, None])
+        d_par = to_dev(torch, par * present[:, k:, None])
+        enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+        assert enc.stat(1) <= 8  # CEC_STAT_DECODE_CACHED
+        torch.cuda.synchronize()
+        assert np.array_equal(d_data.cpu().numpy(), data), call
+        assert np.array_equal(d_par.cpu().numpy(), par), call
+
+
+def test_back_to_back_plans_on_side_stream(torch, cess, corc):
+    """Per-segment reconstructs with different pattern maps enqueued back to back on a
+    non-blocking side stream without host synchronisation: each call's plan (segment list,
+    chunk pointers) must not be overwritten while earlier launches still read it."""
+    k, m, ln, nseg = 10, 4, 1 << 16, 16
+    n = k + m
+    rng = np.random.default_rng(99)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    par = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    enc = cess.New(k, m)
+    enc.set_option(6, 4)
+    calls = []
+    for _ in range(6):
+        present = np.ones((nseg, n), np.uint8)
+        for s in range(nseg):
+            present[s, rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False)] = 0
+        calls.append((present, to_dev(torch, data * present[:, :k, None]),
+                      to_dev(torch, par * present[:, k:, None])))
+    torch.cuda.synchronize()  # inputs in place; from here the calls only enqueue
+    side = torch.cuda.Stream()
+    for present, d_data, d_par in calls:
+        enc.ReconstructBatch(d_data, d_par, nseg, ln, present, stream=side)
+    side.synchronize()
+    for present, d_data, d_par in calls:
+        assert np.array_equal(d_data.cpu().numpy(), data)
+        assert np.array_equal(d_par.cpu().numpy(), par)

@@ -162,3 +162,87 @@ def test_segment_hash_shares_fragment0_stream(k, flen):
     seg_hex, d0_hex = segment_and_first_fragment_hex([memoryview(seg[i]) for i in range(k)])
     assert seg_hex == hashlib.sha256(seg.tobytes()).hexdigest().encode()
     assert d0_hex == hashlib.sha256(seg[0].tobytes()).hexdigest().encode()
+
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+@pytest.fixture(scope="module")
+def gfx950_code_object(tmp_path_factory):
+    """The gfx950 code object embedded in the shipped libcessec.so: (disassembly, notes)."""
+    from cess_amd import _lib
+    t = tmp_path_factory.mktemp("co")
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={t}/fb.bin",
+                    _lib.LIB_PATH, f"{t}/lib.copy"], check=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                    f"--input={t}/fb.bin", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                    f"--output={t}/k.co"], check=True)
+    dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", f"{t}/k.co"], check=True,
+                         capture_output=True, text=True).stdout
+    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", f"{t}/k.co"], check=True,
+                           capture_output=True, text=True).stdout
+    return dis, notes
+
+
+def kernel_bodies(dis, pat):
+    """{symbol: [instruction text]} for kernels whose symbol matches `pat`."""
+    out, cur = {}, None
+    for line in dis.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            cur = m.group(1) if re.search(pat, m.group(1)) else None
+            if cur:
+                out[cur] = []
+            continue
+        if cur and line.startswith("\t"):
+            ins = line.strip().split("//")[0].strip()
+            if ins:
+                out[cur].append(ins)
+    return out
+
+
+def test_rthx_index_mode_wait_states(gfx950_code_object):
+    """k_rthx (run-time Horner with M0-indexed table XORs, kernels.hip) is correct only if every
+    SALU write of M0 (s_set_gpr_idx_on / _idx / _off) is followed by one wait state before the next
+    VALU, only table XORs (SRC0 in the reserved v24..v151 range) run in index mode, and nothing
+    else in the kernel touches M0 (the asm blocks clobber it). Checked on the shipped code object,
+    so a compiler change that moves or drops a wait state fails here, without a GPU."""
+    dis, _ = gfx950_code_object
+    bodies = kernel_bodies(dis, r"k_rthx")
+    assert len(bodies) == 6, sorted(bodies)  # NG = 1, 2, 3, 4, 6, 8
+    for name, ins in bodies.items():
+        n_idx, on = 0, False
+        for i, t in enumerate(ins):
+            op = t.split()[0]
+            if op.startswith("s_set_gpr_idx_"):
+                n_idx += 1
+                assert ins[i + 1].split()[0] == "s_nop", (name, i, t, ins[i + 1])
+                on = op != "s_set_gpr_idx_off"
+                continue
+            if on and op.startswith("v_"):
+                m = re.match(r"v_xor_b32_e32 v\d+, v(\d+), v\d+$", t)
+                assert m and 24 <= int(m.group(1)) < 152, (name, i, t)
+            assert "m0" not in t, (name, i, t)
+        assert not on, name
+        assert n_idx > 0, name
+
+
+def test_rthx_resources(gfx950_code_object):
+    """k_rthx<NG> reserves v[24, 24 + 16 NG) for its tables above a 24-register compiler budget:
+    the descriptor must count them, with no scratch and no AGPRs."""
+    _, notes = gfx950_code_object
+    rows, cur = [], {}
+    for line in notes.splitlines():
+        m = re.match(r"\s+\.([a-z_]+):\s+(\S+)", line)
+        if m:
+            cur[m.group(1)] = m.group(2)
+            if m.group(1) == "vgpr_spill_count":
+                rows.append(dict(cur))
+    rthx = {r["name"]: r for r in rows if "k_rthx" in r.get("name", "")}
+    assert len(rthx) == 6
+    for name, r in rthx.items():
+        ng = int(re.search(r"k_rthxILi(\d+)E", name).group(1))
+        assert int(r["private_segment_fixed_size"]) == 0, name
+        assert int(r["vgpr_spill_count"]) == 0 and int(r["sgpr_spill_count"]) == 0, name
+        assert int(r.get("agpr_count", 0)) == 0, name
+        assert int(r["vgpr_count"]) >= 24 + 16 * ng, (name, r["vgpr_count"])

@@ -23,8 +23,6 @@ def main():
     args = ap.parse_args()
     import torch
     import cess_amd
-    enc = cess_amd.New(2, 1)
-    enc.set_option(5, args.pf)
     ln = args.blocks * 64
     stride = max(args.stride, ln)
     nmax = max(int(c) for c in args.chains.split(","))
@@ -32,11 +30,13 @@ def main():
     cess_amd.fill_synthetic(buf, stride, nmax, 0, 7)
     st = torch.cuda.Stream()
     with cess_amd.HashQueue(capacity=1 << 10, stream=st) as q:  # warm-up (code load, clocks)
+        q.set_option(1, args.pf)
         q.add(buf, 1024, 1, stride, stride, ln, None)
         q.finish()
         st.synchronize()
     for n in [int(c) for c in args.chains.split(",")]:
         q = cess_amd.HashQueue(capacity=1 << max(10, (n - 1).bit_length()), stream=st)
+        q.set_option(1, args.pf)  # CEC_HQOPT_TICK
         times = []
         for _ in range(args.reps):
             q.add(buf, n, 1, stride, stride, ln, None)

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""Repeat the RS(32,32) full-geometry per-segment decode (config 6 shape) and count wrong dwords
-per run for the run-time kernels (catches timing-dependent faults that one run can miss).
-usage: CESS_EC_LIB=... python tools/stress_rthx.py [--runs 10] [--mode 0]"""
+"""Repeat the RS(32,32) full-geometry per-segment decode (config 6 shape: 32 random erasures per
+segment, run-time coefficients) and count wrong bytes per run against the C oracle (data =
+the synthetic generator, parity = oracle/rs_oracle.c), for the run-time kernels. A repeat-run
+check for timing-dependent faults; the static wait-state rule of k_rthx is pinned on the code
+object by tests/test_host.py::test_rthx_index_mode_wait_states.
+usage: python tools/stress_rthx.py [--runs 10] [--mode 0] [--nseg 64]"""
 import argparse
 import os
 import sys
@@ -20,18 +23,23 @@ def main():
     args = ap.parse_args()
     import torch
     import cess_amd
+    from oracle.c_oracle import load_c_oracle
+    orc = load_c_oracle()
     k, m, F, nseg = 32, 32, 512 * 1024, args.nseg
-    d_data = torch.empty((nseg, k, F), dtype=torch.uint8, device="cuda")
-    d_par = torch.empty((nseg, m, F), dtype=torch.uint8, device="cuda")
-    cess_amd.fill_synthetic(d_data, k * F, nseg, 0, 0xCE550005)
-    enc = cess_amd.New(k, m)
-    enc.EncodeBatch(d_data, d_par, nseg, F)
-    ref_d, ref_p = d_data.clone(), d_par.clone()
+    seed = 0xCE550005
+    data = np.empty((nseg, k, F), np.uint8)
+    par = np.empty((nseg, m, F), np.uint8)
+    orc.orc_fill_synthetic(data.ctypes.data, k * F, nseg, 0, seed)
+    orc.orc_encode_batch(k, m, data.ctypes.data, par.ctypes.data, nseg, F,
+                         min(16, os.cpu_count() or 1), 1)
+    ref_d = torch.from_numpy(data).cuda()
+    ref_p = torch.from_numpy(par).cuda()
     rng = np.random.default_rng(3)
     present = np.ones((nseg, k + m), np.uint8)
     for s in range(nseg):
         present[s, rng.choice(k + m, size=m, replace=False)] = 0
     pres_t = torch.from_numpy(present).cuda().bool()
+    enc = cess_amd.New(k, m)
     enc.set_option(4, args.mode)
     bad = []
     for _ in range(args.runs):
@@ -41,9 +49,9 @@ def main():
         enc.ReconstructBatch(dd, dp, nseg, F, present)
         torch.cuda.synchronize()
         bad.append(int((dd != ref_d).sum() + (dp != ref_p).sum()))
-    print(os.environ.get("CESS_EC_LIB", "default"), "mode", args.mode, "bad bytes per run", bad,
-          flush=True)
+    print("mode", args.mode, "wrong bytes per run vs the C oracle", bad, flush=True)
+    return 1 if any(bad) else 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
