@@ -4,8 +4,9 @@ The compute path is libcessec (HIP kernels for gfx950 behind the C ABI in includ
 this package is the host-side mirror of the off-chain codec API (klauspost/reedsolomon shape)
 plus the CESS segment / fragment records.
 """
-from . import geometry
+from . import geometry, records
 from .hashq import HashQueue, sha256_blocks
+from .records import ErrTooManySegments
 from .reedsolomon import (
     CecError,
     Encoder,
@@ -26,5 +27,5 @@ __all__ = [
     "geometry", "CecError", "Encoder", "New", "ErrInvShardNum", "ErrMaxShardNum",
     "ErrReconstructRequired", "ErrShardNoData", "ErrShardSize", "ErrShortData",
     "ErrTooFewShards", "HipError", "fill_synthetic", "sha256_hex_device", "HashQueue",
-    "sha256_blocks",
+    "sha256_blocks", "records", "ErrTooManySegments",
 ]

@@ -4,13 +4,30 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+from ctypes import (CFUNCTYPE, POINTER, Structure, c_char_p, c_double, c_int, c_longlong,
+                    c_size_t, c_uint8, c_uint32, c_uint64, c_void_p)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CESS_EC_LIB", os.path.join(_HERE, "libcessec.so"))
 # tuning build of the same library: every kernel variant of the sweeps (CEC_OPT_CT_VARIANT);
 # used only by bench.py --sweep and the variant tests, never by the product path
 TUNE_LIB_PATH = os.path.join(_HERE, "libcessec_tune.so")
+
+# cec_pipeline_* callback and struct types (include/cess_ec.h)
+READ_FN = CFUNCTYPE(c_longlong, c_void_p, c_void_p, c_size_t)
+FRAGMENTS_FN = CFUNCTYPE(c_int, c_void_p, c_uint64, POINTER(c_void_p), c_size_t)
+RECORD_FN = CFUNCTYPE(c_int, c_void_p, c_uint64, c_void_p, c_void_p)
+
+
+class PipelineOpts(Structure):
+    _fields_ = [("shard_len", c_size_t), ("batch_segments", c_size_t), ("depth", c_int),
+                ("hash", c_int), ("window", c_int), ("max_segments", c_uint64)]
+
+
+class PipelineStats(Structure):
+    _fields_ = [("segments", c_uint64), ("bytes_in", c_uint64), ("seconds", c_double),
+                ("read_seconds", c_double), ("wait_seconds", c_double)]
+
 
 # exported symbols and their (restype, argtypes); tests check this against include/cess_ec.h
 SIGNATURES = {
@@ -20,6 +37,7 @@ SIGNATURES = {
     "cec_device_count": (c_int, []),
     "cec_create": (c_int, [c_int, c_int, c_int, POINTER(c_void_p)]),
     "cec_destroy": (None, [c_void_p]),
+    "cec_codec_info": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
     "cec_matrix": (c_int, [c_void_p, POINTER(c_uint8)]),
     "cec_encode": (c_int, [c_void_p, POINTER(c_void_p), c_size_t]),
     "cec_reconstruct": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint8), c_size_t, c_int]),
@@ -47,6 +65,18 @@ SIGNATURES = {
     "cec_hashq_status": (c_int, [c_void_p, c_uint64, POINTER(c_int), POINTER(c_size_t),
                                  POINTER(c_uint64)]),
     "cec_hashq_set_option": (c_int, [c_void_p, c_int, c_int]),
+    "cec_pipeline_create": (c_int, [c_void_p, POINTER(PipelineOpts), POINTER(c_void_p)]),
+    "cec_pipeline_destroy": (None, [c_void_p]),
+    "cec_pipeline_run": (c_int, [c_void_p, READ_FN, FRAGMENTS_FN, RECORD_FN, c_void_p,
+                                 POINTER(PipelineStats)]),
+    "cec_scale_compact": (c_int, [c_uint32, c_void_p, c_size_t, POINTER(c_size_t)]),
+    "cec_scale_deal_info": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t,
+                                    POINTER(c_size_t)]),
+    "cec_scale_upload_declaration": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t,
+                                             c_void_p, c_void_p, c_size_t, c_void_p, c_size_t,
+                                             c_void_p, c_size_t, POINTER(c_size_t)]),
+    "cec_shard_id": (c_int, [c_void_p, c_uint32, c_void_p]),
+    "cec_hash_from_shard_id": (c_int, [c_void_p, c_void_p]),
 }
 
 CEC_OK = 0
@@ -60,6 +90,8 @@ CEC_ESHORTDATA = -7
 CEC_ENODEV = -8
 CEC_ESEGCOUNT = -9
 CEC_ECALLBACK = -10
+CEC_SEGMENT_COUNT = 1000
+CEC_FRAGMENT_COUNT = 3
 
 CEC_OPT_FORCE_GENERIC = 1
 CEC_OPT_CT_VARIANT = 2

@@ -1,7 +1,17 @@
-"""cess-ec command line: `python -m cess_amd.cli encode <file> [--out DIR] [--k 2 --m 1]`
-prints the file's SegmentList records (the `deal_info` of FileBank::upload_declaration,
-c-pallets/file-bank/src/lib.rs:423) as JSON; with --out every fragment is written as
-DIR/<fragment hash>. `verify <file> <json>` re-encodes and compares the records."""
+"""cess-ec command line.
+
+  python -m cess_amd.cli encode <file> [--out DIR] [--scale FILE] [--k 2 --m 1]
+      streams the file through the GPU (libcessec host pipeline: pinned multi-buffered copies,
+      RS encode, GPU SegmentList hashes) and prints the file's SegmentList records (the
+      deal_info of FileBank::upload_declaration, c-pallets/file-bank/src/lib.rs:419-428) as
+      JSON. --out writes every fragment as DIR/<fragment hash> while the file streams (host
+      memory holds the pipeline's pinned batches, not the file). --scale writes the SCALE bytes
+      of deal_info; --call also writes the whole upload_declaration call data (needs --account,
+      --name, --bucket). A file over SegmentCount = 1000 segments (runtime/src/lib.rs:1026) is
+      rejected unless --no-segment-limit.
+  python -m cess_amd.cli verify <file> <json>
+      re-encodes and compares the records.
+"""
 import argparse
 import json
 import os
@@ -10,49 +20,82 @@ import sys
 from . import geometry
 
 
+def _encode(args) -> int:
+    from .pipeline import encode_file_records
+    from .records import ErrTooManySegments
+    from .segments import check_file_spec, needed_space
+    writer = None
+    tmp = {}
+    if args.out:
+        os.makedirs(args.out, exist_ok=True)
+
+        def writer(seg, idx, view):  # hash not known yet: temporary name, renamed on its record
+            path = os.path.join(args.out, f".part-{seg}-{idx}")
+            with open(path, "wb") as f:
+                f.write(memoryview(view))
+            tmp[(seg, idx)] = path
+    limit = 0 if args.no_segment_limit else geometry.SEGMENT_COUNT
+    try:
+        rec, st = encode_file_records(args.file, args.k, args.m, args.segment_size, args.device,
+                                      on_fragment=writer, max_segments=limit,
+                                      window=args.window)
+    except ErrTooManySegments:
+        for p in tmp.values():
+            os.unlink(p)
+        print(json.dumps({"error": f"file exceeds SegmentCount = {geometry.SEGMENT_COUNT} "
+                                   f"segments of {args.segment_size} bytes"}))
+        return 2
+    if args.out:
+        for (s, i), p in tmp.items():
+            os.replace(p, os.path.join(args.out, rec.segments[s].fragment_list[i].decode()))
+    out = rec.to_json()
+    out["check_file_spec"] = check_file_spec(rec.segments, args.k + args.m)
+    out["needed_space"] = needed_space(rec.segments, args.segment_size)
+    out["pipeline"] = {"seconds": round(st.seconds, 4), "read_seconds": round(st.read_seconds, 4),
+                       "GBps": round(st.bytes_in / max(st.seconds, 1e-9) / 1e9, 3)}
+    if args.scale:
+        with open(args.scale, "wb") as f:
+            f.write(rec.deal_info_scale())
+    if args.call:
+        if not (args.account and args.name and args.bucket):
+            print("--call needs --account, --name and --bucket", file=sys.stderr)
+            return 2
+        with open(args.call, "wb") as f:
+            f.write(rec.upload_declaration(bytes.fromhex(args.account), args.name.encode(),
+                                           args.bucket.encode()))
+    json.dump(out, sys.stdout)
+    print()
+    return 0
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="cess-ec")
     sub = ap.add_subparsers(dest="cmd", required=True)
     e = sub.add_parser("encode")
     e.add_argument("file")
     e.add_argument("--out", default=None)
+    e.add_argument("--scale", default=None, help="write deal_info's SCALE bytes here")
+    e.add_argument("--call", default=None, help="write upload_declaration call data here")
+    e.add_argument("--account", default=None, help="AccountId32 as 64 hex chars")
+    e.add_argument("--name", default=None)
+    e.add_argument("--bucket", default=None)
     e.add_argument("--k", type=int, default=geometry.DATA_SHARDS)
     e.add_argument("--m", type=int, default=geometry.PARITY_SHARDS)
     e.add_argument("--segment-size", type=int, default=geometry.SEGMENT_SIZE)
+    e.add_argument("--window", type=int, default=16)
     e.add_argument("--device", type=int, default=0)
+    e.add_argument("--no-segment-limit", action="store_true")
     v = sub.add_parser("verify")
     v.add_argument("file")
     v.add_argument("records")
     args = ap.parse_args(argv)
 
-    from .segments import SegmentEncoder, check_file_spec, needed_space
     if args.cmd == "encode":
-        se = SegmentEncoder(args.k, args.m, args.segment_size, device=args.device)
-        writer = None
-        if args.out:
-            os.makedirs(args.out, exist_ok=True)
-            pending = {}
-
-            def writer(s, i, buf):  # hash is known only after the batch: stash, write below
-                pending[(s, i)] = bytes(buf)
-        rec = se.encode_file(args.file, on_fragment=writer)
-        if args.out:
-            for (s, i), buf in pending.items():
-                with open(os.path.join(args.out, rec.segments[s].fragment_list[i].decode()),
-                          "wb") as f:
-                    f.write(buf)
-        se.close()
-        out = rec.to_json()
-        out["check_file_spec"] = check_file_spec(rec.segments, args.k + args.m)
-        out["needed_space"] = needed_space(rec.segments, args.segment_size)
-        json.dump(out, sys.stdout)
-        print()
-        return 0
+        return _encode(args)
+    from .pipeline import encode_file_records
     with open(args.records) as f:
         want = json.load(f)
-    se = SegmentEncoder()
-    got = se.encode_file(args.file).to_json()
-    se.close()
+    got = encode_file_records(args.file)[0].to_json()
     ok = got["segments"] == want["segments"] and got["file_hash"] == want["file_hash"]
     print(json.dumps({"ok": ok}))
     return 0 if ok else 1

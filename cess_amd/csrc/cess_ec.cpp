@@ -651,6 +651,14 @@ int cec_create(int k, int m, int device, cec_codec** out) {
 
 void cec_destroy(cec_codec* codec) { delete codec; }
 
+int cec_codec_info(const cec_codec* c, int* k, int* m, int* device) {
+  if (!c) return set_err(CEC_EINVAL, "null codec");
+  if (k) *k = c->k;
+  if (m) *m = c->m;
+  if (device) *device = c->device;
+  return CEC_OK;
+}
+
 int cec_matrix(const cec_codec* c, uint8_t* out) {
   if (!c || !out) return set_err(CEC_EINVAL, "null");
   for (int r = 0; r < c->k + c->m; ++r)

@@ -1,0 +1,207 @@
+"""Python mirror of libcessec's host pipeline (include/cess_ec.h `cec_pipeline_*`): a file in host
+memory -> segments -> fragments + SegmentList hashes through one GPU, with the pinned
+hipMemcpyAsync multi-buffering done in C++ (cess_amd/csrc/pipeline.cpp).
+
+The records it produces are `SegmentList { hash, fragment_list }`
+(c-pallets/file-bank/src/types.rs:13-16) for FileBank::upload_declaration
+(c-pallets/file-bank/src/lib.rs:419-428). Callbacks run on the calling thread; a Python exception
+raised in one aborts the run and is re-raised here.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import ctypes
+import os
+from ctypes import byref, c_void_p
+from typing import BinaryIO, Callable, Optional, Union
+
+import numpy as np
+
+from . import _lib, geometry
+from .reedsolomon import CecError, Encoder, check
+
+Source = Union[str, bytes, bytearray, memoryview, np.ndarray, BinaryIO]
+
+
+class _Reader:
+    """read() callback over a path (parallel os.preadv, GIL released), an in-memory buffer
+    (parallel numpy copies) or a binary stream (readinto)."""
+
+    def __init__(self, src: Source, threads: int = 8):
+        self.pool = cf.ThreadPoolExecutor(max_workers=threads)
+        self.threads = threads
+        self.fd = self.arr = self.stream = None
+        self.pos = 0
+        if isinstance(src, str):
+            self.fd = os.open(src, os.O_RDONLY)
+            self.size = os.fstat(self.fd).st_size
+        elif isinstance(src, (bytes, bytearray, memoryview, np.ndarray)):
+            self.arr = (src.reshape(-1).view(np.uint8) if isinstance(src, np.ndarray)
+                        else np.frombuffer(src, np.uint8))
+            self.size = self.arr.size
+        else:
+            self.stream = src
+            self.size = None
+
+    def _pread(self, mv: memoryview, off: int) -> None:
+        got = 0
+        while got < len(mv):
+            n = os.preadv(self.fd, [mv[got:]], off + got)
+            if n <= 0:
+                raise IOError("short read")
+            got += n
+
+    def __call__(self, dst: int, cap: int) -> int:
+        mv = memoryview((ctypes.c_uint8 * cap).from_address(dst)).cast("B")
+        if self.stream is not None:
+            n = self.stream.readinto(mv)
+            return n or 0
+        n = min(cap, self.size - self.pos)
+        if n <= 0:
+            return 0
+        step = max(4 << 20, -(-n // self.threads))
+        futs = []
+        for a in range(0, n, step):
+            e = min(n, a + step)
+            if self.arr is not None:
+                futs.append(self.pool.submit(np.copyto, np.frombuffer(mv[a:e], np.uint8),
+                                             self.arr[self.pos + a:self.pos + e]))
+            else:
+                futs.append(self.pool.submit(self._pread, mv[a:e], self.pos + a))
+        for f in futs:
+            f.result()
+        self.pos += n
+        return n
+
+    def close(self) -> None:
+        self.pool.shutdown(wait=True)
+        if self.fd is not None:
+            os.close(self.fd)
+            self.fd = None
+
+
+class Pipeline:
+    """cec_pipeline bound to one codec: `depth` pinned host batches of `batch_segments`
+    segments, GPU SegmentList hashing over a window of `window` batches when hash=True."""
+
+    def __init__(self, enc: Encoder, shard_len: int = geometry.FRAGMENT_SIZE,
+                 batch_segments: int = 64, depth: int = 3, hash: bool = True, window: int = 16,
+                 max_segments: int = 0):
+        self.enc = enc
+        self.k, self.m = enc.DataShards, enc.ParityShards
+        self.F = shard_len
+        self.opts = _lib.PipelineOpts(shard_len, batch_segments, depth, 1 if hash else 0, window,
+                                      max_segments)
+        self._lib = enc._lib
+        self._h = c_void_p()
+        check(self._lib.cec_pipeline_create(enc._h, byref(self.opts), byref(self._h)),
+              "Pipeline")
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.cec_pipeline_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def run(self, src: Source,
+            on_fragments: Optional[Callable[[int, list], None]] = None,
+            on_record: Optional[Callable[[int, bytes, list], None]] = None,
+            read_threads: int = 8) -> _lib.PipelineStats:
+        """Stream `src` through the GPU. on_fragments(seg, [k+m uint8 views]) sees every
+        segment's shards (views valid during the call only); on_record(seg, seg_hex,
+        [k+m fragment hex]) its hashes (hash=True). Returns the run's PipelineStats."""
+        n = self.k + self.m
+        F = self.F
+        reader = _Reader(src, read_threads)
+        err = []
+
+        def rd(_u, dst, cap):
+            try:
+                return reader(dst, cap)
+            except BaseException as e:  # noqa: BLE001 - re-raised after the C call returns
+                err.append(e)
+                return -1
+
+        def fr(_u, seg, shards, _len):
+            try:
+                views = [np.ctypeslib.as_array((ctypes.c_uint8 * F).from_address(shards[i]))
+                         for i in range(n)]
+                on_fragments(seg, views)
+                return 0
+            except BaseException as e:  # noqa: BLE001
+                err.append(e)
+                return -1
+
+        def rc_(_u, seg, seg_hex, frag_hex):
+            try:
+                fh = ctypes.string_at(frag_hex, 64 * n)
+                on_record(seg, ctypes.string_at(seg_hex, 64),
+                          [fh[64 * i:64 * (i + 1)] for i in range(n)])
+                return 0
+            except BaseException as e:  # noqa: BLE001
+                err.append(e)
+                return -1
+
+        cb_read = _lib.READ_FN(rd)
+        cb_frag = _lib.FRAGMENTS_FN(fr) if on_fragments else _lib.FRAGMENTS_FN()
+        cb_rec = _lib.RECORD_FN(rc_) if on_record else _lib.RECORD_FN()
+        stats = _lib.PipelineStats()
+        try:
+            rc = self._lib.cec_pipeline_run(self._h, cb_read, cb_frag, cb_rec, None, byref(stats))
+        finally:
+            reader.close()
+        if err:
+            raise err[0]
+        if rc == _lib.CEC_ESEGCOUNT:
+            from .records import ErrTooManySegments
+            raise ErrTooManySegments(ErrTooManySegments.__doc__)
+        check(rc, "Pipeline.run")
+        return stats
+
+
+def encode_file_records(path_or_buf: Source, k: int = geometry.DATA_SHARDS,
+                        m: int = geometry.PARITY_SHARDS,
+                        segment_size: int = geometry.SEGMENT_SIZE, device: int = 0,
+                        on_fragment: Optional[Callable[[int, int, np.ndarray], None]] = None,
+                        max_segments: int = 0, **kw):
+    """File -> FileRecord (SegmentLists + two-level file hash) through the C pipeline.
+    on_fragment(seg, idx, view) sees each fragment before its hash is known."""
+    from .segments import FileRecord, SegmentList, file_hash
+    if segment_size % k:
+        raise ValueError("segment_size must be a multiple of k")
+    recs = {}
+    if "batch_segments" not in kw:  # a small file does not need 1 GiB pinned batches
+        size = (os.path.getsize(path_or_buf) if isinstance(path_or_buf, str)
+                else len(path_or_buf) if isinstance(path_or_buf, (bytes, bytearray)) else None)
+        kw["batch_segments"] = 64 if size is None else max(1, min(64, -(-size // segment_size)))
+    enc = Encoder(k, m, device)
+    try:
+        with Pipeline(enc, segment_size // k, max_segments=max_segments, **kw) as p:
+            def frags(seg, views):
+                for i, v in enumerate(views):
+                    on_fragment(seg, i, v)
+
+            st = p.run(path_or_buf, frags if on_fragment else None,
+                       lambda seg, sh, fl: recs.__setitem__(seg, SegmentList(sh, fl)))
+    finally:
+        enc.close()
+    if not recs:
+        from .reedsolomon import ErrShortData
+        raise ErrShortData(ErrShortData.__doc__)
+    out = FileRecord(b"", int(st.bytes_in), [recs[s] for s in range(len(recs))])
+    out.file_hash = file_hash(out.segments)
+    return out, st
+
+
+__all__ = ["Pipeline", "encode_file_records", "CecError"]

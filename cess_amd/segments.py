@@ -73,6 +73,18 @@ class FileRecord:
         return {"file_hash": self.file_hash.decode(), "size": self.size,
                 "segments": [s.to_json() for s in self.segments]}
 
+    def deal_info_scale(self) -> bytes:
+        """SCALE bytes of upload_declaration's deal_info (records.deal_info); raises
+        records.ErrTooManySegments past SegmentCount = 1000 segments."""
+        from .records import deal_info
+        return deal_info(self.segments)
+
+    def upload_declaration(self, account: bytes, file_name: bytes, bucket_name: bytes) -> bytes:
+        """Call data of FileBank::upload_declaration for this file (records.upload_declaration)."""
+        from .records import upload_declaration
+        return upload_declaration(self.file_hash, self.segments, account, file_name,
+                                  bucket_name)
+
 
 def file_hash(seg_list: List[SegmentList]) -> bytes:
     """SHA-256 hex over the concatenated segment hashes (two-level file hash)."""

@@ -59,6 +59,8 @@ int cec_device_count(void);
 /* New(k, m): codec bound to `device`. Builds the (k+m) x k matrix; k >= 1, m >= 1, k+m <= 256. */
 int cec_create(int k, int m, int device, cec_codec** out);
 void cec_destroy(cec_codec* codec);
+/* k, m and device of a codec (any output pointer may be NULL). */
+int cec_codec_info(const cec_codec* codec, int* k, int* m, int* device);
 /* Copy the (k+m) x k encode matrix, row-major, into `out`. Host only, no GPU work. */
 int cec_matrix(const cec_codec* codec, uint8_t* out);
 
@@ -143,6 +145,88 @@ int cec_hashq_set_option(cec_hashq* q, int option, int value);
  * zero-padded past seg_len. Requires k*shard_len >= seg_len > 0. */
 int cec_split_segment(const uint8_t* seg, size_t seg_len, int k, uint8_t* const* shards,
                       size_t shard_len);
+
+/* ---- host pipeline: a file in host memory through the GPU ------------------------------------
+ * The north_star's pinned hipMemcpyAsync multi-buffering behind the C ABI. A pipeline owns a
+ * ring of `depth` pinned host batches and device slots for one codec; cec_pipeline_run streams
+ * a source through it batch by batch: read() fills a pinned batch (the file's next bytes; the
+ * last segment is zero-padded, klauspost Split), H2D on a copy stream, cec_encode_batch on a
+ * compute stream, parity D2H on a third stream, so reading batch i+1 overlaps the copies and
+ * kernels of batch i and H2D overlaps D2H. With hash = 1 every SegmentList hash (segment hash
+ * and the k+m fragment hashes, SHA-256 hex) is computed on the GPU by a hash queue that keeps
+ * `window` batches hashing at once (device slots = window + 1).
+ *   read(user, dst, cap): write up to cap source bytes at dst; return the count, 0 at the end,
+ *     < 0 to abort (CEC_ECALLBACK).
+ *   on_fragments(user, seg, shards, shard_len): the k+m shards of segment `seg`, host memory
+ *     valid during the call; in segment order, as soon as the batch's parity is back.
+ *   on_record(user, seg, seg_hex, frag_hex): the segment's 64 hex chars and its k+m fragment
+ *     hashes (k+m)*64 hex chars, fragment index order; in segment order, `window` batches later.
+ * Callbacks run on the calling thread and return 0 (nonzero aborts with CEC_ECALLBACK). */
+typedef long long (*cec_read_fn)(void* user, uint8_t* dst, size_t cap);
+typedef int (*cec_fragments_fn)(void* user, uint64_t seg, const uint8_t* const* shards,
+                                size_t shard_len);
+typedef int (*cec_record_fn)(void* user, uint64_t seg, const uint8_t* seg_hex,
+                             const uint8_t* frag_hex);
+typedef struct cec_pipeline_opts {
+  size_t shard_len;      /* F: a segment is k * F bytes */
+  size_t batch_segments; /* segments per batch (0: 64) */
+  int depth;             /* pinned host batches (0: 3; >= 2) */
+  int hash;              /* 1: SegmentList hashes on the GPU (on_record); 0: none */
+  int window;            /* batches hashing at once when hash = 1 (0: 16) */
+  uint64_t max_segments; /* 0: no limit; else CEC_ESEGCOUNT when the source has more segments
+                            (CEC_SEGMENT_COUNT: what one upload_declaration can carry) */
+} cec_pipeline_opts;
+typedef struct cec_pipeline_stats {
+  uint64_t segments;   /* segments encoded */
+  uint64_t bytes_in;   /* source bytes read */
+  double seconds;      /* wall time of the run */
+  double read_seconds; /* time inside read() */
+  double wait_seconds; /* host time blocked on the GPU */
+} cec_pipeline_stats;
+typedef struct cec_pipeline cec_pipeline;
+int cec_pipeline_create(cec_codec* codec, const cec_pipeline_opts* opts, cec_pipeline** out);
+void cec_pipeline_destroy(cec_pipeline* p);
+/* Stream one source through the pipeline (reusable: run again for the next file). */
+int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_fragments,
+                     cec_record_fn on_record, void* user, cec_pipeline_stats* stats);
+
+/* ---- on-chain records (host only, no GPU) ---------------------------------------------------
+ * SCALE bytes of what the codec's outputs become on chain:
+ *   FileBank::upload_declaration(file_hash: Hash, deal_info: BoundedVec<SegmentList,
+ *     SegmentCount>, user_brief: UserBrief)          c-pallets/file-bank/src/lib.rs:419-428
+ *   SegmentList { hash: Hash, fragment_list: BoundedVec<Hash, FragmentCount> }   types.rs:13-16
+ *   UserBrief { user: AccountId32, file_name, bucket_name: BoundedVec<u8, 63> }  types.rs:105-109
+ *   Hash([u8; 64]) (a fixed array: 64 bytes, no length prefix)  primitives/common/src/lib.rs:16
+ * Hashes are passed as 64 lowercase hex characters each. Every function writes at most out_cap
+ * bytes to `out` and sets *out_len to the encoded size; out == NULL only sizes the encoding. */
+#define CEC_SEGMENT_COUNT 1000 /* runtime/src/lib.rs:1026 (SegmentCount) */
+#define CEC_FRAGMENT_COUNT 3   /* runtime/src/lib.rs:1027 (FragmentCount) */
+#define CEC_NAME_MIN 3         /* runtime/src/lib.rs:1051 (NameMinLength) */
+#define CEC_NAME_MAX 63        /* runtime/src/lib.rs:1041 (NameStrLimit) */
+#define CEC_FILEBANK_PALLET 60 /* runtime/src/lib.rs:1532 */
+#define CEC_CALL_UPLOAD_DECLARATION 0 /* c-pallets/file-bank/src/lib.rs:420 call_index(0) */
+/* SCALE compact encoding of n. */
+int cec_scale_compact(uint32_t n, uint8_t* out, size_t out_cap, size_t* out_len);
+/* deal_info = compact(nseg) ++ per segment: hash ++ compact(nfrag) ++ nfrag hashes.
+ * seg_hex: nseg * 64 bytes; frag_hex: nseg * nfrag * 64 (fragment index order).
+ * CEC_ESEGCOUNT if nseg > CEC_SEGMENT_COUNT (the extrinsic would be rejected: split the file);
+ * CEC_EINVAL if nfrag is 0 or > CEC_FRAGMENT_COUNT or a hash is not lowercase hex. */
+int cec_scale_deal_info(const uint8_t* seg_hex, const uint8_t* frag_hex, size_t nseg,
+                        size_t nfrag, uint8_t* out, size_t out_cap, size_t* out_len);
+/* Call data of upload_declaration: pallet index, call index, file_hash, deal_info, user_brief
+ * (account: 32 bytes; names 3..63 bytes). */
+int cec_scale_upload_declaration(const uint8_t* file_hash_hex, const uint8_t* seg_hex,
+                                 const uint8_t* frag_hex, size_t nseg, size_t nfrag,
+                                 const uint8_t* account, const uint8_t* file_name,
+                                 size_t file_name_len, const uint8_t* bucket_name,
+                                 size_t bucket_name_len, uint8_t* out, size_t out_cap,
+                                 size_t* out_len);
+/* 68-byte shard id = 64 hex chars ++ "-NNN" (index 0..999), the form Hash::from_shard_id reads
+ * back (primitives/common/src/lib.rs:45-49; c-pallets/audit/src/tests.rs:267-269 builds
+ * file_hash ++ "-001"). */
+int cec_shard_id(const uint8_t* hash_hex, uint32_t index, uint8_t* out68);
+/* Hash::from_shard_id: the first 64 bytes. */
+int cec_hash_from_shard_id(const uint8_t* shard_id68, uint8_t* hash_hex_out);
 
 /* Synthetic segments in HBM: little-endian 64-bit word w of segment s is
  * splitmix64(seed ^ ((seg0 + s) << 32) ^ w). seg_bytes must be a multiple of 8. */

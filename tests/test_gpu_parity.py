@@ -385,29 +385,6 @@ def test_degraded_read_single_rank(torch, cess, corc):
         assert np.array_equal(t.cpu().numpy(), full[s][f])
 
 
-def test_cli_encode_and_verify(tmp_path, orc):
-    import json
-    import subprocess
-    import sys
-    rng = np.random.default_rng(3)
-    blob = rng.integers(0, 256, 3 * MiB + 5, dtype=np.uint8).tobytes()
-    src = tmp_path / "f.bin"
-    src.write_bytes(blob)
-    outdir = tmp_path / "frags"
-    r = subprocess.run([sys.executable, "-m", "cess_amd.cli", "encode", str(src), "--out",
-                        str(outdir), "--segment-size", str(1 << 20)], capture_output=True,
-                       text=True, timeout=300, check=True)
-    rec = json.loads(r.stdout)
-    want = orc.segment_list(blob, 2, 1, 1 << 20)
-    assert [(s["hash"].encode(), [f.encode() for f in s["fragment_list"]])
-            for s in rec["segments"]] == want
-    assert rec["check_file_spec"] and rec["needed_space"] == 4 * (1 << 20) * 15 // 10
-    files = sorted(p.name for p in outdir.iterdir())
-    assert files == sorted({f.decode() for _, fl in want for f in fl})
-    for p in outdir.iterdir():
-        assert hashlib.sha256(p.read_bytes()).hexdigest() == p.name
-
-
 def test_max_shards_256(cess, corc):
     """k + m = 256 (the GF(2^8) limit): run-time kernel, outputs split over chunks of 32."""
     k, m, ln = 200, 56, 272

@@ -1,0 +1,109 @@
+"""The C host pipeline (cec_pipeline_*, pinned multi-buffered H2D / encode / D2H + GPU
+SegmentList hashes) driven from C (tests/native/pipeline_e2e.c) and from Python
+(cess_amd.pipeline), against the C / Python oracles: every sampled segment's fragments and
+hashes, delivery order, zero-padded tails, SegmentCount enforcement, callback errors."""
+import hashlib
+import json
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+MiB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def e2e_exe(tmp_path_factory):
+    exe = tmp_path_factory.mktemp("native") / "pipeline_e2e"
+    lib, orc = f"{ROOT}/cess_amd", f"{ROOT}/oracle/build"
+    subprocess.run(["gcc", "-O2", "-pthread", f"{ROOT}/tests/native/pipeline_e2e.c",
+                    f"-I{ROOT}/include", f"-L{lib}", "-lcessec", f"-L{orc}", "-loracle",
+                    f"-Wl,-rpath,{lib}:{orc}", "-o", str(exe)], check=True)
+    return str(exe)
+
+
+@pytest.mark.parametrize("args", [
+    # k m F nseg batch depth hash window uniq check_every tail
+    (2, 1, 1 << 19, 41, 8, 3, 1, 2, 41, 1, 12345),   # CESS shape, hashes, padded tail
+    (2, 1, 1 << 19, 41, 8, 2, 0, 0, 41, 1, 1),       # no hashing, depth 2
+    (4, 2, 4160, 33, 5, 3, 1, 3, 33, 1, 0),          # F % 64 == 0: prefix-digest segment chain
+    (32, 32, 1000, 20, 4, 2, 1, 1, 20, 1, 999),      # F % 64 != 0, window 1, wide code
+    (10, 4, 4096, 7, 64, 3, 1, 16, 7, 1, 0),         # one partial batch
+])
+def test_pipeline_from_c(e2e_exe, args):
+    r = subprocess.run([e2e_exe] + [str(a) for a in args], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["pipeline"] == "ok" and out["bad"] == 0 and out["checked"] == args[3]
+
+
+def test_pipeline_python_records(orc):
+    from cess_amd.pipeline import encode_file_records
+    for size, seg, k, m in [(5 * MiB + 7, MiB, 2, 1), (3 * MiB, MiB // 2, 4, 2),
+                            (MiB - 3, MiB // 4, 32, 32)]:
+        blob = np.random.default_rng(size).integers(0, 256, size, dtype=np.uint8).tobytes()
+        frags = {}
+        rec, st = encode_file_records(
+            blob, k, m, seg, batch_segments=2, window=2,
+            on_fragment=lambda s, i, v: frags.__setitem__((s, i), hashlib.sha256(v).hexdigest()))
+        want = orc.segment_list(blob, k, m, seg)
+        assert [(s.hash, s.fragment_list) for s in rec.segments] == want
+        assert rec.file_hash == orc.file_hash(want) and rec.size == size
+        assert st.segments == len(want)
+        for (s, i), h in frags.items():
+            assert h.encode() == want[s][1][i]
+
+
+def test_pipeline_segment_limit_and_callback_errors():
+    import cess_amd
+    from cess_amd.pipeline import Pipeline
+    blob = np.zeros(5 * 4096 * 2, np.uint8)
+    enc = cess_amd.New(2, 1)
+    with Pipeline(enc, 4096, batch_segments=2, window=2, max_segments=4) as p:
+        with pytest.raises(cess_amd.ErrTooManySegments):
+            p.run(blob)
+    with Pipeline(enc, 4096, batch_segments=2, window=2) as p:
+        def boom(seg, views):
+            if seg == 3:
+                raise KeyError("stop")
+        with pytest.raises(KeyError):
+            p.run(blob, on_fragments=boom)
+        st = p.run(blob)  # the pipeline is reusable after an aborted run
+        assert st.segments == 5
+
+
+def test_cli_encode_streams_fragments_and_scale(tmp_path, orc):
+    import sys
+    from cess_amd import records
+    from cess_amd.segments import SegmentList
+    rng = np.random.default_rng(3)
+    blob = rng.integers(0, 256, 3 * MiB + 5, dtype=np.uint8).tobytes()
+    src = tmp_path / "f.bin"
+    src.write_bytes(blob)
+    outdir = tmp_path / "frags"
+    r = subprocess.run([sys.executable, "-m", "cess_amd.cli", "encode", str(src), "--out",
+                        str(outdir), "--segment-size", str(1 << 20), "--scale",
+                        str(tmp_path / "deal.scale")], capture_output=True, text=True,
+                       timeout=300, check=True, cwd=ROOT)
+    rec = json.loads(r.stdout)
+    want = orc.segment_list(blob, 2, 1, 1 << 20)
+    assert [(s["hash"].encode(), [f.encode() for f in s["fragment_list"]])
+            for s in rec["segments"]] == want
+    assert rec["check_file_spec"] and rec["needed_space"] == 4 * (1 << 20) * 15 // 10
+    files = sorted(p.name for p in outdir.iterdir())
+    assert files == sorted({f.decode() for _, fl in want for f in fl})
+    for p in outdir.iterdir():
+        assert hashlib.sha256(p.read_bytes()).hexdigest() == p.name
+    assert (tmp_path / "deal.scale").read_bytes() == records.deal_info(
+        [SegmentList(h, fl) for h, fl in want])
+    # over SegmentCount segments (16 KiB segments: 1001 of them) -> rejected
+    big = tmp_path / "big.bin"
+    big.write_bytes(bytes(1001 * 16384))
+    r = subprocess.run([sys.executable, "-m", "cess_amd.cli", "encode", str(big),
+                        "--segment-size", "16384"], capture_output=True, text=True, timeout=300,
+                       cwd=ROOT)
+    assert r.returncode == 2 and "SegmentCount" in r.stdout
