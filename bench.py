@@ -7,12 +7,17 @@ segments per GPU, RS(k=2, m=1), 8 MiB fragments, device-resident (inputs already
 the timed region starts). A "step" is one batched encode launch over the rank's 64 segments.
 Bytes counted per segment = (k+m) * F (k fragments read, m written).
 
-    python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4|5]
+    python bench.py [--gpus N --steps K --warmup W] [--config 1|2|3|4|5]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, weak scaling)
 
 Rank 0 prints one JSON line. `roofline` is the dominant kernel's algorithmic bytes per launch /
 its average launch time (HIP events on the launch stream); `cpu_baseline` times the C oracle
 (oracle/rs_oracle.c, kind "port": the reference ships no codec) on a bounded sample on rank 0.
+With N > 1 the default line also carries `extra.degraded_gather`: the RCCL survivor gather of
+BASELINE config 4 (fragment f of segment s on GPU (s + f) mod N) and the rebuild after it.
+Config 1 is the CPU codec alone (one 16 MiB segment: encode + the 3 single-erasure rebuilds at
+1 thread and at the host's CPU share); config 4 is 64 GiB sharded over the ranks with the
+degraded-read gather inside every step.
 """
 from __future__ import annotations
 
@@ -35,9 +40,13 @@ SEED0 = 0xCE550000
 
 CONFIGS = {
     # id: (k, m, fragment bytes, segments per GPU, description)
+    1: (2, 1, 8 * MiB, 1, "single 16 MiB segment RS(2,1): encode + the 3 single-erasure "
+                          "reconstructs, CPU codec (no GPU)"),
     2: (2, 1, 8 * MiB, 64, "batched RS(2,1) encode of 1 GiB of 16 MiB segments per GPU"),
     3: (2, 1, 8 * MiB, 64, "degraded reconstruct RS(2,1), erased fragment = seg mod 3, 1 GiB"),
-    4: (2, 1, 8 * MiB, 4096, "64 GiB file (4096 x 16 MiB segments) encoded, sharded over GPUs"),
+    4: (2, 1, 8 * MiB, 4096, "64 GiB file (4096 x 16 MiB segments) encoded, sharded over GPUs, "
+                             "+ cross-GPU degraded-read gather (RCCL) of 64 segments per GPU "
+                             "and their rebuild, every step"),
     5: (32, 32, 512 * 1024, 64, "RS(32,32) encode of 1 GiB + SHA-256 of all 64 fragments "
                                 "(encode + GPU hash queue, a window of batches hashing at once)"),
     # stress variant of config 3 for the wide code (not a BASELINE config): every segment loses
@@ -50,12 +59,22 @@ CONFIGS = {
 }
 
 
+GPU_BOX_CPU_SHARE = 16  # CPUs the harness gives one GPU's job on the box (its pools obey this)
+
+
 def cpu_threads() -> int:
+    """Threads for the CPU baseline: the host's CPU share for this GPU. The GPU box shows the
+    whole machine's CPUs to nproc / os.cpu_count() but gives one GPU's job a 16-CPU share, and
+    worker pools must stay within it; the CPU rate is therefore quoted at that share, with
+    the per-thread rate beside it."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(16, n))  # a GPU box gives one GPU a 16-CPU share
+    return max(1, min(GPU_BOX_CPU_SHARE, n))
+
+
+SIMD_NAMES = {0: "scalar table", 1: "AVX2 split-nibble", 2: "AVX-512BW + GFNI affine"}
 
 
 def cpu_model() -> str:
@@ -73,7 +92,7 @@ def cpu_baseline(k: int, m: int, F: int, target_s: float) -> dict:
     """Time the C oracle (oracle/rs_oracle.c) on a bounded sample of the same workload."""
     from oracle.c_oracle import load_c_oracle
     orc = load_c_oracle()
-    simd = orc.orc_set_simd(-1)
+    simd = orc.orc_set_simd(-1)  # the best form the host has
     # same workload shape as the GPU step (1 GiB of segments), larger than the host's LLC
     nseg = max(1, (1 << 30) // (k * F))
     data = np.empty(nseg * k * F, np.uint8)
@@ -93,11 +112,152 @@ def cpu_baseline(k: int, m: int, F: int, target_s: float) -> dict:
         "cores": threads,
         "kind": "port",
         "sample": f"{reps} x {nseg} segments of {k * F // MiB} MiB, RS({k},{m}), "
-                  f"{'AVX2 split-nibble' if simd == 1 else 'scalar table'} C oracle, "
-                  f"{threads} threads, {t:.1f} s",
+                  f"{SIMD_NAMES[simd]} C oracle, {threads} threads (this GPU's CPU share), "
+                  f"{t:.1f} s",
         "value_1thread": round(n1 * per_seg / st / GB, 3),
         "cpu_model": cpu_model(),
+        "host_cpus_visible": os.cpu_count(),
     }
+
+
+def cpu_sha256(k: int, m: int, F: int, target_s: float) -> dict:
+    """CPU leg of config 5's hashing: OpenSSL SHA-256 (hashlib; SHA-NI where the host has it)
+    over the fragments of one batch, on the CPU share (hashlib releases the GIL)."""
+    import concurrent.futures as cf
+    import hashlib
+    nfrag = (1 << 30) // F  # 1 GiB of fragments
+    buf = np.frombuffer(np.random.default_rng(5).bytes(nfrag * F), np.uint8).reshape(nfrag, F)
+    threads = cpu_threads()
+    t0 = time.perf_counter()
+    reps = 0
+    with cf.ThreadPoolExecutor(threads) as ex:
+        while True:
+            list(ex.map(lambda i: hashlib.sha256(buf[i]).digest(), range(nfrag)))
+            reps += 1
+            if time.perf_counter() - t0 > target_s:
+                break
+    t = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    for i in range(min(nfrag, 64)):
+        hashlib.sha256(buf[i]).digest()
+    t1 = time.perf_counter() - t1
+    return {"value": round(reps * nfrag * F / t / GB, 3), "unit": "GB/s hashed",
+            "cores": threads, "kind": "library (OpenSSL via hashlib)",
+            "sample": f"{reps} x {nfrag} fragments of {F // 1024} KiB, {threads} threads",
+            "value_1thread": round(min(nfrag, 64) * F / t1 / GB, 3)}
+
+
+def config1_cpu(args) -> dict:
+    """BASELINE config 1: one 16 MiB segment, RS(2,1): encode + the 3 single-erasure rebuilds,
+    on the CPU codec (oracle/rs_oracle.c, kind "port": the reference has no codec), at 1 thread
+    and at this GPU's CPU share; the same ops on the GPU (device resident) beside it."""
+    from oracle.c_oracle import load_c_oracle, ptrs
+    k, m, F = 2, 1, 8 * MiB
+    orc = load_c_oracle()
+    simd = orc.orc_set_simd(-1)
+    seg = np.empty(k * F, np.uint8)
+    orc.orc_fill_synthetic(seg.ctypes.data, k * F, 1, 0, SEED0 + 1)
+    shards = [seg[:F].copy(), seg[F:].copy(), np.zeros(F, np.uint8)]
+    per_op = (k + m) * F  # read k, write 1 (RS(2,1)): 24 MiB per op
+    ops = 1 + (k + m)
+    out = {}
+    for th in (1, cpu_threads()):
+        orc.orc_segment_ops(k, m, ptrs(shards), F, th, 1)
+        t1 = orc.orc_segment_ops(k, m, ptrs(shards), F, th, 1)
+        reps = max(1, int(args.cpu_seconds / 2 / max(t1, 1e-6)))
+        t = orc.orc_segment_ops(k, m, ptrs(shards), F, th, reps)
+        out[th] = (reps * ops * per_op / t / GB, reps, t)
+    threads = cpu_threads()
+    res = {
+        "metric": METRIC, "value": round(out[threads][0], 3), "unit": "GB/s", "n_gpus": 0,
+        "steps": out[threads][1], "warmup": 1,
+        "ms_per_step": round(out[threads][2] / out[threads][1] * 1e3, 4),
+        "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64 counter generator)",
+        "config": {"workload": CONFIGS[1][4], "baseline_config": 1, "k": k, "m": m,
+                   "fragment_bytes": F, "ops_per_step": "encode + rebuild of shard 0, 1, 2",
+                   "bytes_per_op": per_op},
+        "roofline": None,
+        "cpu_baseline": {"value": round(out[threads][0], 3), "unit": "GB/s", "cores": threads,
+                         "kind": "port",
+                         "sample": f"{out[threads][1]} x (encode + 3 rebuilds) of one 16 MiB "
+                                   f"segment, {SIMD_NAMES[simd]}, columns split over {threads} "
+                                   f"threads (this GPU's CPU share)",
+                         "value_1thread": round(out[1][0], 3), "cpu_model": cpu_model(),
+                         "host_cpus_visible": os.cpu_count()},
+        "note": "the reference ships no codec (SURVEY.md §0.1); the CPU codec is this repo's C "
+                "restatement of klauspost/reedsolomon",
+    }
+    try:
+        import torch
+        if torch.cuda.is_available():
+            import cess_amd
+            dev = torch.device("cuda", 0)
+            d_data = torch.from_numpy(seg.reshape(1, k, F)).to(dev)
+            d_par = torch.empty((1, m, F), dtype=torch.uint8, device=dev)
+            enc = cess_amd.New(k, m)
+            st = torch.cuda.current_stream(dev)
+            pats = [np.array([int(i != e) for i in range(k + m)], np.uint8) for e in range(k + m)]
+
+            def step():
+                enc.EncodeBatch(d_data, d_par, 1, F, stream=st)
+                for p in pats:
+                    enc.ReconstructBatch(d_data, d_par, 1, F, p, stream=st)
+            for _ in range(5):
+                step()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            for _ in range(50):
+                step()
+            b.record(st)
+            torch.cuda.synchronize(dev)
+            ms = a.elapsed_time(b) / 50
+            res["gpu_same_workload"] = {"GBps": round(ops * per_op / (ms * 1e-3) / GB, 2),
+                                        "ms_per_step": round(ms, 4),
+                                        "note": "one segment per launch: launch-latency bound"}
+    except Exception as e:  # noqa: BLE001 - the CPU leg stands on its own
+        res["gpu_same_workload"] = {"error": str(e)[:200]}
+    return res
+
+
+def degraded_gather(enc, k: int, m: int, F: int, world: int, rank: int, dev, nseg: int):
+    """BASELINE config 4's exchange step, set up once: segments 0..nseg*world-1 stored under the
+    miner-spread placement (fragment f of segment s on GPU (s + f) mod world,
+    c-pallets/file-bank/src/functions.rs:187-283), every segment losing fragment s mod (k+m).
+    Returns (run, plan): run() gathers the survivors over the process group (RCCL point to
+    point; RCCL has no XOR reduction) and rebuilds the lost fragments with libcessec."""
+    import torch
+    import cess_amd
+    from cess_amd import distributed as D
+    n = k + m
+    total = nseg * world
+    mine = D.local_fragments(total, n, world, rank)
+    store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
+                            torch.empty((max(1, len(mine)), F), dtype=torch.uint8, device=dev))
+    seg_d = torch.empty((1, k, F), dtype=torch.uint8, device=dev)
+    seg_p = torch.empty((1, m, F), dtype=torch.uint8, device=dev)
+    for s in range(total):
+        if not any((s, f) in store.slots for f in range(n)):
+            continue
+        cess_amd.fill_synthetic(seg_d, k * F, 1, s, SEED0 + 4)
+        enc.EncodeBatch(seg_d, seg_p, 1, F)
+        for f in range(n):
+            if (s, f) in store.slots:
+                store.data[store.slots[(s, f)]].copy_(seg_d[0, f] if f < k else seg_p[0, f - k])
+    torch.cuda.synchronize(dev)
+    plan = D.plan_gather({s: [s % n] for s in range(total)}, k, m, world, F)
+
+    def run():
+        return D.degraded_read(plan, store, enc, rank)
+
+    def verify(out) -> bool:
+        ok = True
+        for (s, f), got in out.items():
+            cess_amd.fill_synthetic(seg_d, k * F, 1, s, SEED0 + 4)
+            enc.EncodeBatch(seg_d, seg_p, 1, F)
+            ok &= bool(torch.equal(got, seg_d[0, f] if f < k else seg_p[0, f - k]))
+        return ok
+    return run, verify, plan
 
 
 def load_traffic(tag: str, algo_bytes: int, kernel: str):
@@ -142,6 +302,10 @@ def main() -> None:
                     help="comma list of CT variants: interleaved A/B in one process, prints "
                          "median launch ms per variant and exits")
     args = ap.parse_args()
+
+    if args.config == 1:  # CPU codec alone (the GPU on the same workload beside it)
+        print(json.dumps(config1_cpu(args)), flush=True)
+        return
 
     import torch
     import torch.distributed as dist
@@ -197,6 +361,10 @@ def main() -> None:
         for s_ in range(nseg):
             present[s_, rng.choice(k + m, size=ne, replace=False)] = 0
     d_hex = None
+    gather = None
+    if args.config == 4:
+        # the degraded-read gather of 64 segments per rank runs inside every step
+        gather = degraded_gather(enc, k, m, F, world, rank, dev, 64)
     if args.config == 5:
         # Windowed pipeline over steps: step i encodes into parity buffer i % W on the launch
         # stream, then (on the hash stream, after the encode) adds the batch's 64 * nseg
@@ -240,6 +408,9 @@ def main() -> None:
             hq.tick(tick_blocks)
             # this tick completed batch i - W + 1, whose buffer step i + 2 takes
             ev_free[(i - W + 1) % NB].record(sha_stream)
+        elif args.config == 4:
+            enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
+            gather[0]()
         else:
             enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
 
@@ -316,17 +487,22 @@ def main() -> None:
     value = world * bytes_step_gpu * args.steps / elapsed / GB
     achieved = bytes_step_gpu / (launch_ms * 1e-3) / GB
 
+    def timed(fn, reps=5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            fn()
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        return a.elapsed_time(b) / reps
+
     sha_note = None
+    if args.config == 4:
+        # the step holds encode + the degraded-read gather; the roofline is the encode kernel's
+        launch_ms = timed(lambda: enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream), 10)
+        achieved = bytes_step_gpu / (launch_ms * 1e-3) / GB
     if args.config == 5:
         # the step holds encode + SHA-256; time each kernel alone for the roofline
-        def timed(fn, reps=5):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-            for _ in range(reps):
-                fn()
-            b.record(stream)
-            torch.cuda.synchronize(dev)
-            return a.elapsed_time(b) / reps
         enc_ms = timed(lambda: enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream), 20)
         sha_ms = timed(lambda: enc.Sha256Batch(d_data, d_par, nseg, F, d_hex, stream=stream), 3)
         achieved = bytes_step_gpu / (enc_ms * 1e-3) / GB
@@ -379,6 +555,47 @@ def main() -> None:
     if sha_note:
         out["sha256"] = sha_note
 
+    def gather_leg(run_verify_plan, reps=5) -> dict:
+        """Time the degraded read (survivor gather over the process group + rebuild) alone,
+        synchronised per rep, max over ranks; verify the rebuilt fragments."""
+        run, verify, plan = run_verify_plan
+        times = []
+        res = None
+        for _ in range(reps + 1):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            res = run()
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            times.append(time.perf_counter() - t0)
+        t = float(np.median(times[1:]))
+        ok = verify(res)
+        v = torch.tensor([t, 0.0 if ok else 1.0], dtype=torch.float64,
+                         device=dev if (world == 1 or backend == "nccl") else "cpu")
+        if world > 1:
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        t, bad = float(v[0]), bool(v[1])
+        nrebuilt = len(plan.lost)
+        return {"segments": nrebuilt, "lost_per_segment": 1,
+                "placement": "fragment f of segment s on GPU (s + f) mod N "
+                             "(c-pallets/file-bank/src/functions.rs:187-283)",
+                "gather_bytes": plan.bytes_moved, "seconds": round(t, 5),
+                "gather_GBps": round(plan.bytes_moved / t / GB, 2) if plan.bytes_moved else None,
+                "rebuilt_GBps": round(nrebuilt * (k + 1) * F / t / GB, 2),
+                "xgmi_GBps_per_link": 153,
+                "backend": (backend if world > 1 else "local (one GPU: no bytes move)"),
+                "bit_exact": not bad}
+
+    if args.config == 4:
+        out["degraded_gather"] = gather_leg(gather)
+    elif world > 1 and not args.no_extra and args.config == 2:
+        # config 4's exchange step measured in the default (scaling) run as well
+        out.setdefault("extra", {})["degraded_gather"] = gather_leg(
+            degraded_gather(enc, k, m, F, world, rank, dev, 64))
+
     if not args.no_extra and args.config == 2:
         # decode rate in the same process (BASELINE config 3 workload, same bytes)
         pres = np.ones((nseg, k + m), np.uint8)
@@ -392,11 +609,14 @@ def main() -> None:
         b.record(stream)
         torch.cuda.synchronize(dev)
         dms = a.elapsed_time(b) / 20
-        out["extra"] = {"reconstruct_GBps_per_gpu": round(bytes_step_gpu / (dms * 1e-3) / GB, 2),
-                        "reconstruct_ms": round(dms, 4)}
+        out.setdefault("extra", {}).update(
+            {"reconstruct_GBps_per_gpu": round(bytes_step_gpu / (dms * 1e-3) / GB, 2),
+             "reconstruct_ms": round(dms, 4)})
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(k, m, F, args.cpu_seconds)
+        if args.config == 5:
+            out["cpu_baseline"]["sha256"] = cpu_sha256(k, m, F, args.cpu_seconds / 2)
 
     if world > 1:
         dist.barrier()

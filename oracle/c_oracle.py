@@ -31,6 +31,8 @@ def load_c_oracle():
                                          c_int, c_int]
         lib.orc_encode_batch.restype = c_double
         lib.orc_set_simd.argtypes = [c_int]
+        lib.orc_segment_ops.argtypes = [c_int, c_int, POINTER(c_void_p), c_size_t, c_int, c_int]
+        lib.orc_segment_ops.restype = c_double
         _lib = lib
     return _lib
 

@@ -12,8 +12,10 @@
  *     version-unpinned: GF(2^8)/0x11D, E = V * inv(V[:k]), V[r][c] = r^c;
  *   - SHA-256: FIPS 180-4 (readable restatement in the reference at
  *     utils/ring/src/digest/sha2.rs:46-145); vectors utils/ring/third_party/NIST/SHAVS.
- * Encode uses one 256-entry product table per coefficient (scalar) or the split-nibble
- * pshufb form (AVX2, when the host has it); both are checked against each other in tests.
+ * Encode uses one 256-entry product table per coefficient (scalar), the split-nibble pshufb
+ * form (AVX2), or one GF(2) affine transform per coefficient (AVX-512BW + GFNI
+ * vgf2p8affineqb: multiplication by a constant c is GF(2)-linear, an 8x8 bit matrix); the
+ * best the host has by default, all checked against each other in tests.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -136,14 +138,45 @@ __attribute__((target("avx2"))) static void mul_acc_avx2(uint8_t* out, const uin
 }
 #endif
 
-static int g_simd = -1; /* -1 auto, 0 scalar, 1 avx2 */
+#if defined(__x86_64__)
+/* The 8x8 GF(2) matrix of x -> c*x in vgf2p8affineqb's layout: result bit i is the parity of
+ * (x AND matrix byte 7-i), so byte 7-i holds the input bits j whose product c * 2^j has bit i. */
+static uint64_t affine_matrix(uint8_t c) {
+  uint64_t a = 0;
+  for (int i = 0; i < 8; ++i) {
+    unsigned row = 0;
+    for (int j = 0; j < 8; ++j)
+      if (g_mul[c][1u << j] >> i & 1) row |= 1u << j;
+    a |= (uint64_t)row << (8 * (7 - i));
+  }
+  return a;
+}
+
+__attribute__((target("avx512f,avx512bw,gfni"))) static void mul_acc_gfni(
+    uint8_t* out, const uint8_t* in, uint8_t c, size_t len, int first) {
+  const __m512i A = _mm512_set1_epi64((long long)affine_matrix(c));
+  size_t i = 0;
+  for (; i + 64 <= len; i += 64) {
+    __m512i p = _mm512_gf2p8affine_epi64_epi8(_mm512_loadu_si512((const void*)(in + i)), A, 0);
+    if (!first) p = _mm512_xor_si512(p, _mm512_loadu_si512((const void*)(out + i)));
+    _mm512_storeu_si512((void*)(out + i), p);
+  }
+  if (i < len) mul_acc_scalar(out + i, in + i, c, len - i, first);
+}
+#endif
+
+static int g_simd = -1; /* -1 auto, 0 scalar, 1 avx2, 2 avx512bw + gfni */
 
 int orc_set_simd(int v) {
   gf_init();
 #if defined(__x86_64__)
-  if (v < 0) v = __builtin_cpu_supports("avx2") ? 1 : 0;
+  const int have_gfni = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("gfni");
+  const int have_avx2 = __builtin_cpu_supports("avx2");
+  if (v < 0) v = have_gfni ? 2 : have_avx2 ? 1 : 0;
+  if (v == 2 && !have_gfni) v = have_avx2 ? 1 : 0;
+  if (v == 1 && !have_avx2) v = 0;
 #else
-  if (v != 0) v = 0;
+  v = 0;
 #endif
   g_simd = v;
   return g_simd;
@@ -152,6 +185,10 @@ int orc_set_simd(int v) {
 static void mul_acc(uint8_t* out, const uint8_t* in, uint8_t c, size_t len, int first) {
   if (g_simd < 0) orc_set_simd(-1);
 #if defined(__x86_64__)
+  if (g_simd == 2) {
+    mul_acc_gfni(out, in, c, len, first);
+    return;
+  }
   if (g_simd == 1) {
     mul_acc_avx2(out, in, c, len, first);
     return;
@@ -347,5 +384,55 @@ double orc_encode_batch(int k, int m, const uint8_t* data, uint8_t* parity, size
   free(th);
   free(jobs);
   free(e);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ---- one segment on all threads (config 1: single-segment CPU encode + reconstruct) ------- */
+typedef struct {
+  int k, m, op; /* op -1: encode; e >= 0: reconstruct shard e from the others */
+  uint8_t* const* shards;
+  size_t len, c0, c1;
+} seg_job_t;
+
+static void* seg_worker(void* arg) {
+  seg_job_t* j = (seg_job_t*)arg;
+  uint8_t* sh[256];
+  for (int i = 0; i < j->k + j->m; ++i) sh[i] = j->shards[i] + j->c0;
+  const size_t n = j->c1 - j->c0;
+  if (n == 0) return NULL;
+  if (j->op < 0) {
+    orc_encode(j->k, j->m, (const uint8_t* const*)sh, sh + j->k, n);
+  } else {
+    uint8_t present[256];
+    for (int i = 0; i < j->k + j->m; ++i) present[i] = i != j->op;
+    orc_reconstruct(j->k, j->m, sh, present, n, 0);
+  }
+  return NULL;
+}
+
+/* `reps` x (encode + every single-erasure reconstruct, shard e rebuilt in place from the
+ * others) of one segment's k+m shards of `len` bytes, columns split over `threads` threads.
+ * Returns wall seconds. Bytes per op = (k+m)*len (k read + 1 or m written, RS(2,1)). */
+double orc_segment_ops(int k, int m, uint8_t* const* shards, size_t len, int threads, int reps) {
+  gf_init();
+  if (threads < 1) threads = 1;
+  pthread_t* th = (pthread_t*)calloc(threads, sizeof(pthread_t));
+  seg_job_t* jobs = (seg_job_t*)calloc(threads, sizeof(seg_job_t));
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int r = 0; r < reps; ++r)
+    for (int op = -1; op < k + m; ++op) {
+      for (int t = 0; t < threads; ++t) {
+        /* 64-byte aligned column ranges */
+        size_t c0 = (len * t / threads) & ~(size_t)63, c1 = (len * (t + 1) / threads) & ~(size_t)63;
+        if (t == threads - 1) c1 = len;
+        jobs[t] = (seg_job_t){k, m, op, shards, len, c0, c1};
+        pthread_create(&th[t], NULL, seg_worker, &jobs[t]);
+      }
+      for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+    }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  free(th);
+  free(jobs);
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }

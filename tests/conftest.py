@@ -30,7 +30,7 @@ def orc():
 @pytest.fixture(scope="session")
 def corc():
     """C oracle (test infrastructure), built on demand."""
-    from tests.oracle_c import load_c_oracle
+    from oracle.c_oracle import load_c_oracle
     return load_c_oracle()
 
 

@@ -1,9 +1,10 @@
 /* C consumer of libcessec's host pipeline (cec_pipeline_*, include/cess_ec.h only): what a
  * cgo / FFI binding drives to encode a file from host memory. A synthetic source (splitmix64
  * segments, repeated every `uniq` segments) is read by an 8-thread memcpy callback; sampled
- * segments' parity and SegmentList hashes are checked against the C oracle (linked separately,
- * test infrastructure). Prints one JSON line with the end-to-end rate (PCIe-inclusive: H2D of
- * the data, D2H of the parity, hashes on the GPU).
+ * segments' shards and SegmentList hashes are stashed by the callbacks and checked against the
+ * C oracle (linked separately, test infrastructure) after the timed run. Prints one JSON line
+ * with the end-to-end rate (PCIe-inclusive: H2D of the data, D2H of the parity, hashes on the
+ * GPU).
  * usage: pipeline_e2e k m F nseg batch depth hash window [uniq] [check_every]
  * build: gcc -O2 -pthread tests/native/pipeline_e2e.c -Iinclude -Lcess_amd -lcessec
  *            -Loracle/build -loracle -Wl,-rpath,... -o pipeline_e2e */
@@ -22,8 +23,17 @@ void orc_fill_synthetic(unsigned char* out, size_t seg_bytes, size_t nseg, uint6
                         uint64_t seed);
 
 typedef struct {
+  uint64_t seg;
+  unsigned char* shards; /* (k + m) * F */
+  unsigned char hex[64 * 257];
+  int have_hex;
+} sample_t;
+
+typedef struct {
   int k, m;
   size_t F, SB, nseg, uniq, check_every;
+  sample_t* samples;
+  size_t nsamples;
   unsigned char* src; /* uniq segments */
   size_t pos, total;  /* source bytes handed out, source size */
   uint64_t frags_seen, recs_seen, checked, bad;
@@ -73,6 +83,16 @@ static const unsigned char* src_shard(ctx_t* x, uint64_t seg, int j) {
   return x->src + (seg % x->uniq) * x->SB + (size_t)j * x->F;
 }
 
+static int sampled(ctx_t* x, uint64_t seg) {
+  return seg % x->check_every == 0 || seg == x->nseg - 1;
+}
+
+static sample_t* sample_of(ctx_t* x, uint64_t seg) {
+  for (size_t i = 0; i < x->nsamples; ++i)
+    if (x->samples[i].seg == seg) return &x->samples[i];
+  return NULL;
+}
+
 static int on_frags(void* user, uint64_t seg, const uint8_t* const* shards, size_t shard_len) {
   ctx_t* x = (ctx_t*)user;
   if (seg != x->next_frag++ || shard_len != x->F) {
@@ -80,8 +100,18 @@ static int on_frags(void* user, uint64_t seg, const uint8_t* const* shards, size
     return 0;
   }
   x->frags_seen++;
-  if (seg % x->check_every && seg != x->nseg - 1) return 0;
-  /* data shards pass through; parity equals the oracle's (the last segment may be padded) */
+  if (!sampled(x, seg)) return 0;
+  sample_t* s = &x->samples[x->nsamples++];
+  s->seg = seg;
+  s->have_hex = 0;
+  s->shards = malloc((size_t)(x->k + x->m) * x->F);
+  for (int i = 0; i < x->k + x->m; ++i) memcpy(s->shards + (size_t)i * x->F, shards[i], x->F);
+  return 0;
+}
+
+/* after the run: data shards = the source (zero-padded tail), parity = the oracle's */
+static void check_frags(ctx_t* x, sample_t* sm) {
+  const uint64_t seg = sm->seg;
   const size_t real = (seg + 1) * x->SB <= x->total ? x->SB : x->total - seg * x->SB;
   unsigned char* d[256];
   unsigned char* p[256];
@@ -89,17 +119,16 @@ static int on_frags(void* user, uint64_t seg, const uint8_t* const* shards, size
     d[j] = calloc(1, x->F);
     size_t off = (size_t)j * x->F;
     if (off < real) memcpy(d[j], src_shard(x, seg, j), real - off < x->F ? real - off : x->F);
-    if (memcmp(d[j], shards[j], x->F)) x->bad++;
+    if (memcmp(d[j], sm->shards + (size_t)j * x->F, x->F)) x->bad++;
   }
   for (int j = 0; j < x->m; ++j) p[j] = malloc(x->F);
   orc_encode(x->k, x->m, (const unsigned char* const*)d, p, x->F);
   for (int j = 0; j < x->m; ++j) {
-    if (memcmp(p[j], shards[x->k + j], x->F)) x->bad++;
+    if (memcmp(p[j], sm->shards + (size_t)(x->k + j) * x->F, x->F)) x->bad++;
     free(p[j]);
   }
   for (int j = 0; j < x->k; ++j) free(d[j]);
   x->checked++;
-  return 0;
 }
 
 static int on_rec(void* user, uint64_t seg, const uint8_t* seg_hex, const uint8_t* frag_hex) {
@@ -109,25 +138,32 @@ static int on_rec(void* user, uint64_t seg, const uint8_t* seg_hex, const uint8_
     return 0;
   }
   x->recs_seen++;
-  if (seg % x->check_every && seg != x->nseg - 1) return 0;
-  const size_t real = (seg + 1) * x->SB <= x->total ? x->SB : x->total - seg * x->SB;
-  unsigned char* segbuf = calloc(1, x->SB);
-  memcpy(segbuf, src_shard(x, seg, 0), real);
-  char h[64];
-  orc_sha256_hex(segbuf, x->SB, h);
-  if (memcmp(h, seg_hex, 64)) x->bad++;
-  unsigned char* p[256];
-  const unsigned char* d[256];
-  for (int j = 0; j < x->k; ++j) d[j] = segbuf + (size_t)j * x->F;
-  for (int j = 0; j < x->m; ++j) p[j] = malloc(x->F);
-  orc_encode(x->k, x->m, d, p, x->F);
-  for (int i = 0; i < x->k + x->m; ++i) {
-    orc_sha256_hex(i < x->k ? d[i] : p[i - x->k], x->F, h);
-    if (memcmp(h, frag_hex + 64 * i, 64)) x->bad++;
+  if (!sampled(x, seg)) return 0;
+  sample_t* s = sample_of(x, seg);
+  if (!s) {  /* on_fragments of a segment always precedes its on_record */
+    x->bad++;
+    return 0;
   }
-  for (int j = 0; j < x->m; ++j) free(p[j]);
-  free(segbuf);
+  memcpy(s->hex, seg_hex, 64);
+  memcpy(s->hex + 64, frag_hex, 64 * (size_t)(x->k + x->m));
+  s->have_hex = 1;
   return 0;
+}
+
+/* after the run: SegmentList hashes = SHA-256 hex of the oracle's segment and fragments */
+static void check_rec(ctx_t* x, sample_t* sm) {
+  if (!sm->have_hex) {
+    x->bad++;
+    return;
+  }
+  char h[64];
+  unsigned char* segbuf = sm->shards; /* the k data shards are the zero-padded segment */
+  orc_sha256_hex(segbuf, x->SB, h);
+  if (memcmp(h, sm->hex, 64)) x->bad++;
+  for (int i = 0; i < x->k + x->m; ++i) {
+    orc_sha256_hex(segbuf + (size_t)i * x->F, x->F, h);
+    if (memcmp(h, sm->hex + 64 * (i + 1), 64)) x->bad++;
+  }
 }
 
 int main(int argc, char** argv) {
@@ -156,6 +192,7 @@ int main(int argc, char** argv) {
   x.SB = (size_t)x.k * x.F;
   x.total = x.nseg * x.SB - tail;
   x.src = malloc(x.uniq * x.SB);
+  x.samples = calloc(x.nseg / x.check_every + 2, sizeof(sample_t));
   orc_fill_synthetic(x.src, x.SB, x.uniq, 0, 0xCE550004ull);
 
   cec_codec* c = NULL;
@@ -169,6 +206,11 @@ int main(int argc, char** argv) {
   if (rc) {
     fprintf(stderr, "run: %d %s\n", rc, cec_last_error());
     return 1;
+  }
+  for (size_t i = 0; i < x.nsamples; ++i) { /* checks outside the timed run */
+    check_frags(&x, &x.samples[i]);  /* parity checked first, so the hashes below use it */
+    if (o.hash) check_rec(&x, &x.samples[i]);
+    free(x.samples[i].shards);
   }
   const int ok = x.bad == 0 && x.frags_seen == x.nseg && (!o.hash || x.recs_seen == x.nseg) &&
                  st.segments == x.nseg && st.bytes_in == x.total;

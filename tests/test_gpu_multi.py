@@ -1,0 +1,76 @@
+"""Multi-GPU degraded read over RCCL (BASELINE config 4's exchange step): two or more ranks, one
+process per GPU, backend "nccl" (= RCCL over xGMI). Survivors of each segment are gathered on the
+lost fragment's home GPU (fragment f of segment s on GPU (s + f) mod G,
+c-pallets/file-bank/src/functions.rs:187-283) and rebuilt by libcessec; every rebuilt fragment is
+compared with the C oracle's. Skips cleanly when fewer than two GPUs are visible (the same path
+is covered on CPU by tests/test_distributed.py with gloo)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, k, m, nseg, F, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch
+    import torch.distributed as dist
+    import cess_amd
+    from cess_amd import distributed as D
+    from oracle.c_oracle import c_encode, load_c_oracle
+    torch.cuda.set_device(rank)
+    dev = torch.device("cuda", rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    corc = load_c_oracle()
+    n = k + m
+    rng = np.random.default_rng(7)  # same on every rank: every codeword known to all
+    full = []
+    for s in range(nseg):
+        data = [rng.integers(0, 256, F, dtype=np.uint8) for _ in range(k)]
+        full.append(data + c_encode(corc, k, m, data))
+    mine = D.local_fragments(nseg, n, world, rank)
+    store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
+                            torch.from_numpy(np.stack([full[s][f] for s, f in mine])).to(dev))
+    lost = {s: sorted(rng.choice(n, size=1 + s % m, replace=False).tolist()) for s in range(nseg)}
+    plan = D.plan_gather(lost, k, m, world, F)
+    out = D.degraded_read(plan, store, cess_amd.New(k, m, device=rank), rank)
+    torch.cuda.synchronize(dev)
+    ok = all(np.array_equal(t.cpu().numpy(), full[s][f]) for (s, f), t in out.items())
+    q.put((rank, ok, len(out), plan.bytes_moved))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (4, 2)])
+def test_degraded_read_rccl(k, m):
+    import torch
+    import torch.multiprocessing as mp
+    world = min(torch.cuda.device_count(), 4)
+    if world < 2:
+        pytest.skip("RCCL degraded read needs >= 2 visible GPUs")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    nseg, F = 12, 1 << 20
+    procs = [ctx.Process(target=_rank, args=(r, world, port, k, m, nseg, F, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _, _ in res), res
+    assert sum(n for _, _, n, _ in res) == sum(1 + s % m for s in range(nseg))
+    assert res[0][3] > 0  # survivors crossed GPUs

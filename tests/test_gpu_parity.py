@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from tests.conftest import case_data, parse_shavs
-from tests.oracle_c import c_encode, ptrs
+from oracle.c_oracle import c_encode, ptrs
 
 pytestmark = pytest.mark.gpu
 
@@ -610,3 +610,45 @@ def test_back_to_back_plans_on_side_stream(torch, cess, corc):
     for present, d_data, d_par in calls:
         assert np.array_equal(d_data.cpu().numpy(), data)
         assert np.array_equal(d_par.cpu().numpy(), par)
+
+
+def test_full_geometry_config4_64gib(torch, cess, corc):
+    """BASELINE config 4 at world 1: the 64 GiB file (4096 x 16 MiB segments) encoded in one
+    batch in HBM (64 GiB data + 32 GiB parity); 8 sampled segments against the C oracle, then
+    the round-trip property on every segment: erase fragment s mod 3 of each, rebuild all 4096
+    in one per-segment call, compare with the erased originals (kept in HBM)."""
+    k, m, F, nseg = 2, 1, 8 * MiB, 4096
+    free, _ = torch.cuda.mem_get_info()
+    if free < (140 << 30):
+        pytest.skip(f"needs ~140 GiB of free HBM, {free >> 30} GiB free")
+    d_data = torch.empty((nseg, k, F), dtype=torch.uint8, device="cuda")
+    d_par = torch.empty((nseg, m, F), dtype=torch.uint8, device="cuda")
+    cess.fill_synthetic(d_data, k * F, nseg, 0, 0xCE550004)
+    enc = cess.New(k, m)
+    enc.EncodeBatch(d_data, d_par, nseg, F)
+    torch.cuda.synchronize()
+    sample = [0, 1, 777, 1500, 2048, 3001, 4094, 4095]
+    host = d_data[sample].cpu().numpy()
+    want = np.zeros((len(sample), m, F), np.uint8)
+    corc.orc_encode_batch(k, m, host.ctypes.data, want.ctypes.data, len(sample), F, 8, 1)
+    assert np.array_equal(d_par[sample].cpu().numpy(), want)
+    # keep the fragment each segment loses (32 GiB), erase it, rebuild everything at once
+    seg = torch.arange(nseg, device="cuda")
+    lost = seg % 3
+    keep = torch.empty((nseg, F), dtype=torch.uint8, device="cuda")
+    for e in range(3):
+        idx = seg[lost == e]
+        src = d_data[idx, e] if e < k else d_par[idx, e - k]
+        keep[idx] = src
+        if e < k:
+            d_data[idx, e] = 0
+        else:
+            d_par[idx, e - k] = 0
+    present = np.ones((nseg, k + m), np.uint8)
+    present[np.arange(nseg), np.arange(nseg) % 3] = 0
+    enc.ReconstructBatch(d_data, d_par, nseg, F, present)
+    torch.cuda.synchronize()
+    for e in range(3):
+        idx = seg[lost == e]
+        got = d_data[idx, e] if e < k else d_par[idx, e - k]
+        assert torch.equal(got, keep[idx]), e

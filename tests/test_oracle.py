@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from tests.conftest import case_data, parse_shavs
-from tests.oracle_c import c_encode, c_sha256_hex, ptrs
+from oracle.c_oracle import c_encode, c_sha256_hex, ptrs
 
 
 def test_galois_kats(orc, golden):
@@ -157,11 +157,29 @@ def test_synthetic_generator_pinned(orc, corc, golden):
     assert buf.tobytes() == want
 
 
-def test_c_simd_matches_scalar(corc):
-    rng = np.random.default_rng(5)
-    data = [rng.integers(0, 256, 4099, dtype=np.uint8) for _ in range(4)]
+@pytest.mark.parametrize("k,m", [(4, 3), (2, 1), (32, 32)])
+def test_c_simd_matches_scalar(corc, k, m):
+    """Scalar table, AVX2 split-nibble and AVX-512 GFNI affine forms of the C oracle agree
+    (each form the host lacks falls back, so the comparison is against what runs)."""
+    rng = np.random.default_rng(5 + k)
+    data = [rng.integers(0, 256, 4099, dtype=np.uint8) for _ in range(k)]
     corc.orc_set_simd(0)
-    a = c_encode(corc, 4, 3, data)
+    a = c_encode(corc, k, m, data)
+    for mode in (1, 2, -1):
+        got = corc.orc_set_simd(mode)
+        b = c_encode(corc, k, m, data)
+        assert all(np.array_equal(x, y) for x, y in zip(a, b)), (mode, got)
     corc.orc_set_simd(-1)
-    b = c_encode(corc, 4, 3, data)
-    assert all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+def test_c_segment_ops_threaded(corc):
+    """orc_segment_ops (config 1's CPU leg): encode + every single-erasure rebuild of one segment
+    split over threads leaves the shards a consistent codeword."""
+    from oracle.c_oracle import ptrs
+    k, m, F = 2, 1, (1 << 16) + 40
+    rng = np.random.default_rng(11)
+    data = [rng.integers(0, 256, F, dtype=np.uint8) for _ in range(k)]
+    want = data + c_encode(corc, k, m, data)
+    sh = [d.copy() for d in data] + [np.zeros(F, np.uint8)]
+    corc.orc_segment_ops(k, m, ptrs(sh), F, 5, 2)
+    assert all(np.array_equal(x, y) for x, y in zip(sh, want))
