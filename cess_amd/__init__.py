@@ -4,7 +4,7 @@ The compute path is libcessec (HIP kernels for gfx950 behind the C ABI in includ
 this package is the host-side mirror of the off-chain codec API (klauspost/reedsolomon shape)
 plus the CESS segment / fragment records.
 """
-from . import geometry, records
+from . import audit, geometry, records
 from .hashq import HashQueue, sha256_blocks
 from .records import ErrTooManySegments
 from .reedsolomon import (
@@ -27,5 +27,5 @@ __all__ = [
     "geometry", "CecError", "Encoder", "New", "ErrInvShardNum", "ErrMaxShardNum",
     "ErrReconstructRequired", "ErrShardNoData", "ErrShardSize", "ErrShortData",
     "ErrTooFewShards", "HipError", "fill_synthetic", "sha256_hex_device", "HashQueue",
-    "sha256_blocks", "records", "ErrTooManySegments",
+    "sha256_blocks", "records", "ErrTooManySegments", "audit",
 ]

@@ -69,6 +69,10 @@ SIGNATURES = {
     "cec_pipeline_destroy": (None, [c_void_p]),
     "cec_pipeline_run": (c_int, [c_void_p, READ_FN, FRAGMENTS_FN, RECORD_FN, c_void_p,
                                  POINTER(PipelineStats)]),
+    "cec_challenge_indices": (c_int, [POINTER(c_uint64), c_size_t, c_uint32, c_uint32,
+                                      POINTER(c_uint32), POINTER(c_size_t)]),
+    "cec_audit_chunks": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_uint32,
+                                 POINTER(c_uint32), c_uint32, c_void_p, c_void_p, c_void_p]),
     "cec_scale_compact": (c_int, [c_uint32, c_void_p, c_size_t, POINTER(c_size_t)]),
     "cec_scale_deal_info": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t,
                                     POINTER(c_size_t)]),
@@ -90,6 +94,7 @@ CEC_ESHORTDATA = -7
 CEC_ENODEV = -8
 CEC_ESEGCOUNT = -9
 CEC_ECALLBACK = -10
+CEC_CHUNK_COUNT = 1024
 CEC_SEGMENT_COUNT = 1000
 CEC_FRAGMENT_COUNT = 3
 

@@ -832,6 +832,82 @@ int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t s
   return check_launch();
 }
 
+// ---- storage audit chunks -----------------------------------------------------------------
+
+int cec_challenge_indices(const uint64_t* randoms, size_t nrand, uint32_t chunk_count,
+                          uint32_t need, uint32_t* out, size_t* used) {
+  if ((nrand && !randoms) || (need && !out)) return set_err(CEC_EINVAL, "null");
+  if (chunk_count == 0 || need > chunk_count)
+    return set_err(CEC_EINVAL, "need must be <= chunk_count, chunk_count > 0");
+  // c-pallets/audit/src/lib.rs:955-964
+  uint32_t got = 0;
+  size_t i = 0;
+  for (; i < nrand && got < need; ++i) {
+    const uint32_t idx = (uint32_t)(randoms[i] % chunk_count);
+    bool seen = false;
+    for (uint32_t q = 0; q < got && !seen; ++q) seen = out[q] == idx;
+    if (!seen) out[got++] = idx;
+  }
+  if (used) *used = i;
+  if (got < need) return set_err(CEC_EINVAL, "random stream exhausted before `need` indices");
+  return CEC_OK;
+}
+
+int cec_audit_chunks(cec_codec* c, const uint8_t* d_data, const uint8_t* d_parity, size_t nseg,
+                     size_t shard_len, uint32_t chunk_count, const uint32_t* indices,
+                     uint32_t nidx, uint8_t* d_chunks, uint8_t* d_hex, void* hip_stream) {
+  if (!c || !indices || (nseg && !d_data) || (!d_chunks && !d_hex))
+    return set_err(CEC_EINVAL, "null");
+  if (chunk_count == 0 || shard_len == 0 || shard_len % chunk_count)
+    return set_err(CEC_ESHARDLEN, "shard_len must be a nonzero multiple of chunk_count");
+  for (uint32_t j = 0; j < nidx; ++j)
+    if (indices[j] >= chunk_count) return set_err(CEC_EINVAL, "chunk index out of range");
+  if (nseg == 0 || nidx == 0) return CEC_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = pick_stream(c, hip_stream);
+  const int nsh = d_parity ? c->k + c->m : c->k;
+  const uint64_t nfrag = (uint64_t)nseg * nsh;
+  const uint64_t chunk = shard_len / chunk_count;
+  Layout L = batch_layout(c, d_data, d_parity, shard_len);
+  void* d_idx = nullptr;
+  int rc = c->pool.alloc(nidx * sizeof(uint32_t), &d_idx);
+  if (rc) return rc;
+  const size_t idx_bytes = nidx * sizeof(uint32_t);
+  hipError_t e = hipMemcpyAsync(d_idx, indices, idx_bytes, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    c->pool.retire(d_idx, idx_bytes);
+    return set_err(CEC_EHIP, std::string("index upload: ") + hipGetErrorString(e));
+  }
+  void* scratch = nullptr;
+  const size_t gbytes = nfrag * nidx * chunk;
+  if (!d_chunks) {
+    rc = c->pool.alloc(gbytes, &scratch);
+    if (rc) {
+      c->pool.retire(d_idx, idx_bytes);
+      return rc;
+    }
+    d_chunks = static_cast<uint8_t*>(scratch);
+  }
+  cec::launch_chunk_gather(L, nsh, nfrag, static_cast<const uint32_t*>(d_idx), nidx, chunk,
+                           d_chunks, st);
+  rc = check_launch();
+  if (!rc && d_hex) {
+    Layout G{};  // the gathered chunks as nfrag * nidx one-shard "segments"
+    G.data = d_chunks;
+    G.len = chunk;
+    G.shard_stride = chunk;
+    G.data_seg_stride = chunk;
+    G.k = 1;
+    cec::launch_sha256_hex(c->opts.sha_mode, nullptr, &G, 1, nfrag * nidx, chunk, d_hex, st);
+    rc = check_launch();
+  }
+  const int mrc = c->pool.mark(st);  // the index array and scratch stay until these complete
+  c->pool.retire(d_idx, idx_bytes);
+  if (scratch) c->pool.retire(scratch, gbytes);
+  return rc ? rc : mrc;
+}
+
 // ---- host-buffer API -------------------------------------------------------------------
 
 int cec_encode(cec_codec* c, uint8_t* const* shards, size_t shard_len) {

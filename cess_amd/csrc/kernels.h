@@ -120,6 +120,11 @@ void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
 void launch_sha256_tick(int tick_mode, ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,
                         uint32_t max_blocks, uint64_t live, hipStream_t st);
 
+// Audit chunk gather (audit.hip): chunk idx[j] (chunk_len bytes) of fragment f, fragments in
+// batch order (f = seg * nshards + shard, shards of layout L), to out[(f * nidx + j) * chunk_len].
+void launch_chunk_gather(const Layout& L, int nshards, uint64_t nfrag, const uint32_t* d_idx,
+                         uint32_t nidx, uint64_t chunk_len, uint8_t* out, hipStream_t st);
+
 // Synthetic segment bytes: 64-bit word w of segment s = splitmix64(seed ^ (s << 32) ^ w),
 // little-endian; segments are seg_bytes long and contiguous from `out`.
 void launch_fill_splitmix(uint8_t* out, uint64_t seg_bytes, uint64_t nseg, uint64_t seg0,

@@ -73,6 +73,11 @@ def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
     moved = 0
     for s in sorted(lost):
         erased = set(lost[s])
+        if not erased:
+            continue  # nothing lost: no decoder, no moves
+        bad = [f for f in erased if not 0 <= f < n]
+        if bad:
+            raise ValueError(f"segment {s}: fragment indices {bad} outside 0..{n - 1}")
         if len(erased) > m:
             raise ValueError(f"segment {s}: {len(erased)} erasures > m = {m}")
         dec = fragment_owner(s, min(erased), world)
@@ -86,7 +91,8 @@ def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
             moves[(s, f)] = (src, dec)
             if src != dec:
                 moved += frag_bytes
-    return GatherPlan(segs, moves, present, {s: sorted(set(v)) for s, v in lost.items()}, moved)
+    return GatherPlan(segs, moves, present, {s: sorted(set(v)) for s, v in lost.items() if v},
+                      moved)
 
 
 def gather_survivors(plan: GatherPlan, store: FragmentStore, k: int, m: int, rank: int,

@@ -190,6 +190,30 @@ void cec_pipeline_destroy(cec_pipeline* p);
 int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_fragments,
                      cec_record_fn on_record, void* user, cec_pipeline_stats* stats);
 
+/* ---- storage audit chunks ---------------------------------------------
+ * A fragment is CHUNK_COUNT = 1024 chunks (primitives/common/src/lib.rs:62): 8 KiB chunks of an
+ * 8 MiB fragment. A challenge names need = CHUNK_COUNT * 46 / 1000 = 47 distinct chunk indices
+ * (NetSnapShot.random_index_list, c-pallets/audit/src/types.rs:21), drawn by
+ * c-pallets/audit/src/lib.rs:955-964 from the chain's randomness: for seed = 1, 2, ...,
+ * index = random_number(seed) % CHUNK_COUNT, repeats skipped. The PoDR2 tag arithmetic over the
+ * chunks runs in the TEE and is not in the reference (unpinned, not provided). */
+#define CEC_CHUNK_COUNT 1024
+#define CEC_CHALLENGE_NEED (CEC_CHUNK_COUNT * 46 / 1000)
+/* The selection loop over a given random stream: randoms[i] = random_number(seed i + 1) (the
+ * chain's randomness, decoded as u64). Writes `need` indices; *used = randoms consumed.
+ * CEC_EINVAL when the stream runs out first. Host only. */
+int cec_challenge_indices(const uint64_t* randoms, size_t nrand, uint32_t chunk_count,
+                          uint32_t need, uint32_t* out, size_t* used);
+/* Gather chunks indices[0..nidx) of every fragment of an HBM batch ([nseg][k][shard_len] data,
+ * [nseg][m][shard_len] parity; d_parity NULL: data fragments only) into d_chunks
+ * [nfrag][nidx][chunk] (fragments in batch order, seg * (k+m) + shard), chunk = shard_len /
+ * chunk_count, and/or the SHA-256 hex of each gathered chunk into d_hex [nfrag][nidx][64].
+ * Either output may be NULL (not both). Enqueued on hip_stream. */
+int cec_audit_chunks(cec_codec* codec, const uint8_t* d_data, const uint8_t* d_parity,
+                     size_t nseg, size_t shard_len, uint32_t chunk_count,
+                     const uint32_t* indices, uint32_t nidx, uint8_t* d_chunks, uint8_t* d_hex,
+                     void* hip_stream);
+
 /* ---- on-chain records (host only, no GPU) ---------------------------------------------------
  * SCALE bytes of what the codec's outputs become on chain:
  *   FileBank::upload_declaration(file_hash: Hash, deal_info: BoundedVec<SegmentList,

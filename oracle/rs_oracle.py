@@ -284,3 +284,28 @@ def synthetic_segment(seed: int, seg: int, nbytes: int) -> np.ndarray:
     w = np.arange(nbytes // 8, dtype=np.uint64)
     words = splitmix64(np.uint64(seed) ^ (np.uint64(seg) << np.uint64(32)) ^ w)
     return words.astype("<u8").view(np.uint8)
+
+
+# ---- storage audit (c-pallets/audit) -----------------------------------------------------------
+def challenge_indices(randoms, chunk_count=1024, need=1024 * 46 // 1000):
+    """generation_challenge's chunk selection (c-pallets/audit/src/lib.rs:955-964): for seed =
+    1, 2, ..., random_index = random_number(seed) % CHUNK_COUNT, kept if new, until `need`
+    indices. `randoms[i]` = random_number(i + 1). Returns (indices, randoms consumed)."""
+    out = []
+    used = 0
+    for r in randoms:
+        if len(out) >= need:
+            break
+        used += 1
+        idx = int(r) % chunk_count
+        if idx not in out:
+            out.append(idx)
+    if len(out) < need:
+        raise ValueError("random stream exhausted")
+    return out, used
+
+
+def chunk(fragment, index, chunk_count=1024):
+    """Chunk `index` of a fragment: CHUNK_COUNT equal chunks (primitives/common/src/lib.rs:62)."""
+    n = len(fragment) // chunk_count
+    return fragment[index * n:(index + 1) * n]

@@ -43,6 +43,11 @@ def test_plan_gather_counts():
     assert plan.bytes_moved == 64 * k * F
     with pytest.raises(ValueError):
         D.plan_gather({0: [0, 1]}, k, m, G, F)
+    with pytest.raises(ValueError):
+        D.plan_gather({0: [3]}, k, m, G, F)  # index outside 0..k+m-1
+    # a segment with nothing lost is skipped (no decoder, no moves)
+    p2 = D.plan_gather({0: [], 1: [2]}, k, m, G, F)
+    assert list(p2.lost) == [1] and len(p2.moves) == k
 
 
 def _worker(rank, world, port, k, m, nseg, F, q):
