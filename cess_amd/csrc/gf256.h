@@ -172,4 +172,48 @@ constexpr int gf_decode_plan(int k, int m, const uint8_t* present, bool data_onl
   return 0;
 }
 
+// ---- additive FFT over the subspace of the first 2^K field elements -------------------------
+// RS(2^K, 2^K) in this convention has data = f(0..2^K-1) and parity i = f(2^K + i) for the
+// unique f of degree < 2^K (E = V * inv(V_top), V[r][c] = r^c). The points 0..2^K-1 are the
+// GF(2)-span of the basis v_i = 2^i (the integers XOR-combine like field elements), and
+// 2^K + i = 2^K ^ i is its coset by beta = 2^K. So encode = the Lin-Chung-Han additive IFFT
+// over the subspace (data -> coefficients of f in the novel polynomial basis) followed by the
+// FFT over the coset (coefficients -> parity): the same bytes as the matrix product, since f is
+// unique. Skew of layer i (butterfly half-distance 2^i) for the block starting at position t0:
+//   s = What_i(t0 ^ beta),  What_i(x) = W_i(x) / W_i(v_i),  W_i(x) = prod_{a in span(v_0..v_{i-1})} (x - a).
+// IFFT layer i: b ^= a; a ^= s*b (i = 0 .. K-1). FFT layer i: a ^= s*b; b ^= a (i = K-1 .. 0).
+constexpr uint8_t lch_w(int i, uint8_t x) {
+  uint8_t r = 1;
+  for (int a = 0; a < (1 << i); ++a) r = gf_mul(r, (uint8_t)(x ^ a));
+  return r;
+}
+constexpr uint8_t lch_what(int i, uint8_t x) {
+  return gf_mul(lch_w(i, x), gf_inv(lch_w(i, (uint8_t)(1 << i))));
+}
+// skew[i][b]: layer i, block b (positions b * 2^(i+1) .. + 2^(i+1) - 1), for shift beta
+template <int K>
+struct LchSkews {
+  uint8_t s[K][1 << (K - 1)] = {};
+};
+template <int K>
+constexpr LchSkews<K> lch_skews(uint8_t beta) {
+  LchSkews<K> r{};
+  for (int i = 0; i < K; ++i)
+    for (int b = 0; b < (1 << (K - 1 - i)); ++b)
+      r.s[i][b] = lch_what(i, (uint8_t)((b << (i + 1)) ^ beta));
+  return r;
+}
+// GF(2) matrix of x -> c*x on bit planes: row q = mask of input bits p whose product c * 2^p has
+// bit q (plane q of c*x = XOR of planes p in row q).
+struct BitMatrix {
+  uint8_t row[8] = {};
+};
+constexpr BitMatrix gf_bitmatrix(uint8_t c) {
+  BitMatrix m{};
+  for (int q = 0; q < 8; ++q)
+    for (int p = 0; p < 8; ++p)
+      if (gf_mul(c, (uint8_t)(1u << p)) >> q & 1) m.row[q] |= (uint8_t)(1u << p);
+  return m;
+}
+
 }  // namespace cec

@@ -65,6 +65,11 @@ bool launch_decode_ct(const KernelOpts& o, int k, int m, int missing, const Layo
 bool launch_decode1_mixed(const KernelOpts& o, int k, int m, const Layout& L,
                           const uint32_t* tagged, uint32_t nseg, hipStream_t st);
 
+// RS(32,32) encode as an additive FFT on bit-sliced data (fft.hip). False (nothing launched)
+// when the layout does not fit (shard_len % 1024, 16-byte alignment).
+bool launch_fft_rs3232(const Layout& L, const uint32_t* seg_list, uint32_t nseg, int nt,
+                       hipStream_t st);
+
 // Whether a compile-time single-erasure decode kernel exists for (k, m, missing).
 bool has_decode_ct(int k, int m, int missing);
 

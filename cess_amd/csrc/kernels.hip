@@ -1186,18 +1186,28 @@ void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_
     case 18: run_hg<P, 3, 8>(L, seg_list, nseg, st); return;
     case 19: run_hg<P, 4, 16>(L, seg_list, nseg, st); return;
     case 20: run_hg<P, 4, 17>(L, seg_list, nseg, st); return;
+    case 21: run_hg<P, 4, 0>(L, seg_list, nseg, st); return;  // r01 default (matrix form)
+    case 22: case 23: case 24:  // FFT with cached loads+stores / NT loads / NT stores
+      if (P::NI == 32 && P::NO == 32 &&
+          launch_fft_rs3232(L, seg_list, nseg, o.ct_variant == 22 ? 0 : o.ct_variant == 23 ? 1 : 2,
+                            st))
+        return;
+      break;
     default: break;
   }
 #else
   (void)o;
 #endif
-  run_hg<P, 4, 0>(L, seg_list, nseg, st);  // r01 sweep: 3.11 -> 5.26 TB/s
+  // RS(32,32): additive FFT on bit-sliced data (fft.hip) where the layout allows; else the
+  // Horner-over-groups matrix form (r01 sweep: 3.11 -> 5.26 TB/s)
+  if (P::NI == 32 && P::NO == 32 && launch_fft_rs3232(L, seg_list, nseg, 3, st)) return;
+  run_hg<P, 4, 0>(L, seg_list, nseg, st);
 }
 
 }  // namespace
 
 #ifdef CEC_TUNING
-int max_ct_variant() { return 20; }
+int max_ct_variant() { return 24; }
 #else
 int max_ct_variant() { return 0; }
 #endif

@@ -153,7 +153,8 @@ def test_reconstruct_batch_per_segment(torch, cess, corc, k, m, ln, nseg, generi
 
 
 @pytest.mark.parametrize("k,m,ln", [(2, 1, (1 << 16) + 48), (32, 32, (1 << 14) + 4),
-                                    (32, 32, 3000 * 4 + 7), (32, 32, 5)])
+                                    (32, 32, 3000 * 4 + 7), (32, 32, 5), (32, 32, 1 << 14),
+                                    (32, 32, 96), (32, 32, 3 << 10)])
 def test_ct_variants_identical(torch, cess, corc, k, m, ln):
     """Every kernel variant of the tuning build (libcessec_tune.so) is bit-exact too."""
     nseg = 4
@@ -162,7 +163,7 @@ def test_ct_variants_identical(torch, cess, corc, k, m, ln):
     want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
     d_data = to_dev(torch, data)
     enc = cess.New(k, m, tuning=True)
-    for v in range(-1, 21):
+    for v in range(-1, 25):
         enc.set_option(2, v)
         d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
         enc.EncodeBatch(d_data, d_par, nseg, ln)
