@@ -290,6 +290,8 @@ def main() -> None:
                     help="config 5: batches hashing at once in the GPU hash queue")
     ap.add_argument("--hash-stream", type=int, default=1,
                     help="config 5: 1 = hash queue on a second stream, 0 = after the encode")
+    ap.add_argument("--prio", type=int, default=0,
+                    help="config 5: 1 = encode on a high-priority stream, hashing on a low one")
     ap.add_argument("--tick-pf", type=int, default=0,
                     help="hash-queue tick prefetch depth (1 or 2; 0 = library default)")
     ap.add_argument("--rt-mode", type=int, default=0,
@@ -381,7 +383,14 @@ def main() -> None:
         pipe_hex = [d_hex] + [torch.empty_like(d_hex) for _ in range(NB - 1)]
         # --hash-stream 1: hash queue on its own stream (ticks overlap the next encode);
         # 0: one stream, encode then tick (the tick keeps the whole chip)
-        sha_stream = torch.cuda.Stream(dev) if args.hash_stream else stream
+        if args.prio:
+            # the encode's waves are dispatched ahead of the tick's as CUs free up: the HBM-bound
+            # encode and the VALU-bound ticks share the chip instead of taking turns
+            torch.cuda.synchronize(dev)  # inputs were produced on the default stream
+            stream = torch.cuda.Stream(dev, priority=-1)
+            sha_stream = torch.cuda.Stream(dev, priority=0)
+        else:
+            sha_stream = torch.cuda.Stream(dev) if args.hash_stream else stream
         chains = W * nseg * (k + m)
         hq = cess_amd.HashQueue(capacity=1 << max(10, (chains - 1).bit_length()), device=local,
                                 stream=sha_stream)
@@ -522,7 +531,7 @@ def main() -> None:
 
     tag = f"c{args.config}"
     kernel_name = {2: "k_ct<EncCT<2, 1>>", 3: "k_ct_dec1_mixed21 (Dec1CT<2, 1, e> / EncCT<2, 1> per segment)",
-                   4: "k_ct<EncCT<2, 1>>", 5: "k_hg<EncCT<32, 32>, 4>", 6: "k_rthx<8>",
+                   4: "k_ct<EncCT<2, 1>>", 5: "k_fft3232<true, true>", 6: "k_rthx<8>",
                    7: "k_rthx<8>", 8: "k_rthx<3>"}[args.config]
     if args.generic:
         kernel_name = "k_rthx" if k <= 32 else "k_rt"

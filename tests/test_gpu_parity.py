@@ -653,3 +653,26 @@ def test_full_geometry_config4_64gib(torch, cess, corc):
         idx = seg[lost == e]
         got = d_data[idx, e] if e < k else d_par[idx, e - k]
         assert torch.equal(got, keep[idx]), e
+
+
+def test_config1_single_segment_host_api(cess, corc):
+    """BASELINE config 1's workload through the klauspost-shaped host API: one 16 MiB segment
+    split into 2 x 8 MiB fragments, encoded, then each of the 3 fragments erased and rebuilt;
+    bit-exact vs the C oracle (and the C oracle's threaded single-segment ops agree)."""
+    from oracle.c_oracle import ptrs
+    k, m, F = 2, 1, 8 * MiB
+    seg = np.empty(k * F, np.uint8)
+    corc.orc_fill_synthetic(seg.ctypes.data, k * F, 1, 0, 0xCE550001)
+    enc = cess.New(k, m)
+    shards = enc.Split(seg)
+    enc.Encode(shards)
+    want = c_encode(corc, k, m, shards[:k])
+    assert np.array_equal(shards[2], want[0])
+    for e in range(3):
+        sh = [s.copy() for s in shards]
+        sh[e] = None
+        enc.Reconstruct(sh)
+        assert all(np.array_equal(a, b) for a, b in zip(sh, shards)), e
+    cpu = [shards[0].copy(), shards[1].copy(), np.zeros(F, np.uint8)]
+    corc.orc_segment_ops(k, m, ptrs(cpu), F, 4, 1)
+    assert all(np.array_equal(a, b) for a, b in zip(cpu, shards))
