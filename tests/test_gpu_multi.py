@@ -32,6 +32,7 @@ def _rank(rank, world, port, k, m, nseg, F, q):
     torch.cuda.set_device(rank)
     dev = torch.device("cuda", rank)
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    dist.barrier()  # a collective over every rank before the grouped point-to-point ops
     corc = load_c_oracle()
     n = k + m
     rng = np.random.default_rng(7)  # same on every rank: every codeword known to all
