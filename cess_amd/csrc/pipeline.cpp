@@ -6,9 +6,13 @@
 //   s_h2d:   waits until device slot ds = i % nd is free, copies the batch in
 //   s_comp:  cec_encode_batch into the slot's parity
 //   s_d2h:   copies parity into pinned parity slot hs
-//   s_hash:  (hash = 1) adds the batch's segment and fragment chains to the GPU hash queue and
-//            ticks it once: `window` batches hash together and a batch's hex is final `window`
-//            ticks after its add (cec_hashq_*), then copies the hex to pinned memory
+//   s_comp:  (hash = 1) then adds the batch's segment and fragment chains to the GPU hash queue
+//            and ticks it once: `window` batches hash together and a batch's hex is final
+//            `window` ticks after its add (cec_hashq_*); the hex is copied to pinned memory
+//            there too. Ticks share the compute stream with the encodes on purpose: three
+//            streams fit the device's hardware queues (GPU_MAX_HW_QUEUES = 4, one taken by the
+//            codec), and a fourth stream shared a queue with the parity copies, which held every
+//            tick behind a 11 ms D2H (rocprof timeline, profiles/r02/).
 // and the host delivers on_fragments (shards straight from the pinned slots) and on_record (hex)
 // in segment order. Reading batch i+1 on the host overlaps the copies and kernels of batch i,
 // H2D overlaps D2H (PCIe is full duplex), and the hash queue overlaps everything.
@@ -64,7 +68,7 @@ struct cec_pipeline {
   // device slots
   std::vector<uint8_t*> d_data, d_par, d_shex, d_fhex;
   std::vector<uint8_t*> h_shex, h_fhex;  // pinned hex, per device slot
-  hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr, s_hash = nullptr;
+  hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr;
   std::vector<hipEvent_t> ev_h2d, ev_enc, ev_d2h, ev_hex;  // per device slot
   cec_hashq* hq = nullptr;
   uint32_t tick_blocks = 0;
@@ -78,7 +82,7 @@ struct cec_pipeline {
 
   ~cec_pipeline() {
     (void)hipSetDevice(device);
-    for (hipStream_t s : {s_h2d, s_comp, s_d2h, s_hash})
+    for (hipStream_t s : {s_h2d, s_comp, s_d2h})
       if (s) (void)hipStreamSynchronize(s);
     if (hq) cec_hashq_destroy(hq);
     for (auto* v : {&h_in, &h_par, &h_shex, &h_fhex})
@@ -90,7 +94,7 @@ struct cec_pipeline {
     for (auto* v : {&ev_h2d, &ev_enc, &ev_d2h, &ev_hex})
       for (hipEvent_t e : *v)
         if (e) (void)hipEventDestroy(e);
-    for (hipStream_t s : {s_h2d, s_comp, s_d2h, s_hash})
+    for (hipStream_t s : {s_h2d, s_comp, s_d2h})
       if (s) (void)hipStreamDestroy(s);
   }
 
@@ -106,7 +110,9 @@ struct cec_pipeline {
     window = o.window ? o.window : 16;
     if (window < 1) return cec::set_error(CEC_EINVAL, "window must be >= 1");
     max_segments = o.max_segments;
-    nd = hash ? window + 1 : 3;
+    // a slot is reused nd batches later; its hashes are final `window` ticks after its add, and
+    // two more slots keep the H2D of a reused slot from waiting on the tick just enqueued
+    nd = hash ? window + 3 : 3;
     PL_TRY(hipSetDevice(device));
     for (hipStream_t* s : {&s_h2d, &s_comp, &s_d2h})
       PL_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
@@ -126,7 +132,6 @@ struct cec_pipeline {
         PL_TRY(hipEventCreateWithFlags(&(*v)[i], hipEventDisableTiming));
     }
     if (hash) {
-      PL_TRY(hipStreamCreateWithFlags(&s_hash, hipStreamNonBlocking));
       d_shex.assign(nd, nullptr);
       d_fhex.assign(nd, nullptr);
       h_shex.assign(nd, nullptr);
@@ -139,7 +144,7 @@ struct cec_pipeline {
       }
       size_t chains = (size_t)(window + 1) * B * (k + m + 1), cap = 1024;
       while (cap < chains) cap <<= 1;
-      PL_RC(cec_hashq_create(device, cap, s_hash, &hq));
+      PL_RC(cec_hashq_create(device, cap, s_comp, &hq));
       const uint64_t blocks = cec::sha256_blocks(SB);
       tick_blocks = (uint32_t)((blocks + window - 1) / window);
     }
@@ -177,10 +182,10 @@ struct cec_pipeline {
   int copy_hex(Batch& b) {
     while (!hashed(b)) PL_RC(cec_hashq_tick(hq, tick_blocks));
     PL_TRY(hipMemcpyAsync(h_shex[b.ds], d_shex[b.ds], b.nseg * 64, hipMemcpyDeviceToHost,
-                          s_hash));
+                          s_comp));
     PL_TRY(hipMemcpyAsync(h_fhex[b.ds], d_fhex[b.ds], b.nseg * (k + m) * 64,
-                          hipMemcpyDeviceToHost, s_hash));
-    PL_TRY(hipEventRecord(ev_hex[b.ds], s_hash));
+                          hipMemcpyDeviceToHost, s_comp));
+    PL_TRY(hipEventRecord(ev_hex[b.ds], s_comp));
     b.hex_copied = true;
     return CEC_OK;
   }
@@ -212,7 +217,7 @@ int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_frag
   PL_TRY(hipSetDevice(p->device));
   // start clean after an aborted run: no queued copies, no live chains of the old batches
   if (p->hash) PL_RC(cec_hashq_finish(p->hq));
-  for (hipStream_t s : {p->s_h2d, p->s_comp, p->s_d2h, p->s_hash})
+  for (hipStream_t s : {p->s_h2d, p->s_comp, p->s_d2h})
     if (s) PL_TRY(hipStreamSynchronize(s));
   const double t0 = now_s();
   double t_read = 0, t_wait = 0;
@@ -325,10 +330,7 @@ int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_frag
     PL_TRY(hipMemcpyAsync(p->h_par[hs], p->d_par[ds], nseg * p->m * p->F, hipMemcpyDeviceToHost,
                           p->s_d2h));
     PL_TRY(hipEventRecord(p->ev_d2h[ds], p->s_d2h));
-    if (p->hash) {
-      PL_TRY(hipStreamWaitEvent(p->s_hash, p->ev_enc[ds], 0));
-      PL_RC(p->add_hashes(b));
-    }
+    if (p->hash) PL_RC(p->add_hashes(b));  // on s_comp, after the encode
     inflight.push_back(b);
     // deliver whatever has completed, without blocking (a slot's event re-recorded by a newer
     // batch completes later on the same stream, so a query of it is conservative)
@@ -360,7 +362,7 @@ int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_frag
   // drain
   if (p->hash) PL_RC(cec_hashq_finish(p->hq));
   if (i) PL_RC(records_through(i - 1));
-  for (hipStream_t s : {p->s_h2d, p->s_comp, p->s_d2h, p->s_hash})
+  for (hipStream_t s : {p->s_h2d, p->s_comp, p->s_d2h})
     if (s) PL_TRY(hipStreamSynchronize(s));
   if (stats) {
     stats->segments = seg_base;

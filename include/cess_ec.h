@@ -154,7 +154,7 @@ int cec_split_segment(const uint8_t* seg, size_t seg_len, int k, uint8_t* const*
  * compute stream, parity D2H on a third stream, so reading batch i+1 overlaps the copies and
  * kernels of batch i and H2D overlaps D2H. With hash = 1 every SegmentList hash (segment hash
  * and the k+m fragment hashes, SHA-256 hex) is computed on the GPU by a hash queue that keeps
- * `window` batches hashing at once (device slots = window + 1).
+ * `window` batches hashing at once (device slots = window + 3).
  *   read(user, dst, cap): write up to cap source bytes at dst; return the count, 0 at the end,
  *     < 0 to abort (CEC_ECALLBACK).
  *   on_fragments(user, seg, shards, shard_len): the k+m shards of segment `seg`, host memory
