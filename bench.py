@@ -35,6 +35,9 @@ sys.path.insert(0, ROOT)
 MiB = 1 << 20
 GB = 1e9
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# VALU issue peak, full-rate lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (SURVEY.md §8d:
+# the roofline of the SHA-256 stage; half-rate instructions take two of these slots)
+VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12
 METRIC = "RS encode/decode GB/s per GPU and whole node; % of HBM roofline"
 SEED0 = 0xCE550000
 
@@ -260,6 +263,16 @@ def degraded_gather(enc, k: int, m: int, F: int, world: int, rank: int, dev, nse
     return run, verify, plan
 
 
+def load_valu_slots(tag: str):
+    """Static VALU issue slots per 64-byte block of the hash-queue tick (profiles/valu_<tag>.json,
+    written by tools/sha_slots.py from the built code object), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", f"valu_{tag}.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
 def load_traffic(tag: str, algo_bytes: int, kernel: str):
     """Per-launch HBM bytes from the PMC passes (profiles/traffic_<tag>.json), if they were
     collected for this kernel at this launch size; None otherwise."""
@@ -286,8 +299,10 @@ def main() -> None:
                     help="segments per GPU (default: the config's; config 5 at 1024 = 16 GiB in "
                          "flight, enough fragments to give every SIMD a SHA-256 wave)")
     ap.add_argument("--sha-mode", type=int, default=0, help="0 auto, 1 one wave, 2 two waves")
-    ap.add_argument("--window", type=int, default=64,
-                    help="config 5: batches hashing at once in the GPU hash queue")
+    ap.add_argument("--window", type=int, default=96,
+                    help="config 5: batches hashing at once in the GPU hash queue (96 x 4096 "
+                         "fragment chains: 6 one-wave tick workgroups per SIMD; 64 -> 1.74 ms "
+                         "per step, 96..192 -> 1.61-1.63)")
     ap.add_argument("--hash-stream", type=int, default=1,
                     help="config 5: 1 = hash queue on a second stream, 0 = after the encode")
     ap.add_argument("--prio", type=int, default=0,
@@ -528,6 +543,19 @@ def main() -> None:
                                 "); the timed region ends with the window drained",
                     "note": "SHA-256 is one sequential chain per fragment: bounded by streams x "
                             "per-wave issue rate, reported apart from the HBM roofline"}
+        slots = load_valu_slots("c5")
+        if slots:
+            # the step's hashing against the VALU issue roofline: every block of every fragment
+            # chain costs the tick loop's issue slots on one lane
+            blocks = nseg * (k + m) * cess_amd.sha256_blocks(F) * args.steps
+            ach = blocks * slots["issue_slots_per_block"] / elapsed / 1e12
+            sha_note["roofline"] = {
+                "bound": "valu", "kernel": "k_sha256_tick1", "achieved": round(ach, 2),
+                "peak": round(VALU_PEAK_TLANE, 2), "unit": "T lane-slots/s",
+                "frac": round(ach / VALU_PEAK_TLANE, 4),
+                "issue_slots_per_block": slots["issue_slots_per_block"],
+                "valu_instr_per_block": slots["valu_instr_per_block"],
+                "basis": "whole step (hash ticks share the chip with the encode); peak at 2.4 GHz"}
 
     tag = f"c{args.config}"
     kernel_name = {2: "k_ct<EncCT<2, 1>>", 3: "k_ct_dec1_mixed21 (Dec1CT<2, 1, e> / EncCT<2, 1> per segment)",

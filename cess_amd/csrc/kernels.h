@@ -106,11 +106,12 @@ struct ShaChain {
   uint32_t h[8];
   uint8_t* pre_hex;
   uint64_t pre_blk;
-  uint64_t pad_[6];
+  uint32_t pre_h[8];  // state after pre_blk blocks, parked by the one-wave tick until its loop ends
+  uint64_t pad_[2];
 };
 static_assert(sizeof(ShaChain) == 128, "ShaChain is one 128-byte record");
 
-inline uint64_t sha256_blocks(uint64_t len) { return (len >> 6) + ((len & 63) >= 56 ? 2 : 1); }
+__host__ __device__ inline uint64_t sha256_blocks(uint64_t len) { return (len >> 6) + ((len & 63) >= 56 ? 2 : 1); }
 
 // Initialise n chains in slots slot0.. of the ring `tab` (capacity mask + 1, a power of two).
 // pre_blk > 0: chain i also writes the hex of its first pre_blk blocks to

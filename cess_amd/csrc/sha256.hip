@@ -10,6 +10,8 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return xor3_u32(a, b, c);
 }
 
+#define CEC_SHA_AI __attribute__((always_inline))
+
 // ---------------------------------------------------------------------------------------------
 // SHA-256 (FIPS 180-4), one lane per buffer.
 // ---------------------------------------------------------------------------------------------
@@ -37,20 +39,34 @@ __device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
 
+// D >= 0: empty asm statements pin the expansion of message word t + D to round t. Without them
+// (D < 0) the compiler expands all 48 schedule words up front (they do not depend on the state)
+// and holds them. Pinned, the one-wave tick fits in 74 VGPRs instead of 100, leaving room for an
+// RS(32,32) encode wave beside four tick waves per SIMD; measured, that co-residence slowed
+// config 5's step from 1.74 to 2.03 ms, so the ticks run unpinned and only the
+// prefix-digest compression (after the tick loop) is pinned.
+template <int D = -1>
 __device__ __forceinline__ void sha256_block(uint32_t (&h)[8], uint32_t (&w)[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  auto expand = [&](int u) CEC_SHA_AI {  // W[u] into w[u & 15] (which held W[u - 16])
+    const uint32_t w15 = w[(u + 1) & 15], w2 = w[(u + 14) & 15];
+    const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+    const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+    w[u & 15] = w[u & 15] + s0 + w[(u + 9) & 15] + s1;
+  };
 #pragma unroll
   for (int t = 0; t < 64; ++t) {
-    uint32_t wt;
-    if (t < 16) {
-      wt = w[t];
+    if constexpr (D >= 0) {
+      asm volatile("" : "+v"(a), "+v"(e));
+      const int u = t + D;
+      if (u >= 16 && u < 64) {
+        asm volatile("" : "+v"(w[(u + 14) & 15]), "+v"(w[(u + 1) & 15]) : "v"(e));
+        expand(u);
+      }
     } else {
-      const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
-      const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
-      const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-      wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
-      w[t & 15] = wt;
+      if (t >= 16) expand(t);
     }
+    const uint32_t wt = w[t & 15];
     const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
     const uint32_t t1 = hh + S1 + ch(e, f, g) + kSha256K[t] + wt;
     const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
@@ -383,25 +399,31 @@ __device__ __forceinline__ void sha_block_general(uint32_t (&w)[16], const uint8
   }
 }
 
-#define CEC_SHA_AI __attribute__((always_inline))
 
 // Prefix digest of a chain (ShaChain::pre_blk): finish a copy of the state after `blocks` whole
-// message blocks with the one padding block of a 64-byte-multiple length, write its hex. Not
-// inlined: it runs once per chain, and a second inlined compression would raise the tick
-// kernels' VGPR counts.
-// The state goes by value (eight VGPR arguments): a pointer would put the caller's h in scratch.
-__device__ __noinline__ void sha_prefix_hex(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
-                                            uint32_t h4, uint32_t h5, uint32_t h6, uint32_t h7,
-                                            uint64_t blocks, uint8_t* __restrict__ hex) {
-  uint32_t h[8] = {h0, h1, h2, h3, h4, h5, h6, h7}, w[16];
+// message blocks with the one padding block of a 64-byte-multiple length, write its hex.
+template <int D = -1>
+__device__ __forceinline__ void sha_prefix_hex_inl(uint32_t (&h)[8], uint64_t blocks,
+                                                   uint8_t* __restrict__ hex) {
+  uint32_t w[16];
   const uint64_t bits = blocks << 9;
   w[0] = 0x80000000u;
 #pragma unroll
   for (int q = 1; q < 14; ++q) w[q] = 0;
   w[14] = (uint32_t)(bits >> 32);
   w[15] = (uint32_t)bits;
-  sha256_block(h, w);
+  sha256_block<D>(h, w);
   sha_store_hex(hex, h);
+}
+
+// Out-of-line form for the two-wave tick, which reaches the prefix inside its block loop (an
+// inlined second compression there would raise its VGPR count). The state goes by value (eight
+// VGPR arguments): a pointer would put the caller's h in scratch.
+__device__ __noinline__ void sha_prefix_hex(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
+                                            uint32_t h4, uint32_t h5, uint32_t h6, uint32_t h7,
+                                            uint64_t blocks, uint8_t* __restrict__ hex) {
+  uint32_t h[8] = {h0, h1, h2, h3, h4, h5, h6, h7};
+  sha_prefix_hex_inl(h, blocks, hex);
 }
 
 template <int PF>
@@ -535,6 +557,7 @@ __global__ __launch_bounds__(128) void k_sha256_tick(ShaChain* __restrict__ tab,
 // producer and a consumer wave, so it loses in the latency regime (few chains: one wave's issue
 // rate is the bound) and can win in the throughput regime (several waves per SIMD interleave,
 // and no barrier ties a consumer to its producer).
+template <int D>
 __global__ __launch_bounds__(64) void k_sha256_tick1(ShaChain* __restrict__ tab, uint32_t mask,
                                                      uint64_t head, uint32_t n,
                                                      uint32_t max_blocks) {
@@ -557,16 +580,18 @@ __global__ __launch_bounds__(64) void k_sha256_tick1(ShaChain* __restrict__ tab,
   const bool al16 = ((uintptr_t)src & 15) == 0;
   const uint64_t dat = blk0 < nfull ? nfull - blk0 : 0;
   const uint32_t nfast = al16 ? (uint32_t)(dat < nblk ? dat : nblk) : 0u;
+  // 32-bit loop state only: the prefix block relative to blk0 (0: not in this tick), a running
+  // pointer for the fast path; the general path re-reads the chain record
+  const uint32_t pre_rel = pre > blk0 && pre - blk0 <= nblk ? (uint32_t)(pre - blk0) : 0u;
+  const uint8_t* p = src + (blk0 << 6);
   uint32_t w[16];
   u32x4 nx[4] = {};
   if (nfast) {
-    const uint8_t* p = src + (blk0 << 6);
 #pragma unroll
     for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
   }
   // one compression per iteration (a second inlined copy of the rounds doubles the VGPRs)
   for (uint32_t b = 0; b < nblk; ++b) {
-    const uint64_t g = blk0 + b;
     if (b < nfast) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -575,22 +600,38 @@ __global__ __launch_bounds__(64) void k_sha256_tick1(ShaChain* __restrict__ tab,
         w[4 * q + 2] = __builtin_bswap32(nx[q].z);
         w[4 * q + 3] = __builtin_bswap32(nx[q].w);
       }
+      p += 64;
       if (b + 1 < nfast) {
-        const uint8_t* p = src + ((g + 1) << 6);
 #pragma unroll
         for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
       }
     } else {
-      sha_block_general(w, src, g, nfull, r, nb, len, &stage[threadIdx.x][0], 1);
+      const volatile ShaChain* cv = ch_;
+      const uint64_t len_ = cv->len, nfull_ = len_ >> 6;
+      const uint32_t r_ = (uint32_t)(len_ & 63);
+      sha_block_general(w, (const uint8_t*)cv->src, cv->blk + b, nfull_, r_,
+                        nfull_ + (r_ >= 56 ? 2 : 1), len_, &stage[threadIdx.x][0], 1);
     }
-    sha256_block(h, w);
-    if (g + 1 == pre)
-      sha_prefix_hex(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], pre, ch_->pre_hex);
+    sha256_block<D>(h, w);
+    if (b + 1 == pre_rel) {  // parked: a call in the loop would hold the loop's live values across it
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ch_->pre_h[q] = h[q];
+    }
   }
+  // the record's fields are re-read rather than held across the loop
+  const volatile ShaChain* cv = ch_;
+  const uint64_t blk_end = cv->blk + nblk;
+  const bool done = blk_end == sha256_blocks(cv->len);
 #pragma unroll
   for (int q = 0; q < 8; ++q) ch_->h[q] = h[q];
-  ch_->blk = blk0 + nblk;
-  if (blk0 + nblk == nb && ch_->hex) sha_store_hex(ch_->hex, h);
+  if (pre_rel) {  // after the loop, inlined: few values are live here
+    uint32_t ph[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ph[q] = cv->pre_h[q];
+    sha_prefix_hex_inl<D < 0 ? 0 : D>(ph, cv->pre_blk, cv->pre_hex);
+  }
+  ch_->blk = blk_end;
+  if (done && cv->hex) sha_store_hex(cv->hex, h);
 }
 
 // Initialise n chains in queue slots slot0.. (mod capacity): buffer i starts at
@@ -614,7 +655,9 @@ __global__ __launch_bounds__(256) void k_hashq_add(ShaChain* __restrict__ tab, u
   c.pre_blk = pre_hex ? pre_blk : 0;
   c.pre_hex = pre_hex ? pre_hex + (a * pre_hex_outer + b) * 64 : nullptr;
 #pragma unroll
-  for (int q = 0; q < 6; ++q) c.pad_[q] = 0;
+  for (int q = 0; q < 8; ++q) c.pre_h[q] = 0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) c.pad_[q] = 0;
   const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                           0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
 #pragma unroll
@@ -656,8 +699,8 @@ void launch_sha256_tick(int tick_mode, ShaChain* tab, uint32_t mask, uint64_t he
   // crossover, profiles/r01/sha_scale_*.jsonl)
   const int v = tick_mode >= 1 && tick_mode <= 3 ? tick_mode : (live >= (1u << 17) ? 3 : 1);
   if (v == 3)
-    hipLaunchKernelGGL(k_sha256_tick1, dim3((n + 63) / 64), dim3(64), 0, st, tab, mask, head, n,
-                       max_blocks);
+    hipLaunchKernelGGL(k_sha256_tick1<-1>, dim3((n + 63) / 64), dim3(64), 0, st, tab, mask, head,
+                       n, max_blocks);
   else if (v == 2)
     hipLaunchKernelGGL(k_sha256_tick<2>, dim3((n + 63) / 64), dim3(128), 0, st, tab, mask, head,
                        n, max_blocks);

@@ -246,3 +246,21 @@ def test_rthx_resources(gfx950_code_object):
         assert int(r["vgpr_spill_count"]) == 0 and int(r["sgpr_spill_count"]) == 0, name
         assert int(r.get("agpr_count", 0)) == 0, name
         assert int(r["vgpr_count"]) >= 24 + 16 * ng, (name, r["vgpr_count"])
+
+
+def test_sha_tick_slot_count_matches_library():
+    """bench.py prices config 5's hashing against the VALU roofline with the issue slots per block
+    in profiles/valu_c5.json; they must be those of the shipped k_sha256_tick1 block loop."""
+    import json
+    import os
+    import sys
+    from cess_amd import _lib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import sha_slots
+    sym, ops = sha_slots.loop_counts(sha_slots.disassemble(_lib.LIB_PATH))
+    with open(os.path.join(root, "profiles", "valu_c5.json")) as f:
+        rec = json.load(f)
+    assert rec["kernel"] == sym
+    assert rec["valu_instr_per_block"] == sum(ops.values())
+    assert ops["v_alignbit_b32"] >= 64 * 6 + 48 * 4  # every rotate of the rounds and schedule
