@@ -5,7 +5,7 @@ from __future__ import annotations
 import ctypes
 import os
 from ctypes import (CFUNCTYPE, POINTER, Structure, c_char_p, c_double, c_int, c_longlong,
-                    c_size_t, c_uint8, c_uint32, c_uint64, c_void_p)
+                    c_int32, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CESS_EC_LIB", os.path.join(_HERE, "libcessec.so"))
@@ -17,11 +17,17 @@ TUNE_LIB_PATH = os.path.join(_HERE, "libcessec_tune.so")
 READ_FN = CFUNCTYPE(c_longlong, c_void_p, c_void_p, c_size_t)
 FRAGMENTS_FN = CFUNCTYPE(c_int, c_void_p, c_uint64, POINTER(c_void_p), c_size_t)
 RECORD_FN = CFUNCTYPE(c_int, c_void_p, c_uint64, c_void_p, c_void_p)
+# cec_dist_degraded_read locate callback
+LOCATE_FN = CFUNCTYPE(c_void_p, c_void_p, c_uint64, c_int)
 
 
 class PipelineOpts(Structure):
     _fields_ = [("shard_len", c_size_t), ("batch_segments", c_size_t), ("depth", c_int),
                 ("hash", c_int), ("window", c_int), ("max_segments", c_uint64)]
+
+
+class DistMove(Structure):
+    _fields_ = [("seg", c_uint64), ("frag", c_int32), ("src", c_int32), ("dst", c_int32)]
 
 
 class PipelineStats(Structure):
@@ -80,6 +86,14 @@ SIGNATURES = {
                                              c_void_p, c_void_p, c_size_t, c_void_p, c_size_t,
                                              c_void_p, c_size_t, POINTER(c_size_t)]),
     "cec_shard_id": (c_int, [c_void_p, c_uint32, c_void_p]),
+    "cec_dist_unique_id": (c_int, [c_void_p]),
+    "cec_dist_create": (c_int, [c_void_p, c_void_p, c_int, c_int, POINTER(c_void_p)]),
+    "cec_dist_destroy": (None, [c_void_p]),
+    "cec_dist_plan": (c_int, [c_int, c_int, c_int, POINTER(c_uint64), POINTER(c_uint8), c_size_t,
+                              POINTER(DistMove), c_size_t, POINTER(c_size_t), POINTER(c_int32)]),
+    "cec_dist_degraded_read": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint8), c_size_t,
+                                       c_size_t, LOCATE_FN, c_void_p, POINTER(c_void_p), c_void_p,
+                                       POINTER(c_size_t)]),
     "cec_hash_from_shard_id": (c_int, [c_void_p, c_void_p]),
 }
 
@@ -106,6 +120,7 @@ CEC_OPT_DECODE_CACHE = 6
 CEC_STAT_DECODE_CACHED = 1
 CEC_STAT_RETIRED_PENDING = 2
 CEC_HQOPT_TICK = 1
+CEC_DIST_ID_BYTES = 128
 
 _libs = {}
 

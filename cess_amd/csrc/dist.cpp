@@ -1,0 +1,358 @@
+// libcessec multi-GPU degraded read: one process (or thread) per GPU, RCCL over
+// xGMI for the one exchange step of the path.
+//
+// Placement: fragment f of segment s lives on rank (s + f) mod world, the GPU analogue of the
+// chain's miner assignment (random_assign_miner, c-pallets/file-bank/src/functions.rs:187-283,
+// which puts a segment's fragments on distinct miners). A degraded read gathers, for every
+// segment with lost fragments, the first k surviving fragments (the codec's survivor choice) on
+// the rank that owns the segment's first lost fragment (repair restores a fragment where it
+// lives, c-pallets/file-bank/src/lib.rs:943-1122), straight into a [seg][shard][F] staging batch,
+// and rebuilds the lost fragments there with one cec_reconstruct_batch (per-segment patterns).
+// RCCL has no XOR reduction (rccl.h ncclRedOp_t), so survivors move by grouped point-to-point
+// send/recv; every rank issues the moves in the same (segment, fragment) order, which is what
+// pairs each send with its receive. Before any byte moves, the ranks agree (one 4-byte min
+// all-reduce) that every rank found its local survivors, so a caller error fails on all ranks
+// instead of leaving the others waiting in a receive.
+//
+// RCCL is loaded at run time (dlopen): the rest of libcessec does not depend on it, and without
+// it the cec_dist_* entry points return CEC_ENCCL.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cess_ec.h"
+
+namespace cec {
+int set_error(int code, const std::string& msg);
+}
+
+namespace {
+
+#define DI_TRY(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      return cec::set_error(_e == hipErrorOutOfMemory ? CEC_ENOMEM : CEC_EHIP,              \
+                            std::string(#expr) + ": " + hipGetErrorString(_e));             \
+  } while (0)
+
+struct Rccl {
+  bool ok = false;
+  std::string why;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      r.why = std::string("librccl not loadable: ") + dlerror();
+      return;
+    }
+    bool all = true;
+    auto sym = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+      all &= fn != nullptr;
+    };
+    sym(r.get_unique_id, "ncclGetUniqueId");
+    sym(r.comm_init_rank, "ncclCommInitRank");
+    sym(r.comm_destroy, "ncclCommDestroy");
+    sym(r.send, "ncclSend");
+    sym(r.recv, "ncclRecv");
+    sym(r.all_reduce, "ncclAllReduce");
+    sym(r.group_start, "ncclGroupStart");
+    sym(r.group_end, "ncclGroupEnd");
+    sym(r.error_string, "ncclGetErrorString");
+    r.ok = all;
+    if (!all) r.why = "librccl lacks an expected symbol";
+  });
+  return r;
+}
+
+int nccl_err(ncclResult_t res, const char* what) {
+  return cec::set_error(CEC_ENCCL, std::string(what) + ": " + rccl().error_string(res));
+}
+
+#define NC_TRY(expr)                                 \
+  do {                                               \
+    ncclResult_t _r = (expr);                        \
+    if (_r != ncclSuccess) return nccl_err(_r, #expr); \
+  } while (0)
+
+struct Seg {
+  uint64_t seg;
+  std::vector<int> lost;  // sorted, distinct
+  int decoder;
+  std::vector<int> surv;  // first k present fragments
+};
+
+// Group the lost list by segment and apply the placement rule (shared by cec_dist_plan and the
+// degraded read, so the plan a caller inspects is the one that runs).
+int make_plan(int k, int m, int world, const uint64_t* lost_seg, const uint8_t* lost_frag,
+              size_t nlost, std::vector<Seg>* out) {
+  if (k < 1 || m < 1 || k + m > 256 || world < 1 || (nlost && (!lost_seg || !lost_frag)))
+    return cec::set_error(CEC_EINVAL, "dist plan: bad k, m, world or null lost list");
+  std::map<uint64_t, std::vector<int>> by;
+  for (size_t i = 0; i < nlost; ++i) {
+    if (lost_frag[i] >= k + m)
+      return cec::set_error(CEC_EINVAL, "dist plan: lost fragment index " +
+                                            std::to_string(lost_frag[i]) + " outside 0..k+m-1");
+    by[lost_seg[i]].push_back(lost_frag[i]);
+  }
+  out->clear();
+  for (auto& [s, v] : by) {
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    if ((int)v.size() > m)
+      return cec::set_error(CEC_ETOOFEW, "dist plan: segment " + std::to_string(s) + " lost " +
+                                             std::to_string(v.size()) + " > m fragments");
+    Seg g{s, v, (int)((s + (uint64_t)v[0]) % (uint64_t)world), {}};
+    for (int f = 0; f < k + m && (int)g.surv.size() < k; ++f)
+      if (!std::binary_search(v.begin(), v.end(), f)) g.surv.push_back(f);
+    out->push_back(std::move(g));
+  }
+  return CEC_OK;
+}
+
+int owner(uint64_t s, int f, int world) { return (int)((s + (uint64_t)f) % (uint64_t)world); }
+
+}  // namespace
+
+struct cec_dist {
+  cec_codec* codec = nullptr;
+  int k = 0, m = 0, device = 0, world = 0, rank = 0;
+  ncclComm_t comm = nullptr;
+  uint8_t* stage = nullptr;  // staging batch: data [nseg_d][k][F], then parity [nseg_d][m][F]
+  size_t stage_bytes = 0;
+  int* d_flag = nullptr;
+};
+
+extern "C" {
+
+int cec_dist_unique_id(uint8_t* id) {
+  if (!id) return cec::set_error(CEC_EINVAL, "null id");
+  const Rccl& r = rccl();
+  if (!r.ok) return cec::set_error(CEC_ENCCL, r.why);
+  ncclUniqueId u;
+  NC_TRY(r.get_unique_id(&u));
+  std::copy(u.internal, u.internal + NCCL_UNIQUE_ID_BYTES, reinterpret_cast<char*>(id));
+  return CEC_OK;
+}
+
+int cec_dist_create(cec_codec* codec, const uint8_t* id, int world, int rank, cec_dist** out) {
+  if (!codec || !id || !out || world < 1 || rank < 0 || rank >= world)
+    return cec::set_error(CEC_EINVAL, "dist create: null argument or rank outside 0..world-1");
+  static_assert(CEC_DIST_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
+  const Rccl& r = rccl();
+  if (!r.ok) return cec::set_error(CEC_ENCCL, r.why);
+  auto* d = new cec_dist;
+  d->codec = codec;
+  d->world = world;
+  d->rank = rank;
+  cec_codec_info(codec, &d->k, &d->m, &d->device);
+  ncclUniqueId u;
+  std::copy(id, id + NCCL_UNIQUE_ID_BYTES, reinterpret_cast<uint8_t*>(u.internal));
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  hipError_t he = hipSetDevice(d->device);
+  ncclResult_t res = he == hipSuccess ? r.comm_init_rank(&d->comm, world, u, rank) : ncclSuccess;
+  if (he == hipSuccess && res == ncclSuccess) he = hipMalloc(&d->d_flag, sizeof(int));
+  (void)hipSetDevice(prev);
+  if (he != hipSuccess || res != ncclSuccess) {
+    int rc = he != hipSuccess ? cec::set_error(CEC_EHIP, std::string("dist create: ") +
+                                                             hipGetErrorString(he))
+                              : nccl_err(res, "ncclCommInitRank");
+    if (d->comm) r.comm_destroy(d->comm);
+    delete d;
+    return rc;
+  }
+  *out = d;
+  return CEC_OK;
+}
+
+void cec_dist_destroy(cec_dist* d) {
+  if (!d) return;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(d->device);
+  (void)hipDeviceSynchronize();
+  if (d->comm) rccl().comm_destroy(d->comm);
+  (void)hipFree(d->stage);
+  (void)hipFree(d->d_flag);
+  (void)hipSetDevice(prev);
+  delete d;
+}
+
+int cec_dist_plan(int k, int m, int world, const uint64_t* lost_seg, const uint8_t* lost_frag,
+                  size_t nlost, cec_dist_move* moves, size_t moves_cap, size_t* nmoves,
+                  int32_t* decoder) {
+  std::vector<Seg> plan;
+  int rc = make_plan(k, m, world, lost_seg, lost_frag, nlost, &plan);
+  if (rc) return rc;
+  size_t n = 0;
+  for (const Seg& g : plan)
+    for (int f : g.surv) {
+      if (moves && n < moves_cap)
+        moves[n] = cec_dist_move{g.seg, f, owner(g.seg, f, world), g.decoder};
+      ++n;
+    }
+  if (nmoves) *nmoves = n;
+  if (decoder)
+    for (size_t i = 0; i < nlost; ++i)
+      decoder[i] = std::lower_bound(plan.begin(), plan.end(), lost_seg[i],
+                                    [](const Seg& g, uint64_t s) { return g.seg < s; })
+                       ->decoder;
+  if (moves && n > moves_cap) return cec::set_error(CEC_EINVAL, "dist plan: moves_cap too small");
+  return CEC_OK;
+}
+
+int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t* lost_frag,
+                           size_t nlost, size_t shard_len, cec_locate_fn locate, void* user,
+                           uint8_t* const* d_out, void* hip_stream, size_t* nrebuilt) {
+  if (!d || !locate || shard_len == 0)
+    return cec::set_error(CEC_EINVAL, "dist degraded read: null argument or zero shard_len");
+  const Rccl& r = rccl();
+  const int k = d->k, m = d->m, n = k + m, world = d->world, rank = d->rank;
+  const size_t F = shard_len;
+  std::vector<Seg> plan;
+  int rc = make_plan(k, m, world, lost_seg, lost_frag, nlost, &plan);
+  if (rc) return rc;  // every rank sees the same list, so every rank fails here alike
+
+  // this rank's part: segments it rebuilds (staging rows) and the survivors it sends
+  std::vector<const Seg*> mine;
+  std::map<uint64_t, size_t> row;
+  for (const Seg& g : plan)
+    if (g.decoder == rank) {
+      row[g.seg] = mine.size();
+      mine.push_back(&g);
+    }
+  int ok = 1;
+  std::string why;
+  std::vector<const uint8_t*> src_ptr;  // per move issued by this rank as a sender / local copy
+  for (const Seg& g : plan)
+    for (int f : g.surv)
+      if (owner(g.seg, f, world) == rank) {
+        const uint8_t* p = locate(user, g.seg, f);
+        if (!p && ok) {
+          ok = 0;
+          why = "locate returned NULL for fragment (" + std::to_string(g.seg) + ", " +
+                std::to_string(f) + ") the placement assigns to rank " + std::to_string(rank);
+        }
+        src_ptr.push_back(p);
+      }
+  if (!mine.empty() && d_out)
+    for (size_t i = 0; i < nlost; ++i)
+      if (row.count(lost_seg[i]) && !d_out[i] && ok) {
+        ok = 0;
+        why = "d_out[" + std::to_string(i) + "] is NULL for a fragment this rank rebuilds";
+      }
+  if (!mine.empty() && !d_out && ok) {
+    ok = 0;
+    why = "d_out is NULL but this rank rebuilds fragments";
+  }
+
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  DI_TRY(hipSetDevice(d->device));
+  struct Restore {
+    int dev;
+    ~Restore() { (void)hipSetDevice(dev); }
+  } restore{prev};
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+
+  // agree before any byte moves: min over ranks of `ok`
+  DI_TRY(hipMemcpyAsync(d->d_flag, &ok, sizeof(int), hipMemcpyHostToDevice, st));
+  NC_TRY(r.all_reduce(d->d_flag, d->d_flag, 1, ncclInt32, ncclMin, d->comm, st));
+  int all_ok = 0;
+  DI_TRY(hipMemcpyAsync(&all_ok, d->d_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+  DI_TRY(hipStreamSynchronize(st));
+  if (!ok) return cec::set_error(CEC_EINVAL, "dist degraded read: " + why);
+  if (!all_ok) return cec::set_error(CEC_EINVAL, "dist degraded read: another rank failed its checks");
+
+  const size_t need = mine.size() * (size_t)n * F;
+  if (need > d->stage_bytes) {
+    DI_TRY(hipFree(d->stage));
+    d->stage = nullptr;
+    d->stage_bytes = 0;
+    DI_TRY(hipMalloc(&d->stage, need));
+    d->stage_bytes = need;
+  }
+  uint8_t* const st_data = d->stage;
+  uint8_t* const st_par = d->stage + mine.size() * (size_t)k * F;
+  auto slot = [&](uint64_t s, int f) {
+    return f < k ? st_data + (row.at(s) * (size_t)k + f) * F
+                 : st_par + (row.at(s) * (size_t)m + (f - k)) * F;
+  };
+
+  // local survivors, then the grouped exchange
+  size_t si = 0;
+  std::vector<std::pair<size_t, int>> sends;  // (src_ptr index, destination rank)
+  for (const Seg& g : plan)
+    for (int f : g.surv) {
+      const int src = owner(g.seg, f, world);
+      if (src != rank) continue;
+      const uint8_t* p = src_ptr[si++];
+      if (g.decoder == rank)
+        DI_TRY(hipMemcpyAsync(slot(g.seg, f), p, F, hipMemcpyDeviceToDevice, st));
+    }
+  NC_TRY(r.group_start());
+  si = 0;
+  for (const Seg& g : plan)
+    for (int f : g.surv) {
+      const int src = owner(g.seg, f, world);
+      if (src == rank) {
+        const uint8_t* p = src_ptr[si++];
+        if (g.decoder != rank) {
+          ncclResult_t res = r.send(p, F, ncclUint8, g.decoder, d->comm, st);
+          if (res != ncclSuccess) {
+            r.group_end();
+            return nccl_err(res, "ncclSend");
+          }
+        }
+      } else if (g.decoder == rank) {
+        ncclResult_t res = r.recv(slot(g.seg, f), F, ncclUint8, src, d->comm, st);
+        if (res != ncclSuccess) {
+          r.group_end();
+          return nccl_err(res, "ncclRecv");
+        }
+      }
+    }
+  NC_TRY(r.group_end());
+
+  size_t rebuilt = 0;
+  if (!mine.empty()) {
+    std::vector<uint8_t> present(mine.size() * n, 0);
+    for (size_t i = 0; i < mine.size(); ++i)
+      for (int f : mine[i]->surv) present[i * n + f] = 1;
+    rc = cec_reconstruct_batch(d->codec, st_data, st_par, mine.size(), F, present.data(), 1, 0, st);
+    if (rc) return rc;
+    for (size_t i = 0; i < nlost; ++i)
+      if (row.count(lost_seg[i])) {
+        DI_TRY(hipMemcpyAsync(d_out[i], slot(lost_seg[i], lost_frag[i]), F,
+                              hipMemcpyDeviceToDevice, st));
+        ++rebuilt;
+      }
+  }
+  DI_TRY(hipStreamSynchronize(st));
+  if (nrebuilt) *nrebuilt = rebuilt;
+  return CEC_OK;
+}
+
+}  // extern "C"

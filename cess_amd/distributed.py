@@ -14,6 +14,7 @@ distinct miners (c-pallets/file-bank/src/functions.rs:187-283, `random_assign_mi
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 from typing import Dict, List, Sequence, Tuple
 
@@ -158,3 +159,87 @@ def degraded_read(plan: GatherPlan, store: FragmentStore, enc, rank: int, group=
         for f in plan.lost[s]:
             out[(s, f)] = sd[i, f] if f < k else sp[i, f - k]
     return out
+
+
+# -- the same exchange through the C ABI (cec_dist_*, for hosts without torch.distributed) -------
+
+def c_plan(lost: Dict[int, Sequence[int]], k: int, m: int, world: int):
+    """cec_dist_plan: (moves [(seg, frag, src, dst)] in issue order, {(seg, frag): decoder rank})
+    of the plan libcessec's degraded read runs for `lost` (host only)."""
+    from ctypes import byref, c_int32, c_size_t, c_uint8, c_uint64
+    from . import _lib
+    from .reedsolomon import check
+    pairs = [(s, f) for s in sorted(lost) for f in lost[s]]
+    segs = (c_uint64 * max(1, len(pairs)))(*[s for s, _ in pairs])
+    frags = (c_uint8 * max(1, len(pairs)))(*[f for _, f in pairs])
+    lib = _lib.load()
+    n = c_size_t()
+    check(lib.cec_dist_plan(k, m, world, segs, frags, len(pairs), None, 0, byref(n), None),
+          "cec_dist_plan")
+    moves = (_lib.DistMove * max(1, n.value))()
+    dec = (c_int32 * max(1, len(pairs)))()
+    check(lib.cec_dist_plan(k, m, world, segs, frags, len(pairs), moves, n.value, byref(n), dec),
+          "cec_dist_plan")
+    return ([(mv.seg, mv.frag, mv.src, mv.dst) for mv in moves[:n.value]],
+            {p: dec[i] for i, p in enumerate(pairs)})
+
+
+class RcclGroup:
+    """cec_dist_*: libcessec's own RCCL group for the degraded read (one per rank; every rank
+    creates it with the same `uid`, made by `RcclGroup.unique_id()` on one rank)."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        from . import _lib
+        from .reedsolomon import check
+        buf = (ctypes.c_uint8 * _lib.CEC_DIST_ID_BYTES)()
+        check(_lib.load().cec_dist_unique_id(buf), "cec_dist_unique_id")
+        return bytes(buf)
+
+    def __init__(self, enc, uid: bytes, world: int, rank: int):
+        from ctypes import byref, c_void_p
+        from . import _lib
+        from .reedsolomon import check
+        self._lib = _lib.load()
+        self._h = c_void_p()
+        self.enc, self.world, self.rank = enc, world, rank
+        idb = (ctypes.c_uint8 * _lib.CEC_DIST_ID_BYTES).from_buffer_copy(uid)
+        check(self._lib.cec_dist_create(enc._h, idb, world, rank, byref(self._h)),
+              "cec_dist_create")
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.cec_dist_destroy(self._h)
+            self._h = None
+
+    def degraded_read(self, lost: Dict[int, Sequence[int]], store: FragmentStore, stream=None):
+        """Rebuild `lost` = {segment: erased fragments} (the same on every rank) from the ranks'
+        stores; returns {(segment, fragment): tensor[F]} of the fragments this rank rebuilt."""
+        import torch
+        from ctypes import byref, c_size_t, c_uint8, c_uint64, c_void_p
+        from . import _lib
+        from .reedsolomon import check, _stream_handle
+        F = store.data.shape[1]
+        pairs = [(s, f) for s in sorted(lost) for f in lost[s]]
+        _, dec = c_plan(lost, self.enc.DataShards, self.enc.ParityShards, self.world)
+        out = {p: torch.empty(F, dtype=torch.uint8, device=store.data.device)
+               for p in pairs if dec[p] == self.rank}
+        segs = (c_uint64 * max(1, len(pairs)))(*[s for s, _ in pairs])
+        frags = (c_uint8 * max(1, len(pairs)))(*[f for _, f in pairs])
+        d_out = (c_void_p * max(1, len(pairs)))(*[out[p].data_ptr() if p in out else None
+                                                   for p in pairs])
+        base, row = store.data.data_ptr(), store.data.stride(0)
+
+        def locate(_user, seg, frag):
+            i = store.slots.get((seg, frag))
+            return None if i is None else base + i * row
+
+        cb = _lib.LOCATE_FN(locate)
+        n = c_size_t()
+        st = _stream_handle(stream if stream is not None
+                            else torch.cuda.current_stream(store.data.device))
+        check(self._lib.cec_dist_degraded_read(self._h, segs, frags, len(pairs), F, cb, None,
+                                               d_out, st, byref(n)), "cec_dist_degraded_read")
+        assert n.value == len(out)
+        return out
+

@@ -214,6 +214,51 @@ int cec_audit_chunks(cec_codec* codec, const uint8_t* d_data, const uint8_t* d_p
                      const uint32_t* indices, uint32_t nidx, uint8_t* d_chunks, uint8_t* d_hex,
                      void* hip_stream);
 
+/* ---- multi-GPU degraded read over RCCL ----------------------------------------
+ * One process (or thread) per GPU, each with its own codec. Fragment f of segment s is stored on
+ * rank (s + f) mod world, the GPU analogue of the chain's miner placement (random_assign_miner,
+ * c-pallets/file-bank/src/functions.rs:187-283: a segment's fragments on distinct miners). A
+ * degraded read brings the first k surviving fragments of every segment with lost fragments to
+ * the rank that owns the segment's first lost fragment (repair restores a fragment where it
+ * lives, restoral_order_complete, c-pallets/file-bank/src/lib.rs:1075-1122) by RCCL point-to-
+ * point over xGMI, and rebuilds the lost fragments there. RCCL is loaded at run time; without it
+ * these return CEC_ENCCL. This is the C form of cess_amd.distributed.degraded_read. */
+#define CEC_DIST_ID_BYTES 128
+typedef struct cec_dist cec_dist;
+/* A fresh group id (on one rank; hand it to the others out of band, e.g. the host's control
+ * plane). */
+int cec_dist_unique_id(uint8_t* id /* CEC_DIST_ID_BYTES */);
+/* Join the group as `rank` of `world` on the codec's device. Collective: every rank calls it
+ * with the same id. The group keeps using `codec` until cec_dist_destroy. */
+int cec_dist_create(cec_codec* codec, const uint8_t* id, int world, int rank, cec_dist** out);
+void cec_dist_destroy(cec_dist* d);
+/* One survivor transfer of a plan: fragment `frag` of segment `seg` from rank src to rank dst
+ * (src == dst: already local). */
+typedef struct cec_dist_move {
+  uint64_t seg;
+  int32_t frag, src, dst;
+} cec_dist_move;
+/* Host only: the plan a degraded read of the lost list runs. The list holds nlost (segment,
+ * fragment) erasures, any order, duplicates allowed, at most m distinct per segment
+ * (CEC_ETOOFEW otherwise; CEC_EINVAL for an index >= k+m). Writes the survivor moves in issue
+ * order (*nmoves of them; CEC_EINVAL if more than moves_cap, moves may be NULL to count) and,
+ * per lost entry, the rank that rebuilds it (decoder, may be NULL). */
+int cec_dist_plan(int k, int m, int world, const uint64_t* lost_seg, const uint8_t* lost_frag,
+                  size_t nlost, cec_dist_move* moves, size_t moves_cap, size_t* nmoves,
+                  int32_t* decoder);
+/* Device address (shard_len bytes) of fragment (seg, frag) held by this rank, NULL if absent. */
+typedef const uint8_t* (*cec_locate_fn)(void* user, uint64_t seg, int frag);
+/* Degraded read. Collective: every rank passes the same lost list. Rank r sends the survivors
+ * the placement puts on it (found through `locate`) and writes every lost fragment it rebuilds,
+ * entry i, to d_out[i] (device, shard_len bytes; entries other ranks rebuild are not touched and
+ * may be NULL; d_out may be NULL on a rank that rebuilds nothing). Before any byte moves the
+ * ranks agree that each found its survivors: a NULL from `locate` fails the call on every rank
+ * with CEC_EINVAL. Work runs on hip_stream; returns when the rebuilt fragments are in d_out.
+ * *nrebuilt (optional) = fragments written on this rank. */
+int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t* lost_frag,
+                           size_t nlost, size_t shard_len, cec_locate_fn locate, void* user,
+                           uint8_t* const* d_out, void* hip_stream, size_t* nrebuilt);
+
 /* ---- on-chain records (host only, no GPU) ---------------------------------------------------
  * SCALE bytes of what the codec's outputs become on chain:
  *   FileBank::upload_declaration(file_hash: Hash, deal_info: BoundedVec<SegmentList,

@@ -102,3 +102,27 @@ def test_degraded_gather_gloo(world, k, m):
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res), res
     assert sum(n for _, _, n in res) == nseg
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (4, 2), (10, 4), (32, 32)])
+def test_c_plan_matches_python_plan(k, m):
+    """cec_dist_plan (the plan libcessec's RCCL degraded read runs, cec_dist_degraded_read) equals
+    plan_gather's for random lost maps (duplicates, up to m erasures, unsorted) at worlds 1..8."""
+    from cess_amd.reedsolomon import CecError, ErrTooFewShards
+    rng = np.random.default_rng(k * 100 + m)
+    n = k + m
+    for world in range(1, 9):
+        lost = {}
+        for s in rng.choice(1000, size=40, replace=False).tolist():
+            e = rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False).tolist()
+            lost[s] = e + e[:1]  # a duplicate entry
+        moves, dec = D.c_plan(lost, k, m, world)
+        plan = D.plan_gather(lost, k, m, world, 1)
+        assert {(s, f): (src, dst) for s, f, src, dst in moves} == plan.moves
+        assert [(s, f) for s, f, _, _ in moves] == sorted(plan.moves)  # the issue order
+        for (s, f), r in dec.items():
+            assert s in plan.segments[r]
+    with pytest.raises(CecError):
+        D.c_plan({3: [n]}, k, m, 2)  # index outside 0..n-1
+    with pytest.raises(ErrTooFewShards):
+        D.c_plan({3: list(range(m + 1))}, k, m, 2)

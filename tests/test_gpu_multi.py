@@ -75,3 +75,101 @@ def test_degraded_read_rccl(k, m):
     assert all(ok for _, ok, _, _ in res), res
     assert sum(n for _, _, n, _ in res) == sum(1 + s % m for s in range(nseg))
     assert res[0][3] > 0  # survivors crossed GPUs
+
+
+def _codewords(k, m, nseg, F, seed=7):
+    from oracle.c_oracle import c_encode, load_c_oracle
+    corc = load_c_oracle()
+    rng = np.random.default_rng(seed)
+    full = []
+    for s in range(nseg):
+        data = [rng.integers(0, 256, F, dtype=np.uint8) for _ in range(k)]
+        full.append(data + c_encode(corc, k, m, data))
+    lost = {s: sorted(rng.choice(k + m, size=1 + s % m, replace=False).tolist())
+            for s in range(nseg)}
+    return full, lost
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (4, 2), (10, 4)])
+def test_c_dist_degraded_read_world1(k, m):
+    """cec_dist_degraded_read (libcessec's own RCCL group, the C form of degraded_read) at world
+    1: plan, agreement all-reduce, local survivor copies, per-segment rebuild and copy-out, every
+    rebuilt fragment equal to the C oracle's codeword; a store missing a survivor fails with
+    CEC_EINVAL before any byte moves."""
+    import torch
+    import cess_amd
+    from cess_amd import distributed as D
+    from cess_amd.reedsolomon import CecError
+    nseg, F = 12, (1 << 20) + 64
+    full, lost = _codewords(k, m, nseg, F)
+    n = k + m
+    mine = D.local_fragments(nseg, n, 1, 0)
+    store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
+                            torch.from_numpy(np.stack([full[s][f] for s, f in mine])).cuda())
+    enc = cess_amd.New(k, m)
+    g = D.RcclGroup(enc, D.RcclGroup.unique_id(), 1, 0)
+    try:
+        out = g.degraded_read(lost, store)
+        assert len(out) == sum(len(v) for v in lost.values())
+        for (s, f), t in out.items():
+            assert np.array_equal(t.cpu().numpy(), full[s][f]), (s, f)
+        out2 = g.degraded_read({3: [0]}, store)  # a second call reuses the staging
+        assert np.array_equal(out2[(3, 0)].cpu().numpy(), full[3][0])
+        gone = D.FragmentStore({sf: i for sf, i in store.slots.items() if sf != (5, k)},
+                               store.data)
+        with pytest.raises(CecError) as ei:
+            g.degraded_read({5: [0]}, gone)
+        assert ei.value.code == -1
+    finally:
+        g.close()
+
+
+def _c_rank(rank, world, uid_path, k, m, nseg, F, q):
+    os.environ.update(HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import time
+    import torch
+    import cess_amd
+    from cess_amd import distributed as D
+    torch.cuda.set_device(rank)
+    full, lost = _codewords(k, m, nseg, F)
+    n = k + m
+    if rank == 0:
+        with open(uid_path + ".tmp", "wb") as f:
+            f.write(D.RcclGroup.unique_id())
+        os.rename(uid_path + ".tmp", uid_path)
+    while not os.path.exists(uid_path):
+        time.sleep(0.05)
+    uid = open(uid_path, "rb").read()
+    mine = D.local_fragments(nseg, n, world, rank)
+    store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
+                            torch.from_numpy(np.stack([full[s][f] for s, f in mine])).cuda())
+    g = D.RcclGroup(cess_amd.New(k, m, device=rank), uid, world, rank)
+    out = g.degraded_read(lost, store)
+    ok = all(np.array_equal(t.cpu().numpy(), full[s][f]) for (s, f), t in out.items())
+    g.close()
+    q.put((rank, ok, len(out)))
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (4, 2)])
+def test_c_dist_degraded_read_rccl(k, m, tmp_path):
+    """The C-ABI degraded read across 2..4 GPUs (one process each, the group id handed over
+    through a file as a non-Python host would through its control plane)."""
+    import torch
+    import torch.multiprocessing as mp
+    world = min(torch.cuda.device_count(), 4)
+    if world < 2:
+        pytest.skip("RCCL degraded read needs >= 2 visible GPUs")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    nseg, F = 12, 1 << 20
+    uid = str(tmp_path / "uid")
+    procs = [ctx.Process(target=_c_rank, args=(r, world, uid, k, m, nseg, F, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res), res
+    assert sum(n for _, _, n in res) == sum(1 + s % m for s in range(nseg))
