@@ -556,6 +556,60 @@ __global__ __launch_bounds__(BS) void k_hg(Layout L, const uint32_t* __restrict_
   if ((L.len % 4) && blockIdx.x == gridDim.x - 1) ct_tail<P, 4>(L, seg);
 }
 
+// ---------------------------------------------------------------------------------------------
+// RS(2,1) single-erasure rebuilds in closed form
+// ---------------------------------------------------------------------------------------------
+// With p = 3*d0 ^ 2*d1 (E row [3, 2]) the matrix form multiplies by 0xF4 / 0xF5 (lost d0) or
+// 0x8E / 0x8F (lost d1): seven xtimes per dword, ~60 issue slots. Solving the two equations
+// directly costs 19 and 14 (left shifts are half-rate on gfx950, right shifts and v_add full):
+//  * lost d0: q = p ^ 2*d1, d0 = q / 3. 3y = y ^ 2y = q gives y = P(q) ^ (P(q)_7 ? 0x0B : 0), P =
+//    prefix XOR of each byte's bits from bit 0 up (0x0B = P(0x1D); P(0x1D)_7 = parity(0x1D) = 0
+//    makes y_7 = P(q)_7);
+//  * lost d1: q = p ^ d0 ^ 2*d0, d1 = q / 2 = (q >> 1) ^ (q_0 ? 0x8E : 0) (0x8E = 2^-1).
+// Bit-exact with the oracle on the goldens (ramp patterns: every byte value) and full-size random
+// segments (tests/test_gpu_parity.py); the formulas were checked for all 256 byte values.
+__device__ __forceinline__ uint32_t gf_div3(uint32_t q) {
+  uint32_t x = __builtin_amdgcn_bitop3_b32(q, add_self(q), 0xFEFEFEFEu, 0x78);  // a ^ (b & c)
+  x = __builtin_amdgcn_bitop3_b32(x, x << 2, 0xFCFCFCFCu, 0x78);
+  x = __builtin_amdgcn_bitop3_b32(x, x << 4, 0xF0F0F0F0u, 0x78);
+  const uint32_t t = x & 0x80808080u;
+  return __builtin_amdgcn_bitop3_b32(x, t - (t >> 7), 0x0B0B0B0Bu, 0x78);
+}
+__device__ __forceinline__ uint32_t gf_div2(uint32_t q) {
+  const uint32_t u = q & 0x01010101u;
+  const uint32_t w = u << 7;
+  const uint32_t y = __builtin_amdgcn_bitop3_b32(q >> 1, w, 0x7F7F7F7Fu, 0xEC);  // (a & c) | b
+  return __builtin_amdgcn_bitop3_b32(y, w - u, 0x0E0E0E0Eu, 0x78);
+}
+template <int MISSING>
+__device__ __forceinline__ uint32_t rs21_rebuild(uint32_t x, uint32_t p) {
+  // x: the surviving data fragment (d1 when MISSING = 0, d0 when MISSING = 1)
+  if constexpr (MISSING == 0) return gf_div3(p ^ xt_fast(x));
+  else return gf_div2(xor3(p, x, xt_fast(x)));
+}
+template <int MISSING, class TV, class LD, class ST>
+__device__ __forceinline__ void ct_column_rs21(LD ld, ST st) {
+  // Dec1CT<2, 1, MISSING> reads its survivors in index order: input 0 = the other data
+  // fragment, input 1 = the parity
+  const TV x = ld(std::integral_constant<int, 0>{}), p = ld(std::integral_constant<int, 1>{});
+  TV y;
+  if constexpr (sizeof(TV) == 16) {
+    y = TV{rs21_rebuild<MISSING>(x.x, p.x), rs21_rebuild<MISSING>(x.y, p.y),
+           rs21_rebuild<MISSING>(x.z, p.z), rs21_rebuild<MISSING>(x.w, p.w)};
+  } else {
+    y = rs21_rebuild<MISSING>(x, p);
+  }
+  st(std::integral_constant<int, 0>{}, y);
+}
+template <class P>
+struct Rs21Closed {
+  static constexpr int missing = -1;
+};
+template <int E>
+struct Rs21Closed<Dec1CT<2, 1, E>> {
+  static constexpr int missing = E < 2 ? E : -1;
+};
+
 // One workgroup's tile (blockIdx.x) of segment `seg`; k_ct and the mixed-pattern kernel below.
 template <class P, int U, bool NT, class TV, int PF, bool WIN, int BS>
 __device__ __forceinline__ void ct_tile(const Layout& L, uint32_t seg) {
@@ -572,7 +626,8 @@ __device__ __forceinline__ void ct_tile(const Layout& L, uint32_t seg) {
     auto st = [&](auto O, TV y) CEC_AI {
       st16<NT, TV>(shard_ptr_ct<P::K, P::v.out[O]>(L, seg) + off, y);
     };
-    if constexpr (use_horner<P>(U)) ct_column_horner<P, TV>(ld, st);
+    if constexpr (Rs21Closed<P>::missing >= 0) ct_column_rs21<Rs21Closed<P>::missing, TV>(ld, st);
+    else if constexpr (use_horner<P>(U)) ct_column_horner<P, TV>(ld, st);
     else if constexpr (WIN) ct_column_window<P, PF, TV>(ld, st);
     else ct_column_stream<P, PF, TV>(ld, st);
   };
