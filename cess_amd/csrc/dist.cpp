@@ -235,18 +235,13 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
   int rc = make_plan(k, m, world, lost_seg, lost_frag, nlost, &plan);
   if (rc) return rc;  // every rank sees the same list, so every rank fails here alike
 
-  // this rank's part: segments it rebuilds (staging rows) and the survivors it sends
-  std::vector<const Seg*> mine;
-  std::map<uint64_t, size_t> row;
-  for (const Seg& g : plan)
-    if (g.decoder == rank) {
-      row[g.seg] = mine.size();
-      mine.push_back(&g);
-    }
+  // lost entries per segment, and this rank's checks: its survivors found, its outputs given
+  std::map<uint64_t, std::vector<size_t>> entries;
+  for (size_t i = 0; i < nlost; ++i) entries[lost_seg[i]].push_back(i);
   int ok = 1;
   std::string why;
-  std::vector<const uint8_t*> src_ptr;  // per move issued by this rank as a sender / local copy
-  for (const Seg& g : plan)
+  std::vector<const uint8_t*> src_ptr;  // survivors this rank holds, in plan order
+  for (const Seg& g : plan) {
     for (int f : g.surv)
       if (owner(g.seg, f, world) == rank) {
         const uint8_t* p = locate(user, g.seg, f);
@@ -257,15 +252,12 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
         }
         src_ptr.push_back(p);
       }
-  if (!mine.empty() && d_out)
-    for (size_t i = 0; i < nlost; ++i)
-      if (row.count(lost_seg[i]) && !d_out[i] && ok) {
-        ok = 0;
-        why = "d_out[" + std::to_string(i) + "] is NULL for a fragment this rank rebuilds";
-      }
-  if (!mine.empty() && !d_out && ok) {
-    ok = 0;
-    why = "d_out is NULL but this rank rebuilds fragments";
+    if (g.decoder == rank)
+      for (size_t i : entries[g.seg])
+        if ((!d_out || !d_out[i]) && ok) {
+          ok = 0;
+          why = "no output buffer for lost entry " + std::to_string(i) + ", rebuilt on this rank";
+        }
   }
 
   int prev = 0;
@@ -284,69 +276,77 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
   DI_TRY(hipMemcpyAsync(&all_ok, d->d_flag, sizeof(int), hipMemcpyDeviceToHost, st));
   DI_TRY(hipStreamSynchronize(st));
   if (!ok) return cec::set_error(CEC_EINVAL, "dist degraded read: " + why);
-  if (!all_ok) return cec::set_error(CEC_EINVAL, "dist degraded read: another rank failed its checks");
+  if (!all_ok)
+    return cec::set_error(CEC_EINVAL, "dist degraded read: another rank failed its checks");
 
-  const size_t need = mine.size() * (size_t)n * F;
-  if (need > d->stage_bytes) {
-    DI_TRY(hipFree(d->stage));
-    d->stage = nullptr;
-    d->stage_bytes = 0;
-    DI_TRY(hipMalloc(&d->stage, need));
-    d->stage_bytes = need;
-  }
-  uint8_t* const st_data = d->stage;
-  uint8_t* const st_par = d->stage + mine.size() * (size_t)k * F;
-  auto slot = [&](uint64_t s, int f) {
-    return f < k ? st_data + (row.at(s) * (size_t)k + f) * F
-                 : st_par + (row.at(s) * (size_t)m + (f - k)) * F;
-  };
-
-  // local survivors, then the grouped exchange
-  size_t si = 0;
-  std::vector<std::pair<size_t, int>> sends;  // (src_ptr index, destination rank)
-  for (const Seg& g : plan)
-    for (int f : g.surv) {
-      const int src = owner(g.seg, f, world);
-      if (src != rank) continue;
-      const uint8_t* p = src_ptr[si++];
-      if (g.decoder == rank)
-        DI_TRY(hipMemcpyAsync(slot(g.seg, f), p, F, hipMemcpyDeviceToDevice, st));
+  // Rounds of at most kRound segments of the plan (the same split on every rank) bound the
+  // staging batch; rounds follow each other on the stream, so a round's receives land after the
+  // previous round's rebuild has read the staging.
+  constexpr size_t kRound = 256;
+  size_t rebuilt = 0, si = 0;
+  for (size_t r0 = 0; r0 < plan.size(); r0 += kRound) {
+    const size_t r1 = std::min(plan.size(), r0 + kRound);
+    std::vector<const Seg*> mine;
+    std::map<uint64_t, size_t> row;
+    for (size_t i = r0; i < r1; ++i)
+      if (plan[i].decoder == rank) {
+        row[plan[i].seg] = mine.size();
+        mine.push_back(&plan[i]);
+      }
+    const size_t need = mine.size() * (size_t)n * F;
+    if (need > d->stage_bytes) {
+      DI_TRY(hipStreamSynchronize(st));  // the old staging may still be read by queued work
+      DI_TRY(hipFree(d->stage));
+      d->stage = nullptr;
+      d->stage_bytes = 0;
+      DI_TRY(hipMalloc(&d->stage, need));
+      d->stage_bytes = need;
     }
-  NC_TRY(r.group_start());
-  si = 0;
-  for (const Seg& g : plan)
-    for (int f : g.surv) {
-      const int src = owner(g.seg, f, world);
-      if (src == rank) {
-        const uint8_t* p = src_ptr[si++];
-        if (g.decoder != rank) {
-          ncclResult_t res = r.send(p, F, ncclUint8, g.decoder, d->comm, st);
-          if (res != ncclSuccess) {
-            r.group_end();
-            return nccl_err(res, "ncclSend");
-          }
+    uint8_t* const st_data = d->stage;
+    uint8_t* const st_par = d->stage + mine.size() * (size_t)k * F;
+    auto slot = [&](uint64_t s, int f) {
+      return f < k ? st_data + (row.at(s) * (size_t)k + f) * F
+                   : st_par + (row.at(s) * (size_t)m + (f - k)) * F;
+    };
+    // local survivors, then the grouped exchange (sends and receives in plan order)
+    size_t sj = si;
+    for (size_t i = r0; i < r1; ++i)
+      for (int f : plan[i].surv)
+        if (owner(plan[i].seg, f, world) == rank) {
+          const uint8_t* p = src_ptr[sj++];
+          if (plan[i].decoder == rank)
+            DI_TRY(hipMemcpyAsync(slot(plan[i].seg, f), p, F, hipMemcpyDeviceToDevice, st));
         }
-      } else if (g.decoder == rank) {
-        ncclResult_t res = r.recv(slot(g.seg, f), F, ncclUint8, src, d->comm, st);
+    NC_TRY(r.group_start());
+    for (size_t i = r0; i < r1; ++i) {
+      const Seg& g = plan[i];
+      for (int f : g.surv) {
+        const int src = owner(g.seg, f, world);
+        ncclResult_t res = ncclSuccess;
+        if (src == rank) {
+          const uint8_t* p = src_ptr[si++];
+          if (g.decoder != rank) res = r.send(p, F, ncclUint8, g.decoder, d->comm, st);
+        } else if (g.decoder == rank) {
+          res = r.recv(slot(g.seg, f), F, ncclUint8, src, d->comm, st);
+        }
         if (res != ncclSuccess) {
           r.group_end();
-          return nccl_err(res, "ncclRecv");
+          return nccl_err(res, src == rank ? "ncclSend" : "ncclRecv");
         }
       }
     }
-  NC_TRY(r.group_end());
-
-  size_t rebuilt = 0;
-  if (!mine.empty()) {
+    NC_TRY(r.group_end());
+    if (mine.empty()) continue;
     std::vector<uint8_t> present(mine.size() * n, 0);
     for (size_t i = 0; i < mine.size(); ++i)
       for (int f : mine[i]->surv) present[i * n + f] = 1;
-    rc = cec_reconstruct_batch(d->codec, st_data, st_par, mine.size(), F, present.data(), 1, 0, st);
+    rc = cec_reconstruct_batch(d->codec, st_data, st_par, mine.size(), F, present.data(), 1, 0,
+                               st);
     if (rc) return rc;
-    for (size_t i = 0; i < nlost; ++i)
-      if (row.count(lost_seg[i])) {
-        DI_TRY(hipMemcpyAsync(d_out[i], slot(lost_seg[i], lost_frag[i]), F,
-                              hipMemcpyDeviceToDevice, st));
+    for (const Seg* g : mine)
+      for (size_t i : entries[g->seg]) {
+        DI_TRY(hipMemcpyAsync(d_out[i], slot(g->seg, lost_frag[i]), F, hipMemcpyDeviceToDevice,
+                              st));
         ++rebuilt;
       }
   }

@@ -220,6 +220,7 @@ class RcclGroup:
         from . import _lib
         from .reedsolomon import check, _stream_handle
         F = store.data.shape[1]
+        lost = {s: sorted(set(v)) for s, v in lost.items() if len(v)}
         pairs = [(s, f) for s in sorted(lost) for f in lost[s]]
         _, dec = c_plan(lost, self.enc.DataShards, self.enc.ParityShards, self.world)
         out = {p: torch.empty(F, dtype=torch.uint8, device=store.data.device)

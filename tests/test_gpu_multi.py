@@ -90,17 +90,17 @@ def _codewords(k, m, nseg, F, seed=7):
     return full, lost
 
 
-@pytest.mark.parametrize("k,m", [(2, 1), (4, 2), (10, 4)])
-def test_c_dist_degraded_read_world1(k, m):
+@pytest.mark.parametrize("k,m,nseg,F", [(2, 1, 12, (1 << 20) + 64), (4, 2, 12, (1 << 20) + 64),
+                                         (10, 4, 12, (1 << 20) + 64), (2, 1, 600, 65536)])
+def test_c_dist_degraded_read_world1(k, m, nseg, F):
     """cec_dist_degraded_read (libcessec's own RCCL group, the C form of degraded_read) at world
     1: plan, agreement all-reduce, local survivor copies, per-segment rebuild and copy-out, every
     rebuilt fragment equal to the C oracle's codeword; a store missing a survivor fails with
-    CEC_EINVAL before any byte moves."""
+    CEC_EINVAL before any byte moves. 600 segments take three rounds of the bounded staging."""
     import torch
     import cess_amd
     from cess_amd import distributed as D
     from cess_amd.reedsolomon import CecError
-    nseg, F = 12, (1 << 20) + 64
     full, lost = _codewords(k, m, nseg, F)
     n = k + m
     mine = D.local_fragments(nseg, n, 1, 0)
