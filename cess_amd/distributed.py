@@ -212,6 +212,18 @@ class RcclGroup:
             self._lib.cec_dist_destroy(self._h)
             self._h = None
 
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
     def degraded_read(self, lost: Dict[int, Sequence[int]], store: FragmentStore, stream=None):
         """Rebuild `lost` = {segment: erased fragments} (the same on every rank) from the ranks'
         stores; returns {(segment, fragment): tensor[F]} of the fragments this rank rebuilt."""
