@@ -543,6 +543,14 @@ def main() -> None:
                                 "); the timed region ends with the window drained",
                     "note": "SHA-256 is one sequential chain per fragment: bounded by streams x "
                             "per-wave issue rate, reported apart from the HBM roofline"}
+        try:  # measured HBM bytes of a whole step (both kernels), profiles/traffic_c5_step.json
+            with open(os.path.join(ROOT, "profiles", "traffic_c5_step.json")) as f:
+                st = json.load(f)
+            sha_note["step_traffic"] = {"bytes": st["step_bytes"],
+                                        "over_algorithmic": round(st["step_over_algorithmic"], 3),
+                                        "note": "encode 1x + the ticks' re-read of every fragment"}
+        except (OSError, ValueError, KeyError):
+            pass
         slots = load_valu_slots("c5")
         if slots:
             # the step's hashing against the VALU issue roofline: every block of every fragment
