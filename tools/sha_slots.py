@@ -2,8 +2,9 @@
 """VALU instructions and issue slots per 64-byte block of the one-wave hash-queue tick
 (k_sha256_tick1), counted on the built gfx950 code object: the instructions of its block loop
 (the backward branch whose range holds the most v_alignbit), weighted by the issue costs
-measured with tools/valu_bench.hip (profiles/r01/valu_bench_*.jsonl: shifts, v_alignbit,
-v_add3, v_perm and v_lshl_or issue at half rate; v_add, v_bitop3, logic ops at full rate).
+measured with tools/valu_bench.hip (profiles/r01/valu_bench_*.jsonl: left shifts, v_alignbit,
+v_add3, v_perm, v_bfe and v_lshl_or issue at half rate; right shifts, v_add, v_bitop3 and the
+logic ops at full rate).
 The loop range includes the general-path branch (unaligned / padding blocks), a few dozen
 instructions the fast path skips, so the figures are a slight upper bound.
 
@@ -16,8 +17,8 @@ import sys
 import tempfile
 
 B = "/opt/rocm/lib/llvm/bin"
-HALF = ("v_alignbit_b32", "v_add3_u32", "v_lshlrev_b32", "v_lshrrev_b32", "v_lshl_or_b32",
-        "v_perm_b32", "v_lshl_add_u32", "v_bfe_u32", "v_alignbyte_b32")
+HALF = ("v_alignbit_b32", "v_add3_u32", "v_lshlrev_b32", "v_lshl_or_b32", "v_perm_b32",
+        "v_lshl_add_u32", "v_bfe_u32", "v_alignbyte_b32", "v_xad_u32", "v_mul_u32_u24")
 KERNEL = r"k_sha256_tick1"
 
 
