@@ -164,7 +164,10 @@ __device__ __forceinline__ void st32(uint8_t* p, const uint32_t (&w)[8]) {
 // RS(32,32) encode, one lane pair per 32 byte columns of a segment (blockIdx.y = segment): a wave's
 // 32 pairs cover 1 KiB of columns (pair p: bytes 16p..16p+15 and 512+16p..), so shard_len must be
 // a multiple of 1024 with 16-byte aligned shards (checked by the launcher).
-template <bool NT, bool NTS = NT>
+// DIAG (tuning build only): 1 = no butterflies (transposes, loads and stores only), 2 = loads and
+// stores only; the outputs are then not parity. They measure what the memory side alone costs at
+// this access pattern (with LDS > 0 at the kernel's own occupancy of 3 waves per SIMD).
+template <bool NT, bool NTS = NT, int DIAG = 0>
 __global__ __launch_bounds__(256) void k_fft3232(Layout L, const uint32_t* __restrict__ seg_list,
                                                  uint32_t seg0) {
   constexpr int K = 5;
@@ -182,7 +185,18 @@ __global__ __launch_bounds__(256) void k_fft3232(Layout L, const uint32_t* __res
 
   uint32_t X[16][8];
   sfor<16>([&](auto J) CEC_FFT_AI { ld32<NT>(din + J * step, X[J]); });
+  if constexpr (DIAG == 2) {
+    sfor<16>([&](auto J) CEC_FFT_AI { st32<NTS>(dout + J * step, X[J]); });
+    return;
+  }
   sfor<16>([&](auto J) CEC_FFT_AI { tr8(X[J]); });
+  if constexpr (DIAG == 1) {
+    sfor<16>([&](auto J) CEC_FFT_AI {
+      tr8(X[J]);
+      st32<NTS>(dout + J * step, X[J]);
+    });
+    return;
+  }
 
   // IFFT layer 0 (positions 2j, 2j + 1: across the lane pair): b ^= a; a ^= s*b.
   // Z = a ^ b on both lanes; even lane -> a ^ s*Z, odd lane -> Z.
@@ -248,9 +262,22 @@ bool launch_fft_rs3232(const Layout& L, const uint32_t* seg_list, uint32_t nseg,
   const uint64_t gx = (lanes + 255) / 256;
   for (uint32_t s0 = 0; s0 < nseg; s0 += 65535) {
     const uint32_t ny = nseg - s0 < 65535 ? nseg - s0 : 65535;
-    // nt: bit 0 = nontemporal loads, bit 1 = nontemporal stores
+    // nt: bit 0 = nontemporal loads, bit 1 = nontemporal stores; tuning build only: bits 2-3 =
+    // DIAG, bit 4 = 48 KiB of LDS per workgroup (caps a CU at 3 workgroups = 3 waves per SIMD)
     switch (nt & 3) {
       case 3:
+#ifdef CEC_TUNING
+        if (nt & 12) {
+          const unsigned lds = (nt & 16) ? 48 * 1024 : 0;
+          if ((nt & 12) == 4)
+            hipLaunchKernelGGL((k_fft3232<true, true, 1>), dim3((unsigned)gx, ny), dim3(256), lds,
+                               st, L, seg_list, s0);
+          else
+            hipLaunchKernelGGL((k_fft3232<true, true, 2>), dim3((unsigned)gx, ny), dim3(256), lds,
+                               st, L, seg_list, s0);
+          break;
+        }
+#endif
         hipLaunchKernelGGL((k_fft3232<true, true>), dim3((unsigned)gx, ny), dim3(256), 0, st, L,
                            seg_list, s0);
         break;

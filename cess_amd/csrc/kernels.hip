@@ -1248,6 +1248,13 @@ void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_
                             st))
         return;
       break;
+    case 25: case 26: case 27: case 28:  // FFT memory-side diagnostics (outputs are not parity):
+      // no butterflies / loads+stores only, at the natural occupancy / capped at 3 waves per SIMD
+      if (P::NI == 32 && P::NO == 32 &&
+          launch_fft_rs3232(L, seg_list, nseg,
+                            3 | (o.ct_variant & 1 ? 4 : 8) | (o.ct_variant >= 27 ? 16 : 0), st))
+        return;
+      break;
     default: break;
   }
 #else
@@ -1262,7 +1269,7 @@ void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_
 }  // namespace
 
 #ifdef CEC_TUNING
-int max_ct_variant() { return 24; }
+int max_ct_variant() { return 28; }
 #else
 int max_ct_variant() { return 0; }
 #endif
