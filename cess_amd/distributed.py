@@ -100,7 +100,8 @@ def gather_survivors(plan: GatherPlan, store: FragmentStore, k: int, m: int, ran
                      group=None):
     """Run the gather for this rank. Returns (staging_data [nseg_d][k][F],
     staging_parity [nseg_d][m][F], present [nseg_d][k+m], segment list) on the decoding rank;
-    the staging tensors hold every used survivor at its shard index (erased slots zero).
+    the staging tensors hold every used survivor at its shard index; the other slots are left
+    uninitialised (the rebuild writes every shard not marked present).
     Non-decoding ranks only send and return None for the staging tensors."""
     import torch
     import torch.distributed as dist
@@ -109,8 +110,8 @@ def gather_survivors(plan: GatherPlan, store: FragmentStore, k: int, m: int, ran
     dev = store.data.device
     mysegs = plan.segments.get(rank, [])
     row = {s: i for i, s in enumerate(mysegs)}
-    sd = torch.zeros((len(mysegs), k, F), dtype=torch.uint8, device=dev)
-    sp = torch.zeros((len(mysegs), m, F), dtype=torch.uint8, device=dev)
+    sd = torch.empty((len(mysegs), k, F), dtype=torch.uint8, device=dev)
+    sp = torch.empty((len(mysegs), m, F), dtype=torch.uint8, device=dev)
 
     def dst_view(s, f):
         return sd[row[s], f] if f < k else sp[row[s], f - k]

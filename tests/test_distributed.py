@@ -77,8 +77,7 @@ def _worker(rank, world, port, k, m, nseg, F, q):
                 ok &= np.array_equal(got, full[s][f])
                 shards.append(got.copy())
             else:
-                ok &= not got.any()
-                shards.append(None)
+                shards.append(None)  # unused slot (uninitialised staging)
         rec = rs.reconstruct(shards)
         ok &= all(np.array_equal(rec[f], full[s][f]) for f in lost[s])
     q.put((rank, ok, len(segs)))
