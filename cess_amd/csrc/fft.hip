@@ -165,7 +165,8 @@ __device__ __forceinline__ void st32(uint8_t* p, const uint32_t (&w)[8]) {
 // 32 pairs cover 1 KiB of columns (pair p: bytes 16p..16p+15 and 512+16p..), so shard_len must be
 // a multiple of 1024 with 16-byte aligned shards (checked by the launcher).
 // DIAG (tuning build only): 1 = no butterflies (transposes, loads and stores only), 2 = loads and
-// stores only; the outputs are then not parity. They measure what the memory side alone costs at
+// stores only, 3 = the same 4 shards at a time (few VGPRs, full occupancy); the outputs are then
+// not parity. They measure what the memory side alone costs at
 // this access pattern (with LDS > 0 at the kernel's own occupancy of 3 waves per SIMD).
 template <bool NT, bool NTS = NT, int DIAG = 0>
 __global__ __launch_bounds__(256) void k_fft3232(Layout L, const uint32_t* __restrict__ seg_list,
@@ -183,6 +184,14 @@ __global__ __launch_bounds__(256) void k_fft3232(Layout L, const uint32_t* __res
   uint8_t* dout = L.parity + seg * L.par_seg_stride + l * L.shard_stride + col;
   const uint64_t step = 2 * L.shard_stride;  // position t -> t + 2
 
+  if constexpr (DIAG == 3) {  // loads and stores only, 4 shards at a time (few VGPRs, 8 waves)
+    sfor<4>([&](auto H) CEC_FFT_AI {
+      uint32_t Y[4][8];
+      sfor<4>([&](auto J) CEC_FFT_AI { ld32<NT>(din + (4 * H + J) * step, Y[J]); });
+      sfor<4>([&](auto J) CEC_FFT_AI { st32<NTS>(dout + (4 * H + J) * step, Y[J]); });
+    });
+    return;
+  }
   uint32_t X[16][8];
   sfor<16>([&](auto J) CEC_FFT_AI { ld32<NT>(din + J * step, X[J]); });
   if constexpr (DIAG == 2) {
@@ -271,6 +280,9 @@ bool launch_fft_rs3232(const Layout& L, const uint32_t* seg_list, uint32_t nseg,
           const unsigned lds = (nt & 16) ? 48 * 1024 : 0;
           if ((nt & 12) == 4)
             hipLaunchKernelGGL((k_fft3232<true, true, 1>), dim3((unsigned)gx, ny), dim3(256), lds,
+                               st, L, seg_list, s0);
+          else if ((nt & 12) == 12)
+            hipLaunchKernelGGL((k_fft3232<true, true, 3>), dim3((unsigned)gx, ny), dim3(256), lds,
                                st, L, seg_list, s0);
           else
             hipLaunchKernelGGL((k_fft3232<true, true, 2>), dim3((unsigned)gx, ny), dim3(256), lds,

@@ -1248,11 +1248,16 @@ void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_
                             st))
         return;
       break;
-    case 25: case 26: case 27: case 28:  // FFT memory-side diagnostics (outputs are not parity):
-      // no butterflies / loads+stores only, at the natural occupancy / capped at 3 waves per SIMD
+    case 25: case 26: case 27: case 28: case 29: case 30:
+      // FFT memory-side diagnostics (outputs are not parity): no butterflies / loads+stores only,
+      // at the natural occupancy / capped at 3 waves per SIMD; 29/30: loads+stores 4 shards at a
+      // time, uncapped / capped
       if (P::NI == 32 && P::NO == 32 &&
           launch_fft_rs3232(L, seg_list, nseg,
-                            3 | (o.ct_variant & 1 ? 4 : 8) | (o.ct_variant >= 27 ? 16 : 0), st))
+                            3 | (o.ct_variant >= 29 ? 12 : o.ct_variant & 1 ? 4 : 8) |
+                                ((o.ct_variant == 27 || o.ct_variant == 28 || o.ct_variant == 30)
+                                     ? 16 : 0),
+                            st))
         return;
       break;
     default: break;
@@ -1269,7 +1274,7 @@ void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_
 }  // namespace
 
 #ifdef CEC_TUNING
-int max_ct_variant() { return 28; }
+int max_ct_variant() { return 30; }
 #else
 int max_ct_variant() { return 0; }
 #endif
