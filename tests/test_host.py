@@ -264,3 +264,12 @@ def test_sha_tick_slot_count_matches_library():
     assert rec["kernel"] == sym
     assert rec["valu_instr_per_block"] == sum(ops.values())
     assert ops["v_alignbit_b32"] >= 64 * 6 + 48 * 4  # every rotate of the rounds and schedule
+
+
+def test_rust_crate_declares_every_header_symbol():
+    """utils/ec-hip (not compiled here: no rustc) declares every C-ABI entry point of the header."""
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "utils", "ec-hip", "src", "lib.rs")) as f:
+        rs = set(re.findall(r"pub fn (cec_[a-z0-9_]+)\s*\(", f.read()))
+    assert rs == set(header_symbols())

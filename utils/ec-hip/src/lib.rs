@@ -70,6 +70,157 @@ extern "C" {
                                out_len: *mut usize) -> c_int;
 }
 
+/// The rest of `include/cess_ec.h`, declared one to one (HBM-resident batches, hash queue,
+/// audit chunks, records, the multi-GPU degraded read). Device pointers are `*mut u8` /
+/// `*const u8`; HIP streams are `*mut c_void` (null = the null stream).
+pub mod sys {
+    use super::{cec_codec, c_char, c_int, c_void};
+
+    #[repr(C)]
+    pub struct cec_hashq {
+        _p: [u8; 0],
+    }
+    #[repr(C)]
+    pub struct cec_dist {
+        _p: [u8; 0],
+    }
+    #[repr(C)]
+    #[derive(Clone, Copy, Debug, Default)]
+    pub struct cec_dist_move {
+        pub seg: u64,
+        pub frag: i32,
+        pub src: i32,
+        pub dst: i32,
+    }
+    pub const CEC_DIST_ID_BYTES: usize = 128;
+    pub type cec_locate_fn = extern "C" fn(user: *mut c_void, seg: u64, frag: c_int) -> *const u8;
+
+    extern "C" {
+        pub fn cec_version() -> *const c_char;
+        pub fn cec_device_count() -> c_int;
+        pub fn cec_codec_info(c: *const cec_codec, k: *mut c_int, m: *mut c_int,
+                              device: *mut c_int) -> c_int;
+        pub fn cec_matrix(c: *const cec_codec, out: *mut u8) -> c_int;
+        pub fn cec_encode_batch(c: *mut cec_codec, d_data: *const u8, d_parity: *mut u8,
+                                nseg: usize, shard_len: usize, stream: *mut c_void) -> c_int;
+        pub fn cec_reconstruct_batch(c: *mut cec_codec, d_data: *mut u8, d_parity: *mut u8,
+                                     nseg: usize, shard_len: usize, present: *const u8,
+                                     per_segment: c_int, data_only: c_int,
+                                     stream: *mut c_void) -> c_int;
+        pub fn cec_sha256_batch(c: *mut cec_codec, d_data: *const u8, d_parity: *const u8,
+                                nseg: usize, shard_len: usize, d_hex: *mut u8,
+                                stream: *mut c_void) -> c_int;
+        pub fn cec_sha256_hex(d_bufs: *const *const u8, n: usize, len: usize, hex: *mut u8,
+                              stream: *mut c_void) -> c_int;
+        pub fn cec_hashq_create(device: c_int, capacity: usize, stream: *mut c_void,
+                                out: *mut *mut cec_hashq) -> c_int;
+        pub fn cec_hashq_destroy(q: *mut cec_hashq);
+        pub fn cec_hashq_add(q: *mut cec_hashq, d_base: *const u8, n: usize, per: usize,
+                             outer_stride: usize, inner_stride: usize, len: usize,
+                             d_hex: *mut u8, hex_outer: usize, ticket: *mut u64) -> c_int;
+        pub fn cec_hashq_add_prefix(q: *mut cec_hashq, d_base: *const u8, n: usize, per: usize,
+                                    outer_stride: usize, inner_stride: usize, len: usize,
+                                    d_hex: *mut u8, hex_outer: usize, prefix_len: usize,
+                                    d_prefix_hex: *mut u8, prefix_hex_outer: usize,
+                                    ticket: *mut u64) -> c_int;
+        pub fn cec_hashq_tick(q: *mut cec_hashq, max_blocks: u32) -> c_int;
+        pub fn cec_hashq_finish(q: *mut cec_hashq) -> c_int;
+        pub fn cec_hashq_status(q: *const cec_hashq, ticket: u64, done: *mut c_int,
+                                live_chains: *mut usize, blocks_left: *mut u64) -> c_int;
+        pub fn cec_hashq_set_option(q: *mut cec_hashq, option: c_int, value: c_int) -> c_int;
+        pub fn cec_split_segment(seg: *const u8, seg_len: usize, k: c_int,
+                                 shards: *const *mut u8, shard_len: usize) -> c_int;
+        pub fn cec_challenge_indices(randoms: *const u64, nrand: usize, chunk_count: u32,
+                                     need: u32, out: *mut u32, used: *mut usize) -> c_int;
+        pub fn cec_audit_chunks(c: *mut cec_codec, d_data: *const u8, d_parity: *const u8,
+                                nseg: usize, shard_len: usize, chunk_count: u32,
+                                indices: *const u32, nidx: u32, d_chunks: *mut u8,
+                                d_hex: *mut u8, stream: *mut c_void) -> c_int;
+        pub fn cec_scale_compact(n: u32, out: *mut u8, out_cap: usize, out_len: *mut usize)
+                                 -> c_int;
+        pub fn cec_scale_upload_declaration(file_hash_hex: *const u8, seg_hex: *const u8,
+                                            frag_hex: *const u8, nseg: usize, nfrag: usize,
+                                            account: *const u8, file_name: *const u8,
+                                            file_name_len: usize, bucket_name: *const u8,
+                                            bucket_name_len: usize, out: *mut u8,
+                                            out_cap: usize, out_len: *mut usize) -> c_int;
+        pub fn cec_shard_id(hash_hex: *const u8, index: u32, out68: *mut u8) -> c_int;
+        pub fn cec_hash_from_shard_id(shard_id68: *const u8, hash_hex_out: *mut u8) -> c_int;
+        pub fn cec_fill_synthetic(d_out: *mut u8, seg_bytes: usize, nseg: usize, seg0: u64,
+                                  seed: u64, stream: *mut c_void) -> c_int;
+        pub fn cec_set_option(c: *mut cec_codec, option: c_int, value: c_int) -> c_int;
+        pub fn cec_get_stat(c: *const cec_codec, stat: c_int, value: *mut u64) -> c_int;
+        pub fn cec_dist_unique_id(id: *mut u8) -> c_int;
+        pub fn cec_dist_create(c: *mut cec_codec, id: *const u8, world: c_int, rank: c_int,
+                               out: *mut *mut cec_dist) -> c_int;
+        pub fn cec_dist_destroy(d: *mut cec_dist);
+        pub fn cec_dist_plan(k: c_int, m: c_int, world: c_int, lost_seg: *const u64,
+                             lost_frag: *const u8, nlost: usize, moves: *mut cec_dist_move,
+                             moves_cap: usize, nmoves: *mut usize, decoder: *mut i32) -> c_int;
+        pub fn cec_dist_degraded_read(d: *mut cec_dist, lost_seg: *const u64,
+                                      lost_frag: *const u8, nlost: usize, shard_len: usize,
+                                      locate: cec_locate_fn, user: *mut c_void,
+                                      d_out: *const *mut u8, stream: *mut c_void,
+                                      nrebuilt: *mut usize) -> c_int;
+    }
+}
+
+/// One rank's share of the multi-GPU degraded read (libcessec's own RCCL group): fragment f of
+/// segment s lives on rank (s + f) mod world (random_assign_miner's spread,
+/// c-pallets/file-bank/src/functions.rs:187-283).
+pub struct DistGroup<'c> {
+    d: *mut sys::cec_dist,
+    _codec: std::marker::PhantomData<&'c ReedSolomon>,
+}
+
+extern "C" fn locate_cb(user: *mut c_void, seg: u64, frag: c_int) -> *const u8 {
+    let f = unsafe { &mut *(user as *mut &mut dyn FnMut(u64, usize) -> *const u8) };
+    f(seg, frag as usize)
+}
+
+impl<'c> DistGroup<'c> {
+    /// A fresh group id (on one rank; hand it to the others out of band).
+    pub fn unique_id() -> Result<[u8; sys::CEC_DIST_ID_BYTES], Error> {
+        let mut id = [0u8; sys::CEC_DIST_ID_BYTES];
+        check(unsafe { sys::cec_dist_unique_id(id.as_mut_ptr()) })?;
+        Ok(id)
+    }
+
+    /// Join as `rank` of `world` (collective over the ranks).
+    pub fn join(codec: &'c ReedSolomon, id: &[u8; sys::CEC_DIST_ID_BYTES], world: i32,
+                rank: i32) -> Result<Self, Error> {
+        let mut d = std::ptr::null_mut();
+        check(unsafe { sys::cec_dist_create(codec.c, id.as_ptr(), world, rank, &mut d) })?;
+        Ok(DistGroup { d, _codec: std::marker::PhantomData })
+    }
+
+    /// Rebuild the `lost` (segment, fragment) list, the same on every rank; `locate(seg, frag)`
+    /// gives the device address of a fragment this rank holds (null if absent); `out[i]` receives
+    /// lost entry i when this rank rebuilds it. Returns the number rebuilt here.
+    pub fn degraded_read(&mut self, lost: &[(u64, u8)], shard_len: usize,
+                         mut locate: impl FnMut(u64, usize) -> *const u8,
+                         out: &[*mut u8]) -> Result<usize, Error> {
+        let segs: Vec<u64> = lost.iter().map(|l| l.0).collect();
+        let frags: Vec<u8> = lost.iter().map(|l| l.1).collect();
+        let mut f: &mut dyn FnMut(u64, usize) -> *const u8 = &mut locate;
+        let mut n = 0usize;
+        check(unsafe {
+            sys::cec_dist_degraded_read(self.d, segs.as_ptr(), frags.as_ptr(), lost.len(),
+                                        shard_len, locate_cb,
+                                        &mut f as *mut _ as *mut c_void,
+                                        if out.is_empty() { std::ptr::null() } else { out.as_ptr() },
+                                        std::ptr::null_mut(), &mut n)
+        })?;
+        Ok(n)
+    }
+}
+
+impl Drop for DistGroup<'_> {
+    fn drop(&mut self) {
+        unsafe { sys::cec_dist_destroy(self.d) }
+    }
+}
+
 pub const CEC_ETOOFEW: c_int = -2;
 pub const CEC_ESHARDLEN: c_int = -3;
 pub const CEC_ESEGCOUNT: c_int = -9;
