@@ -168,15 +168,10 @@ __device__ __forceinline__ void st32(uint8_t* p, const uint32_t (&w)[8]) {
 // stores only, 3 = the same 4 shards at a time (few VGPRs, full occupancy); the outputs are then
 // not parity. They measure what the memory side alone costs at
 // this access pattern (with LDS > 0 at the kernel's own occupancy of 3 waves per SIMD).
-template <bool NT, bool NTS = NT, int DIAG = 0>
-__global__ __launch_bounds__(256) void k_fft3232(Layout L, const uint32_t* __restrict__ seg_list,
-                                                 uint32_t seg0) {
+template <bool NT, bool NTS, int DIAG>
+__device__ __forceinline__ void fft_cols(const Layout& L, uint32_t seg, uint64_t col) {
   constexpr int K = 5;
   using T = Lch<K>;
-  const uint32_t seg = seg_list ? seg_list[seg0 + blockIdx.y] : seg0 + blockIdx.y;
-  const uint64_t gp = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 1;  // lane pair
-  const uint64_t col = (gp >> 5) * 1024 + (gp & 31) * 16;
-  if (col >= L.len) return;  // whole waves leave together
   const uint32_t l = threadIdx.x & 1;
   const uint32_t em = l ? 0u : 0xFFFFFFFFu;  // even lane (positions 2j)
   const uint32_t om = ~em;
@@ -262,6 +257,28 @@ __global__ __launch_bounds__(256) void k_fft3232(Layout L, const uint32_t* __res
   });
 }
 
+// CPW (tuning build only, else 1): column blocks of 4 KiB per workgroup, walked in a loop, so the
+// workgroups resident at once cover fewer segments.
+template <bool NT, bool NTS = NT, int DIAG = 0, int CPW = 1>
+__global__ __launch_bounds__(256) void k_fft3232(Layout L, const uint32_t* __restrict__ seg_list,
+                                                 uint32_t seg0) {
+  const uint32_t seg = seg_list ? seg_list[seg0 + blockIdx.y] : seg0 + blockIdx.y;
+  if constexpr (CPW == 1) {
+    const uint64_t gp = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 1;  // lane pair
+    const uint64_t col = (gp >> 5) * 1024 + (gp & 31) * 16;
+    if (col >= L.len) return;  // whole waves leave together
+    fft_cols<NT, NTS, DIAG>(L, seg, col);
+  } else {
+    for (int it = 0; it < CPW; ++it) {
+      const uint64_t gp = (((uint64_t)blockIdx.x * CPW + it) * 256 + threadIdx.x) >> 1;
+      const uint64_t col = (gp >> 5) * 1024 + (gp & 31) * 16;
+      if (col >= L.len) return;
+      fft_cols<NT, NTS, DIAG>(L, seg, col);
+    }
+  }
+}
+
+
 bool launch_fft_rs3232(const Layout& L, const uint32_t* seg_list, uint32_t nseg, int nt,
                        hipStream_t st) {
   const uintptr_t bits = (uintptr_t)L.data | (uintptr_t)L.parity | L.shard_stride |
@@ -269,6 +286,7 @@ bool launch_fft_rs3232(const Layout& L, const uint32_t* seg_list, uint32_t nseg,
   if ((bits & 15) || (L.len & 1023) || L.len == 0 || L.k != 32) return false;
   const uint64_t lanes = L.len / 32 * 2;
   const uint64_t gx = (lanes + 255) / 256;
+  const int cpw = (nt >> 5) & 15;  // tuning build: column blocks per workgroup (0: 1)
   for (uint32_t s0 = 0; s0 < nseg; s0 += 65535) {
     const uint32_t ny = nseg - s0 < 65535 ? nseg - s0 : 65535;
     // nt: bit 0 = nontemporal loads, bit 1 = nontemporal stores; tuning build only: bits 2-3 =
@@ -276,6 +294,19 @@ bool launch_fft_rs3232(const Layout& L, const uint32_t* seg_list, uint32_t nseg,
     switch (nt & 3) {
       case 3:
 #ifdef CEC_TUNING
+        if (cpw > 1) {
+          const unsigned g = (unsigned)((gx + cpw - 1) / cpw);
+          if (cpw == 2)
+            hipLaunchKernelGGL((k_fft3232<true, true, 0, 2>), dim3(g, ny), dim3(256), 0, st, L,
+                               seg_list, s0);
+          else if (cpw == 4)
+            hipLaunchKernelGGL((k_fft3232<true, true, 0, 4>), dim3(g, ny), dim3(256), 0, st, L,
+                               seg_list, s0);
+          else
+            hipLaunchKernelGGL((k_fft3232<true, true, 0, 8>), dim3(g, ny), dim3(256), 0, st, L,
+                               seg_list, s0);
+          break;
+        }
         if (nt & 12) {
           const unsigned lds = (nt & 16) ? 48 * 1024 : 0;
           if ((nt & 12) == 4)

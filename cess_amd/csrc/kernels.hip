@@ -1260,6 +1260,11 @@ void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_
                             st))
         return;
       break;
+    case 31: case 32: case 33:  // FFT with 2 / 4 / 8 column blocks of 4 KiB per workgroup
+      if (P::NI == 32 && P::NO == 32 &&
+          launch_fft_rs3232(L, seg_list, nseg, 3 | ((1 << (o.ct_variant - 30)) << 5), st))
+        return;
+      break;
     default: break;
   }
 #else
@@ -1274,7 +1279,7 @@ void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_
 }  // namespace
 
 #ifdef CEC_TUNING
-int max_ct_variant() { return 30; }
+int max_ct_variant() { return 33; }
 #else
 int max_ct_variant() { return 0; }
 #endif

@@ -273,3 +273,22 @@ def test_rust_crate_declares_every_header_symbol():
     with open(os.path.join(root, "utils", "ec-hip", "src", "lib.rs")) as f:
         rs = set(re.findall(r"pub fn (cec_[a-z0-9_]+)\s*\(", f.read()))
     assert rs == set(header_symbols())
+
+
+def test_product_kernel_occupancy():
+    """Register budgets the measured rates depend on: the RS(32,32) FFT encode at
+    3 waves per SIMD (<= 168 VGPRs), the one-wave hash tick at 4 (<= 128), none with scratch."""
+    import os
+    import sys
+    from cess_amd import _lib
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "tools"))
+    import sha_slots
+    res = sha_slots.kernel_resources(_lib.LIB_PATH)
+    budget = {"k_fft3232": 168, "k_sha256_tick1": 128, "k_ct_dec1_mixed21": 64}
+    for pat, cap in budget.items():
+        ks = {n: r for n, r in res.items() if pat in n}
+        assert ks, pat
+        for n, r in ks.items():
+            assert int(r["vgpr_count"]) <= cap, (n, r["vgpr_count"])
+            assert int(r["private_segment_fixed_size"]) == 0, n

@@ -42,6 +42,33 @@ def disassemble(obj: str) -> str:
     return "\n".join(out)
 
 
+def kernel_resources(obj: str) -> dict:
+    """{kernel symbol: {vgpr_count, sgpr_count, private_segment_fixed_size, ...}} from the code
+    object notes of every offload bundle in `obj`."""
+    rows = {}
+    with tempfile.TemporaryDirectory() as t:
+        subprocess.run([f"{B}/llvm-objcopy", f"--dump-section=.hip_fatbin={t}/fb.bin", obj,
+                        f"{t}/copy"], check=True)
+        fb = open(f"{t}/fb.bin", "rb").read()
+        starts = [m.start() for m in re.finditer(b"__CLANG_OFFLOAD_BUNDLE__", fb)] + [len(fb)]
+        for n, (a, b) in enumerate(zip(starts, starts[1:])):
+            with open(f"{t}/b{n}.bin", "wb") as f:
+                f.write(fb[a:b])
+            subprocess.run([f"{B}/clang-offload-bundler", "--unbundle", "--type=o",
+                            f"--input={t}/b{n}.bin", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                            f"--output={t}/k{n}.co"], check=True)
+            notes = subprocess.run([f"{B}/llvm-readelf", "--notes", f"{t}/k{n}.co"], check=True,
+                                   capture_output=True, text=True).stdout
+            cur = {}
+            for line in notes.splitlines():
+                m = re.match(r"\s+\.([a-z_]+):\s+(\S+)", line)
+                if m:
+                    cur[m.group(1)] = m.group(2)
+                    if m.group(1) == "vgpr_spill_count":
+                        rows[cur.get("name", "?")] = dict(cur)
+    return rows
+
+
 def loop_counts(dis: str, kernel: str = KERNEL):
     """(symbol, Counter of VALU opcodes) of the kernel's block loop."""
     lines, sym = [], None
