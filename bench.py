@@ -312,6 +312,9 @@ def main() -> None:
     ap.add_argument("--rt-mode", type=int, default=0,
                     help="run-time kernel: 0 Horner over input groups, index-mode XORs (k <= 32), "
                          "1 per-bit masks, 2 Horner with v_mov table reads")
+    ap.add_argument("--erase", type=int, default=-1,
+                    help="config 3: erased fragment index of every segment (-1: seg mod (k+m), "
+                         "the BASELINE pattern)")
     ap.add_argument("--events", choices=["step", "region"], default="region",
                     help="HIP events around the timed region (default: the mean time per launch "
                          "over the region, rocprof's average within 0.2%%) or around every step "
@@ -374,7 +377,9 @@ def main() -> None:
     present = None
     if args.config == 3:
         present = np.ones((nseg, k + m), np.uint8)
-        present[np.arange(nseg), (seg0 + np.arange(nseg)) % (k + m)] = 0
+        lost = ((seg0 + np.arange(nseg)) % (k + m) if args.erase < 0
+                else np.full(nseg, args.erase))
+        present[np.arange(nseg), lost] = 0
     elif args.config in (6, 7):
         rng = np.random.default_rng(seg0 + args.config)
         present = np.ones((nseg, k + m), np.uint8)
