@@ -487,8 +487,8 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
     }
     if (c->k == 2 && c->m == 1 && plan->ct.size() > 1 && nseg < (1u << 30)) {
       // grouped by erasure pattern, not in segment order: the workgroups resident at once then
-      // share one pattern, and a batch with interleaved patterns runs as fast as a uniform one
-      // (config 3, erased = seg mod 3: 0.253 -> ~0.245 ms per GiB batch, bench.py --erase)
+      // mostly share one pattern (config 3, erased = seg mod 3: 0.253 -> 0.250 ms per GiB batch;
+      // a uniform pattern takes 0.244-0.248, bench.py --erase)
       plan->mixed_off = hl.size();
       plan->mixed_count = tagged.size();
       hl.insert(hl.end(), tagged.begin(), tagged.end());
