@@ -689,6 +689,33 @@ __global__ __launch_bounds__(BS) void k_ct_persist(Layout L, const uint32_t* __r
   }
 }
 
+// XCD-contiguous variant (tuning build): a 1-D grid over the flattened (segment, tile) space,
+// remapped so that XCD x (which receives workgroups x, x + 8, ... from the round-robin dispatch)
+// walks the contiguous 1/8 of the batch starting at x * ceil(total / 8).
+template <class P, bool NT, int BS>
+__global__ __launch_bounds__(BS) void k_ct_xcd(Layout L, const uint32_t* __restrict__ seg_list,
+                                               uint32_t nseg, uint64_t tiles_per_seg) {
+  const uint64_t total = (uint64_t)nseg * tiles_per_seg;
+  const uint64_t per = (total + 7) / 8;
+  const uint64_t t = (uint64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (t >= total) return;
+  const uint32_t y = (uint32_t)(t / tiles_per_seg);
+  const uint64_t tile = t - (uint64_t)y * tiles_per_seg;
+  const uint32_t seg = seg_list ? seg_list[y] : y;
+  const uint64_t v = tile * BS + threadIdx.x;
+  if (v < L.len / 16) {
+    const uint64_t off = v * 16;
+    auto ld = [&](auto J) CEC_AI {
+      return ld16<NT, u32x4>(shard_ptr_ct<P::K, P::v.in[J]>(L, seg) + off);
+    };
+    auto st = [&](auto O, u32x4 yv) CEC_AI {
+      st16<NT, u32x4>(shard_ptr_ct<P::K, P::v.out[O]>(L, seg) + off, yv);
+    };
+    if constexpr (Rs21Closed<P>::missing >= 0) ct_column_rs21<Rs21Closed<P>::missing, u32x4>(ld, st);
+    else ct_column_horner<P, u32x4>(ld, st);
+  }
+}
+
 // Byte-granular variant for layouts whose shard starts are not 16-byte aligned.
 template <class P>
 __global__ __launch_bounds__(256) void k_ct_bytes(Layout L, const uint32_t* __restrict__ seg_list,
@@ -1185,6 +1212,15 @@ void run_ct_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_li
       const unsigned grid = o.ct_variant == 9 ? 2048 : o.ct_variant == 10 ? 4096 : 8192;
       hipLaunchKernelGGL((k_ct_persist<P, true, 256>), dim3(grid), dim3(256), 0, st, L, seg_list,
                          nseg, tiles);
+      return;
+    }
+    case 12: {  // XCD-contiguous tile order
+      if (!layout_vec16_ok(L) || (L.len & 15) || P::NI + P::NO > 3) break;
+      const uint64_t tiles = (L.len / 16 + 255) / 256;
+      const uint64_t total = tiles * nseg;
+      if (total >= (1ull << 31)) break;
+      hipLaunchKernelGGL((k_ct_xcd<P, true, 256>), dim3((unsigned)(((total + 7) / 8) * 8)),
+                         dim3(256), 0, st, L, seg_list, nseg, tiles);
       return;
     }
     default: break;
