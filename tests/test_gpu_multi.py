@@ -173,3 +173,18 @@ def test_c_dist_degraded_read_rccl(k, m, tmp_path):
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res), res
     assert sum(n for _, _, n in res) == sum(1 + s % m for s in range(nseg))
+
+
+def test_c_dist_from_c(tmp_path):
+    """The same world-1 degraded read driven from C (tests/native/dist_world1.c): the path a cgo /
+    FFI host takes, with HBM buffers from the HIP runtime and a locate callback."""
+    import subprocess
+    from tests.conftest import ROOT
+    exe = tmp_path / "dist_world1"
+    subprocess.run(["gcc", "-O2", "-D__HIP_PLATFORM_AMD__", f"{ROOT}/tests/native/dist_world1.c",
+                    f"-I{ROOT}/include", "-I/opt/rocm/include", f"-L{ROOT}/cess_amd", "-lcessec",
+                    "-L/opt/rocm/lib", "-lamdhip64",
+                    f"-Wl,-rpath,{ROOT}/cess_amd:/opt/rocm/lib", "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "dist world1 ok" in r.stdout
