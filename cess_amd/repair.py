@@ -20,7 +20,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from . import geometry
-from .reedsolomon import CecError, Encoder, ErrTooFewShards
+from .reedsolomon import CecError, Encoder, ErrTooFewShards, sha256_hex_device
 
 
 class ErrFragmentHashMismatch(CecError, ValueError):
@@ -58,8 +58,8 @@ def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, pres
                  expected: Optional[Sequence[Dict[int, bytes]]] = None, stream=None):
     """Rebuild every missing fragment of an HBM-resident batch in place (one launch for all
     erasure patterns) and, with `expected` ([{fragment index: recorded hash}] per segment),
-    return per-segment booleans: rebuilt fragments hash to the recorded values (hashed on the
-    host from one D2H copy per fragment, SHA-NI)."""
+    return per-segment booleans: rebuilt fragments hash to the recorded values (all of them
+    hashed in one GPU launch, one chain per fragment, where they were rebuilt)."""
     import torch
     enc.ReconstructBatch(d_data, d_parity, nseg, shard_len, present, stream=stream)
     if expected is None:
@@ -69,13 +69,12 @@ def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, pres
     else:
         stream.synchronize()
     k = enc.DataShards
-    ok = []
-    for s in range(nseg):
-        good = True
-        for i, h in expected[s].items():
-            t = d_data[s, i] if i < k else d_parity[s, i - k]
-            good &= hashlib.sha256(t.cpu().numpy()).hexdigest().encode() == bytes(h)
-        ok.append(good)
+    which = [(s, i, bytes(h)) for s in range(nseg) for i, h in expected[s].items()]
+    ptrs = [(d_data[s, i] if i < k else d_parity[s, i - k]).data_ptr() for s, i, _ in which]
+    got = sha256_hex_device(ptrs, shard_len) if ptrs else []
+    ok = [True] * nseg
+    for (s, _, h), g in zip(which, got):
+        ok[s] &= g == h
     return ok
 
 
@@ -83,11 +82,12 @@ def generate_fillers(n: int, seed: int = 0xF111E5, filler_size: int = geometry.F
                      first: int = 0, device: int = 0):
     """n idle fillers of `filler_size` bytes generated in HBM (splitmix64 counter stream,
     filler i = segment first+i of the generator) with their SHA-256 hex hashes (as
-    `upload_filler` records them). Returns (device tensor [n][filler_size], [hash])."""
+    `upload_filler` records them), hashed on the GPU. Returns (device tensor [n][filler_size],
+    [hash])."""
     import torch
     from .reedsolomon import fill_synthetic
     d = torch.empty((n, filler_size), dtype=torch.uint8, device=torch.device("cuda", device))
     fill_synthetic(d, filler_size, n, first, seed)
     torch.cuda.synchronize(device)
-    hashes = [hashlib.sha256(d[i].cpu().numpy()).hexdigest().encode() for i in range(n)]
+    hashes = sha256_hex_device([d[i].data_ptr() for i in range(n)], filler_size) if n else []
     return d, hashes

@@ -487,8 +487,14 @@ def test_repair_batch_wide(torch, cess, corc, orc):
                          for i in lost})
     dd = to_dev(torch, data * present[:, :k, None])
     dp = to_dev(torch, par * present[:, k:, None])
-    ok = repair_batch(cess.New(k, m), dd, dp, nseg, F, present, expected)
+    enc = cess.New(k, m)
+    ok = repair_batch(enc, dd, dp, nseg, F, present, expected)
     assert ok == [True] * nseg
+    # a recorded hash that the rebuilt fragment does not match flags that segment only
+    wrong = [dict(e) for e in expected]
+    i0 = next(iter(wrong[2]))
+    wrong[2][i0] = b"0" * 64
+    assert repair_batch(enc, dd, dp, nseg, F, present, wrong) == [True, True, False, True, True]
 
 
 def test_generate_fillers(torch, orc):

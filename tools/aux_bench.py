@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Measurements of the §8f rows beside the codec (one MI355X), one JSON line each:
+  repair   (f2) 64 RS(2,1) segments of 8 MiB fragments, each losing fragment s mod 3: the batched
+           rebuild (HBM roofline, (k+1)*F bytes per segment) and the recorded-hash check of the
+           64 rebuilt fragments on the GPU (one SHA-256 chain per fragment: latency bound);
+  audit    (f3) the 47 challenged 8 KiB chunks of all 192 fragments of a 1 GiB batch: the gather
+           (2 x chunk bytes moved) and gather + SHA-256 of every chunk;
+  fillers  (f4) 64 idle fillers of 8 MiB: generation in HBM and their SHA-256 hashes.
+usage: python tools/aux_bench.py [--reps 5]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+GB = 1e9
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import cess_amd
+    from cess_amd import audit, repair
+    k, m, F, nseg = 2, 1, 8 << 20, 64
+    n = k + m
+    dev = torch.device("cuda", 0)
+    enc = cess_amd.New(k, m)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    d = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
+    p = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
+    cess_amd.fill_synthetic(d, k * F, nseg, 0, 0xCE550002)
+    enc.EncodeBatch(d, p, nseg, F)
+    torch.cuda.synchronize()
+    present = np.ones((nseg, n), np.uint8)
+    present[np.arange(nseg), np.arange(nseg) % n] = 0
+    frag = lambda s, i: d[s, i] if i < k else p[s, i - k]  # noqa: E731
+    recorded = cess_amd.sha256_hex_device([frag(s, s % n).data_ptr() for s in range(nseg)], F)
+    expected = [{s % n: recorded[s]} for s in range(nseg)]
+    t_rebuild = timed(lambda: enc.ReconstructBatch(d, p, nseg, F, present))
+    ok = []
+    t_all = timed(lambda: ok.append(repair.repair_batch(enc, d, p, nseg, F, present, expected)))
+    assert all(all(x) for x in ok)
+    print(json.dumps({"row": "f2 repair", "segments": nseg, "fragment_bytes": F,
+                      "rebuild_s": round(t_rebuild, 6),
+                      "rebuild_GBps": round(nseg * (k + 1) * F / t_rebuild / GB, 1),
+                      "rebuild_roofline_frac": round(nseg * (k + 1) * F / t_rebuild / GB / 8000, 3),
+                      "rebuild_and_hash_check_s": round(t_all, 4),
+                      "hash_check_note": "SHA-256 of each 8 MiB rebuilt fragment is one serial "
+                                         "131,073-block chain: latency bound"}), flush=True)
+
+    idx, _ = audit.challenge_indices(list(range(1, 4096)))
+    nfrag, chunk = nseg * n, F // audit.CHUNK_COUNT
+    d_chunks = torch.empty((nfrag, len(idx), chunk), dtype=torch.uint8, device=dev)
+    d_hex = torch.empty((nfrag, len(idx), 64), dtype=torch.uint8, device=dev)
+    t_g = timed(lambda: audit.audit_chunks(enc, d, p, nseg, F, idx, d_chunks=d_chunks))
+    t_h = timed(lambda: audit.audit_chunks(enc, d, p, nseg, F, idx, d_chunks=d_chunks,
+                                           d_hex=d_hex))
+    cb = nfrag * len(idx) * chunk
+    print(json.dumps({"row": "f3 audit", "fragments": nfrag, "chunks_per_fragment": len(idx),
+                      "chunk_bytes": chunk, "gather_s": round(t_g, 6),
+                      "gather_GBps_moved": round(2 * cb / t_g / GB, 1),
+                      "gather_and_sha256_s": round(t_h, 5),
+                      "chunks_per_s": round(nfrag * len(idx) / t_h, 1)}), flush=True)
+
+    out = {}
+    t_f = timed(lambda: out.update(r=repair.generate_fillers(nseg)))
+    print(json.dumps({"row": "f4 fillers", "fillers": nseg, "filler_bytes": F,
+                      "generate_and_hash_s": round(t_f, 4),
+                      "GBps": round(nseg * F / t_f / GB, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
