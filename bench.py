@@ -223,12 +223,14 @@ def config1_cpu(args) -> dict:
     return res
 
 
-def degraded_gather(enc, k: int, m: int, F: int, world: int, rank: int, dev, nseg: int):
+def degraded_gather(enc, k: int, m: int, F: int, world: int, rank: int, dev, nseg: int,
+                    exchange: str = "survivors"):
     """BASELINE config 4's exchange step, set up once: segments 0..nseg*world-1 stored under the
     miner-spread placement (fragment f of segment s on GPU (s + f) mod world,
     c-pallets/file-bank/src/functions.rs:187-283), every segment losing fragment s mod (k+m).
-    Returns (run, plan): run() gathers the survivors over the process group (RCCL point to
-    point; RCCL has no XOR reduction) and rebuilds the lost fragments with libcessec."""
+    Returns (run, verify, plan): run() moves survivors (or, exchange "partials"/"auto", partial
+    rebuilds: SURVEY.md §8e) over the process group (RCCL point to point; RCCL has no XOR
+    reduction) and rebuilds the lost fragments with libcessec."""
     import torch
     import cess_amd
     from cess_amd import distributed as D
@@ -248,7 +250,7 @@ def degraded_gather(enc, k: int, m: int, F: int, world: int, rank: int, dev, nse
             if (s, f) in store.slots:
                 store.data[store.slots[(s, f)]].copy_(seg_d[0, f] if f < k else seg_p[0, f - k])
     torch.cuda.synchronize(dev)
-    plan = D.plan_gather({s: [s % n] for s in range(total)}, k, m, world, F)
+    plan = D.plan_gather({s: [s % n] for s in range(total)}, k, m, world, F, exchange=exchange)
 
     def run():
         return D.degraded_read(plan, store, enc, rank)
@@ -319,6 +321,9 @@ def main() -> None:
                     help="HIP events around the timed region (default: the mean time per launch "
                          "over the region, rocprof's average within 0.2%%) or around every step "
                          "(each event pair costs ~7 us of GPU time per step)")
+    ap.add_argument("--exchange", choices=["survivors", "partials", "auto"], default="survivors",
+                    help="config 4: degraded-read exchange (survivors to the decoder, or partial "
+                         "rebuilds from every GPU holding survivors, SURVEY.md §8e)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
@@ -390,7 +395,7 @@ def main() -> None:
     gather = None
     if args.config == 4:
         # the degraded-read gather of 64 segments per rank runs inside every step
-        gather = degraded_gather(enc, k, m, F, world, rank, dev, 64)
+        gather = degraded_gather(enc, k, m, F, world, rank, dev, 64, args.exchange)
     if args.config == 5:
         # Windowed pipeline over steps: step i encodes into parity buffer i % W on the launch
         # stream, then (on the hash stream, after the encode) adds the batch's 64 * nseg
@@ -619,10 +624,11 @@ def main() -> None:
     if sha_note:
         out["sha256"] = sha_note
 
-    def gather_leg(run_verify_plan, reps=5) -> dict:
-        """Time the degraded read (survivor gather over the process group + rebuild) alone,
+    def gather_leg(run_verify_plan, reps=5, code=(k, F)) -> dict:
+        """Time the degraded read (exchange over the process group + rebuild) alone,
         synchronised per rep, max over ranks; verify the rebuilt fragments."""
         run, verify, plan = run_verify_plan
+        fb = code[1]
         times = []
         res = None
         for _ in range(reps + 1):
@@ -643,12 +649,15 @@ def main() -> None:
             dist.all_reduce(v, op=dist.ReduceOp.MAX)
         t, bad = float(v[0]), bool(v[1])
         nrebuilt = len(plan.lost)
+        kk = code[0]
         return {"segments": nrebuilt, "lost_per_segment": 1,
+                "exchange": ("partials" if plan.partial and not plan.moves else
+                             "mixed" if plan.partial else "survivors"),
                 "placement": "fragment f of segment s on GPU (s + f) mod N "
                              "(c-pallets/file-bank/src/functions.rs:187-283)",
                 "gather_bytes": plan.bytes_moved, "seconds": round(t, 5),
                 "gather_GBps": round(plan.bytes_moved / t / GB, 2) if plan.bytes_moved else None,
-                "rebuilt_GBps": round(nrebuilt * (k + 1) * F / t / GB, 2),
+                "rebuilt_GBps": round(nrebuilt * (kk + 1) * fb / t / GB, 2),
                 "xgmi_GBps_per_link": 153,
                 "backend": (backend if world > 1 else "local (one GPU: no bytes move)"),
                 "bit_exact": not bad}
@@ -659,6 +668,15 @@ def main() -> None:
         # config 4's exchange step measured in the default (scaling) run as well
         out.setdefault("extra", {})["degraded_gather"] = gather_leg(
             degraded_gather(enc, k, m, F, world, rank, dev, 64))
+        # the wide code's single-fragment degraded read, both exchanges: RS(32,32)
+        # with 16 MiB segments (F = 512 KiB), 8 fragments per GPU at world 8
+        wk, wm, wF = CONFIGS[5][:3]
+        wenc = cess_amd.New(wk, wm, device=local)
+        out["extra"]["wide_degraded_gather"] = {
+            ex: gather_leg(degraded_gather(wenc, wk, wm, wF, world, rank, dev, 64, ex),
+                           code=(wk, wF))
+            for ex in ("survivors", "partials")}
+        wenc.close()
 
     if not args.no_extra and args.config == 2:
         # decode rate in the same process (BASELINE config 3 workload, same bytes)
@@ -676,6 +694,23 @@ def main() -> None:
         out.setdefault("extra", {}).update(
             {"reconstruct_GBps_per_gpu": round(bytes_step_gpu / (dms * 1e-3) / GB, 2),
              "reconstruct_ms": round(dms, 4)})
+        # the measured-copy ceiling beside the spec peak: a device-to-device copy
+        # of the same 1 GiB data batch (HIP's blit kernel), read + write bytes per copy
+        src = d_data.view(-1)
+        dst = torch.empty_like(src)
+        for _ in range(3):
+            dst.copy_(src)
+        a.record(stream)
+        for _ in range(20):
+            dst.copy_(src)
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        cms = a.elapsed_time(b) / 20
+        out["roofline"]["copy_ceiling"] = {
+            "GBps": round(2 * src.numel() / (cms * 1e-3) / GB, 1),
+            "what": "D2D copy of the 1 GiB data batch (torch copy_ = hipMemcpyAsync), "
+                    "read + write bytes / time"}
+        del dst
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(k, m, F, args.cpu_seconds)

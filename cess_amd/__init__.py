@@ -21,11 +21,12 @@ from .reedsolomon import (
     New,
     fill_synthetic,
     sha256_hex_device,
+    xor_batch,
 )
 
 __all__ = [
     "geometry", "CecError", "Encoder", "New", "ErrInvShardNum", "ErrMaxShardNum",
     "ErrReconstructRequired", "ErrShardNoData", "ErrShardSize", "ErrShortData",
     "ErrTooFewShards", "HipError", "fill_synthetic", "sha256_hex_device", "HashQueue",
-    "sha256_blocks", "records", "ErrTooManySegments", "audit",
+    "sha256_blocks", "records", "ErrTooManySegments", "audit", "xor_batch",
 ]

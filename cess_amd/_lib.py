@@ -27,7 +27,8 @@ class PipelineOpts(Structure):
 
 
 class DistMove(Structure):
-    _fields_ = [("seg", c_uint64), ("frag", c_int32), ("src", c_int32), ("dst", c_int32)]
+    _fields_ = [("seg", c_uint64), ("frag", c_int32), ("src", c_int32), ("dst", c_int32),
+                ("kind", c_int32)]
 
 
 class PipelineStats(Structure):
@@ -51,6 +52,10 @@ SIGNATURES = {
     "cec_encode_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]),
     "cec_reconstruct_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t,
                                       POINTER(c_uint8), c_int, c_int, c_void_p]),
+    "cec_reconstruct_partial_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t,
+                                              POINTER(c_uint8), POINTER(c_uint8), c_int,
+                                              c_void_p]),
+    "cec_xor_batch": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_void_p]),
     "cec_sha256_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p,
                                  c_void_p]),
     "cec_sha256_hex": (c_int, [POINTER(c_void_p), c_size_t, c_size_t, POINTER(c_uint8),
@@ -91,6 +96,10 @@ SIGNATURES = {
     "cec_dist_destroy": (None, [c_void_p]),
     "cec_dist_plan": (c_int, [c_int, c_int, c_int, POINTER(c_uint64), POINTER(c_uint8), c_size_t,
                               POINTER(DistMove), c_size_t, POINTER(c_size_t), POINTER(c_int32)]),
+    "cec_dist_plan_ex": (c_int, [c_int, c_int, c_int, c_int, POINTER(c_uint64), POINTER(c_uint8),
+                                 c_size_t, POINTER(DistMove), c_size_t, POINTER(c_size_t),
+                                 POINTER(c_int32)]),
+    "cec_dist_set_option": (c_int, [c_void_p, c_int, c_int]),
     "cec_dist_degraded_read": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint8), c_size_t,
                                        c_size_t, LOCATE_FN, c_void_p, POINTER(c_void_p), c_void_p,
                                        POINTER(c_size_t)]),
@@ -121,6 +130,9 @@ CEC_STAT_DECODE_CACHED = 1
 CEC_STAT_RETIRED_PENDING = 2
 CEC_HQOPT_TICK = 1
 CEC_DIST_ID_BYTES = 128
+CEC_DIST_SURVIVOR = 0
+CEC_DIST_PARTIAL = 1
+CEC_DIST_OPT_EXCHANGE = 1
 
 _libs = {}
 

@@ -171,15 +171,18 @@ using ProgPtr = std::shared_ptr<const Program>;
 // Upload coefficient rows for outputs out_idx[o] (coef[o][j]) as run-time chunks. The chunk
 // blocks come from `pool` and go back to it (retired) when the last ProgPtr is dropped. Uploads
 // run on `upload` and are complete when this returns.
+// `partial`: the rows do not rebuild a shard by themselves (cec_reconstruct_partial_batch), so
+// the compile-time single-erasure kernels never stand in for the program.
 int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int nin,
-                  const uint8_t* out_idx, int nout, const BigMat& coef, ProgPtr* out) {
+                  const uint8_t* out_idx, int nout, const BigMat& coef, ProgPtr* out,
+                  bool partial = false) {
   DevPool* pp = &pool;
   std::shared_ptr<Program> prog(new Program, [pp](Program* p) {
     for (auto& c : p->chunks) pp->retire(c.dev, c.bytes);
     delete p;
   });
   prog->nout = nout;
-  prog->single = nout == 1 ? out_idx[0] : -1;
+  prog->single = nout == 1 && !partial ? out_idx[0] : -1;
   std::memcpy(prog->in_idx, in_idx, nin);
   std::memcpy(prog->out_idx, out_idx, nout);
   std::vector<std::vector<uint32_t>> hosts;
@@ -366,6 +369,13 @@ std::string pattern_key(const uint8_t* present, int n, bool data_only) {
   return key;
 }
 
+std::string partial_key(const uint8_t* present, const uint8_t* held, int n, bool data_only) {
+  std::string key = pattern_key(present, n, data_only);
+  key.push_back(2);  // partial marker: never equal to a full pattern's key
+  for (int i = 0; i < n; ++i) key.push_back(held[i] ? 1 : 0);
+  return key;
+}
+
 // Decode program for one erasure pattern (LRU-cached). Nothing is evicted here: the caller
 // evicts after its launches are enqueued and marked (evict_decode), so a program resolved
 // earlier in the same call is never dropped under it.
@@ -390,6 +400,56 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* ou
   if (plan->nout > 0) {
     int rc = build_program(c->pool, c->stream, plan->in_idx, c->k, plan->out_idx, plan->nout,
                            plan->coef, &prog);
+    if (rc) return rc;
+  } else {
+    prog = std::make_shared<const Program>();
+  }
+  c->lru.push_front(key);
+  c->decode_cache.emplace(std::move(key), cec_codec::Entry{prog, c->lru.begin()});
+  *out = std::move(prog);
+  return CEC_OK;
+}
+
+// Partial decode program (the partial-product exchange of SURVEY.md §8e): the decode rows of
+// pattern `present` (survivors = its first k present shards) restricted to the survivors flagged
+// in `held`. The rebuild is linear in the survivors, so the XOR of the partials over any
+// partition of the survivors is the full rebuild. No held survivor: a zero program (one input
+// column with zero coefficients), so the outputs are still written (as zeros). Cached in the
+// decode LRU under its own key.
+int get_partial(cec_codec* c, const uint8_t* present, const uint8_t* held, bool data_only,
+                ProgPtr* out) {
+  const int n = c->k + c->m;
+  std::string key = partial_key(present, held, n, data_only);
+  auto it = c->decode_cache.find(key);
+  if (it != c->decode_cache.end()) {
+    c->lru.splice(c->lru.begin(), c->lru, it->second.lru);
+    *out = it->second.prog;
+    return CEC_OK;
+  }
+  auto plan = std::make_unique<BigPlan>();
+  auto sub = std::make_unique<BigMat>();
+  auto inv = std::make_unique<BigMat>();
+  auto work = std::make_unique<WorkMat>();
+  uint8_t flags[cec::kMaxShards];
+  for (int i = 0; i < n; ++i) flags[i] = present[i] ? 1 : 0;
+  if (cec::gf_decode_plan(c->k, c->m, flags, data_only, *c->E, *plan, *sub, *inv, *work) != 0)
+    return set_err(CEC_ETOOFEW, "fewer than k shards present");
+  ProgPtr prog;
+  if (plan->nout > 0) {
+    uint8_t in_sub[cec::kMaxShards];
+    int nsub = 0;
+    auto coef = std::make_unique<BigMat>();
+    for (int j = 0; j < c->k; ++j)
+      if (held[plan->in_idx[j]]) {
+        for (int o = 0; o < plan->nout; ++o) coef->v[o][nsub] = plan->coef.v[o][j];
+        in_sub[nsub++] = plan->in_idx[j];
+      }
+    if (nsub == 0) {  // zero program: one column, zero coefficients (BigMat starts zeroed)
+      in_sub[0] = plan->in_idx[0];
+      nsub = 1;
+    }
+    int rc = build_program(c->pool, c->stream, in_sub, nsub, plan->out_idx, plan->nout, *coef,
+                           &prog, true);
     if (rc) return rc;
   } else {
     prog = std::make_shared<const Program>();
@@ -446,16 +506,19 @@ Layout stage_layout(cec_codec* c, size_t len) {
 
 // Build the plan of a per-segment reconstruct for the pattern array `pkey` (nseg * n flags +
 // data_only + force_generic) into *out; device arrays are uploaded and complete on return.
+// partial: pkey holds 2n flags per segment (present, then held) and the programs are partial
+// (cec_reconstruct_partial_batch).
 int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_only,
-                  std::unique_ptr<PsPlan>* out) {
+                  std::unique_ptr<PsPlan>* out, bool partial = false) {
   const int n = c->k + c->m;
+  const int per = partial ? 2 * n : n;
   auto plan = std::make_unique<PsPlan>();
   plan->key = pkey;
   // group segments by pattern, in first-appearance order (deterministic launch order)
   std::unordered_map<std::string, size_t> gidx;
   std::vector<std::pair<std::string, std::vector<uint32_t>>> groups;
   for (size_t s = 0; s < nseg; ++s) {
-    std::string k = pkey.substr(s * n, n);
+    std::string k = pkey.substr(s * per, per);
     auto it = gidx.find(k);
     if (it == gidx.end()) {
       it = gidx.emplace(k, groups.size()).first;
@@ -467,10 +530,12 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
   std::vector<std::pair<ProgPtr, const std::vector<uint32_t>*>> progs;
   for (auto& g : groups) {
     ProgPtr p;
-    int rc = get_decode(c, reinterpret_cast<const uint8_t*>(g.first.data()), data_only, &p);
+    const uint8_t* flags = reinterpret_cast<const uint8_t*>(g.first.data());
+    int rc = partial ? get_partial(c, flags, flags + n, data_only, &p)
+                     : get_decode(c, flags, data_only, &p);
     if (rc) return rc;
-    plan->keys.push_back(pattern_key(reinterpret_cast<const uint8_t*>(g.first.data()), n,
-                                     data_only));
+    plan->keys.push_back(partial ? partial_key(flags, flags + n, n, data_only)
+                                 : pattern_key(flags, n, data_only));
     if (!p->nout) continue;
     progs.push_back({p, &g.second});
     plan->progs.push_back(p);
@@ -763,6 +828,61 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
   int mrc = c->pool.mark(st);
   evict_decode(c);
   return rc ? rc : mrc;
+}
+
+int cec_reconstruct_partial_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size_t nseg,
+                                  size_t shard_len, const uint8_t* present, const uint8_t* held,
+                                  int data_only, void* hip_stream) {
+  if (!c || !present || !held || (nseg && (!d_data || !d_parity)))
+    return set_err(CEC_EINVAL, "null");
+  if (shard_len == 0) return set_err(CEC_ESHARDLEN, "zero shard length");
+  if (nseg > 0xffffffffull) return set_err(CEC_EINVAL, "too many segments");
+  if (nseg == 0) return CEC_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = pick_stream(c, hip_stream);
+  const int n = c->k + c->m;
+  Layout L = batch_layout(c, d_data, d_parity, shard_len);
+  // per segment: n presence flags then n held flags; the same plan cache as the full rebuild
+  // (the trailing marker keeps the keys apart)
+  std::string pkey;
+  pkey.reserve(nseg * 2 * n + 3);
+  for (size_t s = 0; s < nseg; ++s) {
+    for (int i = 0; i < n; ++i) pkey.push_back(present[s * n + i] ? 1 : 0);
+    for (int i = 0; i < n; ++i) pkey.push_back(held[s * n + i] ? 1 : 0);
+  }
+  pkey.push_back(data_only ? 1 : 0);
+  pkey.push_back(c->force_generic ? 1 : 0);
+  pkey.push_back(2);
+  int rc = CEC_OK;
+  if (!c->ps || c->ps->key != pkey) {
+    std::unique_ptr<PsPlan> plan;
+    rc = build_ps_plan(c, pkey, nseg, data_only != 0, &plan, true);
+    if (rc) return rc;
+    c->drop_plan();
+    c->ps = std::move(plan);
+  } else {
+    for (const auto& key : c->ps->keys) {
+      auto it = c->decode_cache.find(key);
+      if (it != c->decode_cache.end()) c->lru.splice(c->lru.begin(), c->lru, it->second.lru);
+    }
+  }
+  rc = launch_ps_plan(c, *c->ps, L, st);
+  int mrc = c->pool.mark(st);
+  evict_decode(c);
+  return rc ? rc : mrc;
+}
+
+int cec_xor_batch(uint8_t* d_dst, const uint8_t* d_src, size_t nsrc, size_t src_stride,
+                  size_t len, void* hip_stream) {
+  if ((len && nsrc && (!d_dst || !d_src)) || nsrc > 0xffffffffull)
+    return set_err(CEC_EINVAL, "null buffer or too many sources");
+  if (nsrc > 1 && src_stride < len)
+    return set_err(CEC_EINVAL, "src_stride < len: sources overlap");
+  if ((len + 255) / 256 > 0x7fffffffull) return set_err(CEC_EINVAL, "len too large (> 512 GiB)");
+  if (len == 0 || nsrc == 0) return CEC_OK;
+  cec::launch_xor_reduce(d_dst, d_src, (uint32_t)nsrc, src_stride, len,
+                         reinterpret_cast<hipStream_t>(hip_stream));
+  return check_launch();
 }
 
 int cec_sha256_batch(cec_codec* c, const uint8_t* d_data, const uint8_t* d_parity, size_t nseg,

@@ -96,19 +96,25 @@ int nccl_err(ncclResult_t res, const char* what) {
     if (_r != ncclSuccess) return nccl_err(_r, #expr); \
   } while (0)
 
+int owner(uint64_t s, int f, int world) { return (int)((s + (uint64_t)f) % (uint64_t)world); }
+
 struct Seg {
   uint64_t seg;
   std::vector<int> lost;  // sorted, distinct
   int decoder;
   std::vector<int> surv;  // first k present fragments
+  bool partial = false;   // partial-product exchange: `holders` send one partial per lost
+  std::vector<int> holders;  // ranks other than the decoder holding survivors, ascending
 };
 
-// Group the lost list by segment and apply the placement rule (shared by cec_dist_plan and the
-// degraded read, so the plan a caller inspects is the one that runs).
-int make_plan(int k, int m, int world, const uint64_t* lost_seg, const uint8_t* lost_frag,
-              size_t nlost, std::vector<Seg>* out) {
+// Group the lost list by segment and apply the placement rule (shared by cec_dist_plan_ex and
+// the degraded read, so the plan a caller inspects is the one that runs). exchange: 0 survivors,
+// 1 partials, 2 per segment whichever moves fewer fragments (survivors on a tie).
+int make_plan(int k, int m, int world, int exchange, const uint64_t* lost_seg,
+              const uint8_t* lost_frag, size_t nlost, std::vector<Seg>* out) {
   if (k < 1 || m < 1 || k + m > 256 || world < 1 || (nlost && (!lost_seg || !lost_frag)))
     return cec::set_error(CEC_EINVAL, "dist plan: bad k, m, world or null lost list");
+  if (exchange < 0 || exchange > 2) return cec::set_error(CEC_EINVAL, "dist plan: bad exchange");
   std::map<uint64_t, std::vector<int>> by;
   for (size_t i = 0; i < nlost; ++i) {
     if (lost_frag[i] >= k + m)
@@ -123,26 +129,54 @@ int make_plan(int k, int m, int world, const uint64_t* lost_seg, const uint8_t* 
     if ((int)v.size() > m)
       return cec::set_error(CEC_ETOOFEW, "dist plan: segment " + std::to_string(s) + " lost " +
                                              std::to_string(v.size()) + " > m fragments");
-    Seg g{s, v, (int)((s + (uint64_t)v[0]) % (uint64_t)world), {}};
+    Seg g{s, v, owner(s, v[0], world), {}};
     for (int f = 0; f < k + m && (int)g.surv.size() < k; ++f)
       if (!std::binary_search(v.begin(), v.end(), f)) g.surv.push_back(f);
+    size_t n_surv = 0;
+    for (int f : g.surv) {
+      const int o = owner(s, f, world);
+      if (o == g.decoder) continue;
+      ++n_surv;
+      if (!std::binary_search(g.holders.begin(), g.holders.end(), o))
+        g.holders.insert(std::upper_bound(g.holders.begin(), g.holders.end(), o), o);
+    }
+    const size_t n_part = g.lost.size() * g.holders.size();
+    g.partial = exchange == 1 || (exchange == 2 && n_part < n_surv);
+    if (!g.partial) g.holders.clear();
     out->push_back(std::move(g));
   }
   return CEC_OK;
 }
-
-int owner(uint64_t s, int f, int world) { return (int)((s + (uint64_t)f) % (uint64_t)world); }
 
 }  // namespace
 
 struct cec_dist {
   cec_codec* codec = nullptr;
   int k = 0, m = 0, device = 0, world = 0, rank = 0;
+  int exchange = 0;  // CEC_DIST_OPT_EXCHANGE
   ncclComm_t comm = nullptr;
   uint8_t* stage = nullptr;  // staging batch: data [nseg_d][k][F], then parity [nseg_d][m][F]
   size_t stage_bytes = 0;
+  // partial-product segments: their batch (same layout) and the decoder's partial rows
+  // [holders + 1][pairs][F]
+  uint8_t* pstage = nullptr;
+  size_t pstage_bytes = 0;
   int* d_flag = nullptr;
 };
+
+namespace {
+// Grow a device buffer (its old contents may still be read by work queued on `st`).
+int grow(uint8_t** buf, size_t* have, size_t need, hipStream_t st) {
+  if (need <= *have) return CEC_OK;
+  DI_TRY(hipStreamSynchronize(st));
+  DI_TRY(hipFree(*buf));
+  *buf = nullptr;
+  *have = 0;
+  DI_TRY(hipMalloc(buf, need));
+  *have = need;
+  return CEC_OK;
+}
+}  // namespace
 
 extern "C" {
 
@@ -195,24 +229,52 @@ void cec_dist_destroy(cec_dist* d) {
   (void)hipDeviceSynchronize();
   if (d->comm) rccl().comm_destroy(d->comm);
   (void)hipFree(d->stage);
+  (void)hipFree(d->pstage);
   (void)hipFree(d->d_flag);
   (void)hipSetDevice(prev);
   delete d;
 }
 
+int cec_dist_set_option(cec_dist* d, int option, int value) {
+  if (!d) return cec::set_error(CEC_EINVAL, "null dist");
+  if (option == CEC_DIST_OPT_EXCHANGE) {
+    if (value < 0 || value > 2) return cec::set_error(CEC_EINVAL, "exchange must be 0, 1 or 2");
+    d->exchange = value;
+    return CEC_OK;
+  }
+  return cec::set_error(CEC_EINVAL, "unknown dist option");
+}
+
 int cec_dist_plan(int k, int m, int world, const uint64_t* lost_seg, const uint8_t* lost_frag,
                   size_t nlost, cec_dist_move* moves, size_t moves_cap, size_t* nmoves,
                   int32_t* decoder) {
+  return cec_dist_plan_ex(k, m, world, 0, lost_seg, lost_frag, nlost, moves, moves_cap, nmoves,
+                          decoder);
+}
+
+int cec_dist_plan_ex(int k, int m, int world, int exchange, const uint64_t* lost_seg,
+                     const uint8_t* lost_frag, size_t nlost, cec_dist_move* moves,
+                     size_t moves_cap, size_t* nmoves, int32_t* decoder) {
   std::vector<Seg> plan;
-  int rc = make_plan(k, m, world, lost_seg, lost_frag, nlost, &plan);
+  int rc = make_plan(k, m, world, exchange, lost_seg, lost_frag, nlost, &plan);
   if (rc) return rc;
   size_t n = 0;
-  for (const Seg& g : plan)
+  for (const Seg& g : plan) {
+    if (g.partial) {
+      for (int h : g.holders)
+        for (int f : g.lost) {
+          if (moves && n < moves_cap)
+            moves[n] = cec_dist_move{g.seg, f, h, g.decoder, CEC_DIST_PARTIAL};
+          ++n;
+        }
+      continue;
+    }
     for (int f : g.surv) {
       if (moves && n < moves_cap)
-        moves[n] = cec_dist_move{g.seg, f, owner(g.seg, f, world), g.decoder};
+        moves[n] = cec_dist_move{g.seg, f, owner(g.seg, f, world), g.decoder, CEC_DIST_SURVIVOR};
       ++n;
     }
+  }
   if (nmoves) *nmoves = n;
   if (decoder)
     for (size_t i = 0; i < nlost; ++i)
@@ -232,7 +294,7 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
   const int k = d->k, m = d->m, n = k + m, world = d->world, rank = d->rank;
   const size_t F = shard_len;
   std::vector<Seg> plan;
-  int rc = make_plan(k, m, world, lost_seg, lost_frag, nlost, &plan);
+  int rc = make_plan(k, m, world, d->exchange, lost_seg, lost_frag, nlost, &plan);
   if (rc) return rc;  // every rank sees the same list, so every rank fails here alike
 
   // lost entries per segment, and this rank's checks: its survivors found, its outputs given
@@ -280,75 +342,151 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
     return cec::set_error(CEC_EINVAL, "dist degraded read: another rank failed its checks");
 
   // Rounds of at most kRound segments of the plan (the same split on every rank) bound the
-  // staging batch; rounds follow each other on the stream, so a round's receives land after the
+  // staging; rounds follow each other on the stream, so a round's receives land after the
   // previous round's rebuild has read the staging.
   constexpr size_t kRound = 256;
   size_t rebuilt = 0, si = 0;
   for (size_t r0 = 0; r0 < plan.size(); r0 += kRound) {
     const size_t r1 = std::min(plan.size(), r0 + kRound);
-    std::vector<const Seg*> mine;
-    std::map<uint64_t, size_t> row;
-    for (size_t i = r0; i < r1; ++i)
-      if (plan[i].decoder == rank) {
-        row[plan[i].seg] = mine.size();
-        mine.push_back(&plan[i]);
+    // survivor segments this rank rebuilds; partial segments it decodes or holds survivors of
+    std::vector<const Seg*> mine, pmine;
+    std::map<uint64_t, size_t> row, prow;
+    size_t npairs = 0, H = 0;
+    std::map<std::pair<uint64_t, int>, size_t> pair;  // (segment, lost fragment) -> acc row
+    for (size_t i = r0; i < r1; ++i) {
+      const Seg& g = plan[i];
+      if (!g.partial) {
+        if (g.decoder == rank) {
+          row[g.seg] = mine.size();
+          mine.push_back(&g);
+        }
+        continue;
       }
-    const size_t need = mine.size() * (size_t)n * F;
-    if (need > d->stage_bytes) {
-      DI_TRY(hipStreamSynchronize(st));  // the old staging may still be read by queued work
-      DI_TRY(hipFree(d->stage));
-      d->stage = nullptr;
-      d->stage_bytes = 0;
-      DI_TRY(hipMalloc(&d->stage, need));
-      d->stage_bytes = need;
+      const bool holder = std::binary_search(g.holders.begin(), g.holders.end(), rank);
+      if (g.decoder != rank && !holder) continue;
+      prow[g.seg] = pmine.size();
+      pmine.push_back(&g);
+      if (g.decoder == rank) {
+        H = std::max(H, g.holders.size());
+        for (int f : g.lost) pair[{g.seg, f}] = npairs++;
+      }
     }
+    rc = grow(&d->stage, &d->stage_bytes, mine.size() * (size_t)n * F, st);
+    if (rc) return rc;
+    const size_t pbatch = pmine.size() * (size_t)n * F, acc_row = npairs * F;
+    rc = grow(&d->pstage, &d->pstage_bytes, pbatch + (H + 1) * acc_row, st);
+    if (rc) return rc;
     uint8_t* const st_data = d->stage;
     uint8_t* const st_par = d->stage + mine.size() * (size_t)k * F;
+    uint8_t* const p_data = d->pstage;
+    uint8_t* const p_par = d->pstage + pmine.size() * (size_t)k * F;
+    uint8_t* const acc = d->pstage + pbatch;
     auto slot = [&](uint64_t s, int f) {
       return f < k ? st_data + (row.at(s) * (size_t)k + f) * F
                    : st_par + (row.at(s) * (size_t)m + (f - k)) * F;
     };
-    // local survivors, then the grouped exchange (sends and receives in plan order)
-    size_t sj = si;
-    for (size_t i = r0; i < r1; ++i)
-      for (int f : plan[i].surv)
-        if (owner(plan[i].seg, f, world) == rank) {
-          const uint8_t* p = src_ptr[sj++];
-          if (plan[i].decoder == rank)
-            DI_TRY(hipMemcpyAsync(slot(plan[i].seg, f), p, F, hipMemcpyDeviceToDevice, st));
+    auto pslot = [&](uint64_t s, int f) {
+      return f < k ? p_data + (prow.at(s) * (size_t)k + f) * F
+                   : p_par + (prow.at(s) * (size_t)m + (f - k)) * F;
+    };
+    // local survivors into the survivor staging (decoder) or the partial batch (held), and
+    // this rank's survivors of the round in plan order for the sends
+    std::vector<uint8_t> ppres(pmine.size() * n, 0), pheld(pmine.size() * n, 0);
+    std::vector<const uint8_t*> round_src;
+    for (size_t i = r0; i < r1; ++i) {
+      const Seg& g = plan[i];
+      const bool pm = g.partial && prow.count(g.seg);
+      for (int f : g.surv) {
+        if (pm) ppres[prow[g.seg] * n + f] = 1;
+        if (owner(g.seg, f, world) != rank) continue;
+        const uint8_t* p = src_ptr[si++];
+        round_src.push_back(p);
+        if (pm) {
+          pheld[prow[g.seg] * n + f] = 1;
+          DI_TRY(hipMemcpyAsync(pslot(g.seg, f), p, F, hipMemcpyDeviceToDevice, st));
+        } else if (!g.partial && g.decoder == rank) {
+          DI_TRY(hipMemcpyAsync(slot(g.seg, f), p, F, hipMemcpyDeviceToDevice, st));
         }
+      }
+    }
+    if (!pmine.empty()) {
+      rc = cec_reconstruct_partial_batch(d->codec, p_data, p_par, pmine.size(), F, ppres.data(),
+                                         pheld.data(), 0, st);
+      if (rc) return rc;
+      for (const auto& [key, i] : pair)
+        DI_TRY(hipMemcpyAsync(acc + i * F, pslot(key.first, key.second), F,
+                              hipMemcpyDeviceToDevice, st));
+      bool ragged = false;
+      for (const Seg* g : pmine) ragged |= g->decoder == rank && g->holders.size() < H;
+      if (ragged) DI_TRY(hipMemsetAsync(acc + acc_row, 0, H * acc_row, st));
+    }
+    // one group: survivor moves, then partials, each in plan order (pairs every send with its
+    // receive on the peer)
     NC_TRY(r.group_start());
+    size_t rj = 0;
+    auto fail = [&](ncclResult_t res, const char* what) {
+      r.group_end();
+      return nccl_err(res, what);
+    };
     for (size_t i = r0; i < r1; ++i) {
       const Seg& g = plan[i];
       for (int f : g.surv) {
         const int src = owner(g.seg, f, world);
-        ncclResult_t res = ncclSuccess;
         if (src == rank) {
-          const uint8_t* p = src_ptr[si++];
-          if (g.decoder != rank) res = r.send(p, F, ncclUint8, g.decoder, d->comm, st);
-        } else if (g.decoder == rank) {
-          res = r.recv(slot(g.seg, f), F, ncclUint8, src, d->comm, st);
+          const uint8_t* p = round_src[rj++];
+          if (!g.partial && g.decoder != rank) {
+            ncclResult_t res = r.send(p, F, ncclUint8, g.decoder, d->comm, st);
+            if (res != ncclSuccess) return fail(res, "ncclSend");
+          }
+        } else if (!g.partial && g.decoder == rank) {
+          ncclResult_t res = r.recv(slot(g.seg, f), F, ncclUint8, src, d->comm, st);
+          if (res != ncclSuccess) return fail(res, "ncclRecv");
         }
-        if (res != ncclSuccess) {
-          r.group_end();
-          return nccl_err(res, src == rank ? "ncclSend" : "ncclRecv");
+      }
+    }
+    for (const Seg* g : pmine) {
+      if (g->decoder == rank) {
+        for (size_t h = 0; h < g->holders.size(); ++h)
+          for (int f : g->lost) {
+            ncclResult_t res = r.recv(acc + (h + 1) * acc_row + pair.at({g->seg, f}) * F, F,
+                                      ncclUint8, g->holders[h], d->comm, st);
+            if (res != ncclSuccess) return fail(res, "ncclRecv");
+          }
+      } else {
+        for (int f : g->lost) {
+          ncclResult_t res = r.send(pslot(g->seg, f), F, ncclUint8, g->decoder, d->comm, st);
+          if (res != ncclSuccess) return fail(res, "ncclSend");
         }
       }
     }
     NC_TRY(r.group_end());
-    if (mine.empty()) continue;
-    std::vector<uint8_t> present(mine.size() * n, 0);
-    for (size_t i = 0; i < mine.size(); ++i)
-      for (int f : mine[i]->surv) present[i * n + f] = 1;
-    rc = cec_reconstruct_batch(d->codec, st_data, st_par, mine.size(), F, present.data(), 1, 0,
-                               st);
-    if (rc) return rc;
-    for (const Seg* g : mine)
-      for (size_t i : entries[g->seg]) {
-        DI_TRY(hipMemcpyAsync(d_out[i], slot(g->seg, lost_frag[i]), F, hipMemcpyDeviceToDevice,
-                              st));
-        ++rebuilt;
+    if (!mine.empty()) {
+      std::vector<uint8_t> present(mine.size() * n, 0);
+      for (size_t i = 0; i < mine.size(); ++i)
+        for (int f : mine[i]->surv) present[i * n + f] = 1;
+      rc = cec_reconstruct_batch(d->codec, st_data, st_par, mine.size(), F, present.data(), 1,
+                                 0, st);
+      if (rc) return rc;
+      for (const Seg* g : mine)
+        for (size_t i : entries[g->seg]) {
+          DI_TRY(hipMemcpyAsync(d_out[i], slot(g->seg, lost_frag[i]), F,
+                                hipMemcpyDeviceToDevice, st));
+          ++rebuilt;
+        }
+    }
+    if (npairs) {
+      if (H) {
+        rc = cec_xor_batch(acc, acc + acc_row, H, acc_row, acc_row, st);
+        if (rc) return rc;
       }
+      for (const Seg* g : pmine)
+        if (g->decoder == rank)
+          for (size_t i : entries[g->seg]) {
+            DI_TRY(hipMemcpyAsync(d_out[i], acc + pair.at({g->seg, (int)lost_frag[i]}) * F, F,
+                                  hipMemcpyDeviceToDevice, st));
+            ++rebuilt;
+          }
+    }
   }
   DI_TRY(hipStreamSynchronize(st));
   if (nrebuilt) *nrebuilt = rebuilt;

@@ -131,6 +131,10 @@ void launch_sha256_tick(int tick_mode, ShaChain* tab, uint32_t mask, uint64_t he
 void launch_chunk_gather(const Layout& L, int nshards, uint64_t nfrag, const uint32_t* d_idx,
                          uint32_t nidx, uint64_t chunk_len, uint8_t* out, hipStream_t st);
 
+// XOR reduction (xor.hip): dst[0..len) ^= src[j * stride ..][0..len) for j < nsrc.
+void launch_xor_reduce(uint8_t* dst, const uint8_t* src, uint32_t nsrc, uint64_t stride,
+                       uint64_t len, hipStream_t st);
+
 // Synthetic segment bytes: 64-bit word w of segment s = splitmix64(seed ^ (s << 32) ^ w),
 // little-endian; segments are seg_bytes long and contiguous from `out`.
 void launch_fill_splitmix(uint8_t* out, uint64_t seg_bytes, uint64_t nseg, uint64_t seg0,

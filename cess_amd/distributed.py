@@ -8,6 +8,15 @@ the lost one. RCCL has no XOR reduction (rccl.h ncclRedOp_t: sum/prod/max/min/av
 survivors are moved with grouped point-to-point send/recv (`batch_isend_irecv`) and decoded
 locally by libcessec.
 
+Two exchanges, chosen per segment by `plan_gather(exchange=...)`:
+  * survivors: the k survivors travel to the decoder, which rebuilds the lost fragments;
+  * partials: every other GPU holding survivors multiplies them by their decode coefficients
+    (cec_reconstruct_partial_batch) and sends one partial per lost fragment; the decoder XORs
+    the partials into its own (cec_xor_batch: addition in GF(2^8)). The rebuild is linear, so
+    the sum is the lost fragment. It moves e * (holders) fragments instead of (k - local): for a
+    wide code on 8 GPUs (RS(32,32), 8 fragments per GPU) a single lost fragment costs 7
+    partials instead of 28 survivors. For RS(2,1) the counts tie and survivors are used.
+
 Placement mirrors the chain's miner assignment, which spreads a segment's fragments over
 distinct miners (c-pallets/file-bank/src/functions.rs:187-283, `random_assign_miner`, and
 `:256-276`): fragment f of segment s is stored on GPU (s + f) mod G.
@@ -15,7 +24,7 @@ distinct miners (c-pallets/file-bank/src/functions.rs:187-283, `random_assign_mi
 from __future__ import annotations
 
 import ctypes
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -58,19 +67,35 @@ class GatherPlan:
     # segment -> erased fragment indices
     lost: Dict[int, List[int]]
     bytes_moved: int
+    # partial-product segments: segment -> ranks other than the decoder that hold some of its
+    # survivors and send one partial per lost fragment (no survivor moves for these segments)
+    partial: Dict[int, List[int]] = field(default_factory=dict)
+    # segment -> decoding rank
+    decoder: Dict[int, int] = field(default_factory=dict)
+    world: int = 1
+
+
+EXCHANGES = ("survivors", "partials", "auto")
 
 
 def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
-                frag_bytes: int) -> GatherPlan:
-    """Plan the survivor gather for `lost` = {segment: erased fragment indices}.
+                frag_bytes: int, exchange: str = "survivors") -> GatherPlan:
+    """Plan the degraded read of `lost` = {segment: erased fragment indices}.
 
     The decoder of a segment is the home GPU of its first lost fragment (repair restores the
     fragment where it lives). Survivors = the first k present fragments in index order (the
-    codec's survivor choice), so exactly k fragments per segment are read."""
+    codec's survivor choice), so exactly k fragments per segment are read. `exchange`:
+    "survivors" moves the survivors the decoder lacks; "partials" moves one partial rebuild per
+    lost fragment from every other GPU holding survivors; "auto" takes, per segment, whichever
+    moves fewer bytes (survivors on a tie)."""
+    if exchange not in EXCHANGES:
+        raise ValueError(f"exchange must be one of {EXCHANGES}")
     n = k + m
     segs: Dict[int, List[int]] = {}
     moves = {}
     present = {}
+    partial = {}
+    decoder = {}
     moved = 0
     for s in sorted(lost):
         erased = set(lost[s])
@@ -83,17 +108,52 @@ def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
             raise ValueError(f"segment {s}: {len(erased)} erasures > m = {m}")
         dec = fragment_owner(s, min(erased), world)
         segs.setdefault(dec, []).append(s)
+        decoder[s] = dec
         surv = [f for f in range(n) if f not in erased][:k]
         flags = np.zeros(n, np.uint8)
         flags[surv] = 1
         present[s] = flags
+        holders = sorted({fragment_owner(s, f, world) for f in surv} - {dec})
+        n_surv = sum(fragment_owner(s, f, world) != dec for f in surv)
+        n_part = len(erased) * len(holders)
+        if exchange == "partials" or (exchange == "auto" and n_part < n_surv):
+            partial[s] = holders
+            moved += n_part * frag_bytes
+            continue
         for f in surv:
             src = fragment_owner(s, f, world)
             moves[(s, f)] = (src, dec)
             if src != dec:
                 moved += frag_bytes
     return GatherPlan(segs, moves, present, {s: sorted(set(v)) for s, v in lost.items() if v},
-                      moved)
+                      moved, partial, decoder, world)
+
+
+def _p2p(ops_spec, group, stage: bool):
+    """Issue [(is_send, tensor, peer)] as one grouped point-to-point batch and wait. gloo (CPU
+    tests, rehearsals) needs host buffers: device tensors are staged through host memory."""
+    import torch
+    import torch.distributed as dist
+    ops, copies = [], []
+    for is_send, t, peer in ops_spec:
+        if is_send:
+            ops.append(dist.P2POp(dist.isend, t.cpu() if stage else t, peer, group))
+        elif stage:
+            h = torch.empty(t.shape, dtype=t.dtype)
+            copies.append((t, h))
+            ops.append(dist.P2POp(dist.irecv, h, peer, group))
+        else:
+            ops.append(dist.P2POp(dist.irecv, t, peer, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    for t, h in copies:
+        t.copy_(h)
+
+
+def _staged(dev, group) -> bool:
+    import torch.distributed as dist
+    return dev.type == "cuda" and dist.is_initialized() and dist.get_backend(group) == "gloo"
 
 
 def gather_survivors(plan: GatherPlan, store: FragmentStore, k: int, m: int, rank: int,
@@ -108,7 +168,8 @@ def gather_survivors(plan: GatherPlan, store: FragmentStore, k: int, m: int, ran
 
     F = store.data.shape[1]
     dev = store.data.device
-    mysegs = plan.segments.get(rank, [])
+    # partial-product segments are served by partial_exchange
+    mysegs = [s for s in plan.segments.get(rank, []) if s not in plan.partial]
     row = {s: i for i, s in enumerate(mysegs)}
     sd = torch.empty((len(mysegs), k, F), dtype=torch.uint8, device=dev)
     sp = torch.empty((len(mysegs), m, F), dtype=torch.uint8, device=dev)
@@ -116,57 +177,111 @@ def gather_survivors(plan: GatherPlan, store: FragmentStore, k: int, m: int, ran
     def dst_view(s, f):
         return sd[row[s], f] if f < k else sp[row[s], f - k]
 
-    # RCCL/NCCL moves HBM buffers directly (xGMI); gloo (CPU tests, rehearsals) needs host
-    # buffers, so device tensors are staged through host memory on that backend.
-    stage = dev.type == "cuda" and dist.is_initialized() and dist.get_backend(group) == "gloo"
-    ops, copies = [], []
+    # RCCL/NCCL moves HBM buffers directly (xGMI)
+    ops = []
     for (s, f), (src, dst) in sorted(plan.moves.items()):
         if src == dst == rank:
             dst_view(s, f).copy_(store.data[store.slots[(s, f)]])
         elif src == rank:
-            t = store.data[store.slots[(s, f)]]
-            ops.append(dist.P2POp(dist.isend, t.cpu() if stage else t, dst, group))
+            ops.append((True, store.data[store.slots[(s, f)]], dst))
         elif dst == rank:
-            t = dst_view(s, f)
-            if stage:
-                h = torch.empty(t.shape, dtype=t.dtype)
-                copies.append((t, h))
-                t = h
-            ops.append(dist.P2POp(dist.irecv, t, src, group))
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
-    for t, h in copies:
-        t.copy_(h)
+            ops.append((False, dst_view(s, f), src))
+    _p2p(ops, group, _staged(dev, group))
     if not mysegs:
         return None, None, None, []
     present = np.stack([plan.present[s] for s in mysegs])
     return sd, sp, present, mysegs
 
 
-def degraded_read(plan: GatherPlan, store: FragmentStore, enc, rank: int, group=None):
-    """Gather survivors over RCCL and rebuild the lost fragments on this rank's GPU with
-    libcessec. Returns {(segment, fragment): tensor[F]} of rebuilt fragments for this rank."""
+def partial_exchange(plan: GatherPlan, store: FragmentStore, enc, rank: int, group=None,
+                     xor=None):
+    """The partial-product segments of `plan` on this rank: rebuild, from the survivors this rank
+    holds, the partial of every lost fragment of every partial segment it holds survivors of or
+    decodes (one cec_reconstruct_partial_batch launch); send the partials to their decoders;
+    on the decoder, XOR the received partials into its own (one cec_xor_batch launch).
+    Returns {(segment, fragment): tensor[F]} of the fragments this rank rebuilt."""
+    import torch
+    if xor is None:
+        from .reedsolomon import xor_batch as xor
+    k, m = enc.DataShards, enc.ParityShards
+    n = k + m
+    F = store.data.shape[1]
+    dev = store.data.device
+    mine = [s for s in sorted(plan.partial)
+            if plan.decoder[s] == rank or rank in plan.partial[s]]
+    if not mine:
+        return {}
+    row = {s: i for i, s in enumerate(mine)}
+    sd = torch.empty((len(mine), k, F), dtype=torch.uint8, device=dev)
+    sp = torch.empty((len(mine), m, F), dtype=torch.uint8, device=dev)
+
+    def slot(s, f):
+        return sd[row[s], f] if f < k else sp[row[s], f - k]
+
+    pres = np.stack([plan.present[s] for s in mine])
+    held = np.zeros_like(pres)
+    for s in mine:
+        for f in np.flatnonzero(plan.present[s]):
+            if fragment_owner(s, int(f), plan.world) == rank:
+                held[row[s], f] = 1
+                slot(s, int(f)).copy_(store.data[store.slots[(s, int(f))]])
+    enc.ReconstructPartialBatch(sd, sp, len(mine), F, pres, held,
+                                stream=torch.cuda.current_stream(dev) if dev.type == "cuda"
+                                else None)
+    dsegs = [s for s in mine if plan.decoder[s] == rank]
+    pairs = [(s, f) for s in dsegs for f in plan.lost[s]]
+    pidx = {p: i for i, p in enumerate(pairs)}
+    H = max([len(plan.partial[s]) for s in dsegs], default=0)
+    # row 0: this rank's partials; rows 1..H: the holders' (zero where a segment has fewer)
+    acc = torch.empty((H + 1, max(1, len(pairs)), F), dtype=torch.uint8, device=dev)
+    for (s, f), i in pidx.items():
+        acc[0, i].copy_(slot(s, f))
+    if any(len(plan.partial[s]) < H for s in dsegs):
+        acc[1:].zero_()
+    ops = []
+    for s in mine:  # the same (segment, fragment) order on both sides of every pair
+        if plan.decoder[s] == rank:
+            for h, src in enumerate(plan.partial[s]):
+                for f in plan.lost[s]:
+                    ops.append((False, acc[1 + h, pidx[(s, f)]], src))
+        else:
+            for f in plan.lost[s]:
+                ops.append((True, slot(s, f), plan.decoder[s]))
+    _p2p(ops, group, _staged(dev, group))
+    if H and pairs:
+        xor(acc[0], acc[1], H, acc.stride(0), len(pairs) * F)
+    return {p: acc[0, i] for p, i in pidx.items()}
+
+
+def degraded_read(plan: GatherPlan, store: FragmentStore, enc, rank: int, group=None,
+                  xor=None):
+    """Rebuild the lost fragments of `plan` over the process group (RCCL on GPUs): survivor
+    segments by gathering survivors and one libcessec rebuild, partial-product segments by
+    partial_exchange. Returns {(segment, fragment): tensor[F]} of rebuilt fragments for this
+    rank."""
     k, m = enc.DataShards, enc.ParityShards
     sd, sp, present, segs = gather_survivors(plan, store, k, m, rank, group)
-    if not segs:
-        return {}
-    import torch
-    enc.ReconstructBatch(sd, sp, len(segs), sd.shape[2], present,
-                         stream=torch.cuda.current_stream(sd.device))
-    # unused survivors are rebuilt too (they are absent from the staging); return the lost ones
     out = {}
-    for i, s in enumerate(segs):
-        for f in plan.lost[s]:
-            out[(s, f)] = sd[i, f] if f < k else sp[i, f - k]
+    if segs:
+        import torch
+        enc.ReconstructBatch(sd, sp, len(segs), sd.shape[2], present,
+                             stream=torch.cuda.current_stream(sd.device) if sd.is_cuda else None)
+        # unused survivors are rebuilt too (they are absent from the staging); return the lost
+        for i, s in enumerate(segs):
+            for f in plan.lost[s]:
+                out[(s, f)] = sd[i, f] if f < k else sp[i, f - k]
+    if plan.partial:
+        out.update(partial_exchange(plan, store, enc, rank, group, xor))
     return out
 
 
 # -- the same exchange through the C ABI (cec_dist_*, for hosts without torch.distributed) -------
 
-def c_plan(lost: Dict[int, Sequence[int]], k: int, m: int, world: int):
-    """cec_dist_plan: (moves [(seg, frag, src, dst)] in issue order, {(seg, frag): decoder rank})
-    of the plan libcessec's degraded read runs for `lost` (host only)."""
+def c_plan(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
+           exchange: str = "survivors"):
+    """cec_dist_plan_ex: (moves [(seg, frag, src, dst, kind)] in issue order, {(seg, frag):
+    decoder rank}) of the plan libcessec's degraded read runs for `lost` (host only); kind 0 = a
+    survivor fragment, 1 = a partial rebuild of lost fragment `frag`."""
     from ctypes import byref, c_int32, c_size_t, c_uint8, c_uint64
     from . import _lib
     from .reedsolomon import check
@@ -175,13 +290,14 @@ def c_plan(lost: Dict[int, Sequence[int]], k: int, m: int, world: int):
     frags = (c_uint8 * max(1, len(pairs)))(*[f for _, f in pairs])
     lib = _lib.load()
     n = c_size_t()
-    check(lib.cec_dist_plan(k, m, world, segs, frags, len(pairs), None, 0, byref(n), None),
-          "cec_dist_plan")
+    ex = EXCHANGES.index(exchange)
+    check(lib.cec_dist_plan_ex(k, m, world, ex, segs, frags, len(pairs), None, 0, byref(n),
+                               None), "cec_dist_plan_ex")
     moves = (_lib.DistMove * max(1, n.value))()
     dec = (c_int32 * max(1, len(pairs)))()
-    check(lib.cec_dist_plan(k, m, world, segs, frags, len(pairs), moves, n.value, byref(n), dec),
-          "cec_dist_plan")
-    return ([(mv.seg, mv.frag, mv.src, mv.dst) for mv in moves[:n.value]],
+    check(lib.cec_dist_plan_ex(k, m, world, ex, segs, frags, len(pairs), moves, n.value,
+                               byref(n), dec), "cec_dist_plan_ex")
+    return ([(mv.seg, mv.frag, mv.src, mv.dst, mv.kind) for mv in moves[:n.value]],
             {p: dec[i] for i, p in enumerate(pairs)})
 
 
@@ -197,7 +313,7 @@ class RcclGroup:
         check(_lib.load().cec_dist_unique_id(buf), "cec_dist_unique_id")
         return bytes(buf)
 
-    def __init__(self, enc, uid: bytes, world: int, rank: int):
+    def __init__(self, enc, uid: bytes, world: int, rank: int, exchange: str = "survivors"):
         from ctypes import byref, c_void_p
         from . import _lib
         from .reedsolomon import check
@@ -207,6 +323,9 @@ class RcclGroup:
         idb = (ctypes.c_uint8 * _lib.CEC_DIST_ID_BYTES).from_buffer_copy(uid)
         check(self._lib.cec_dist_create(enc._h, idb, world, rank, byref(self._h)),
               "cec_dist_create")
+        self.exchange = exchange
+        check(self._lib.cec_dist_set_option(self._h, _lib.CEC_DIST_OPT_EXCHANGE,
+                                            EXCHANGES.index(exchange)), "cec_dist_set_option")
 
     def close(self) -> None:
         if self._h:
@@ -235,7 +354,8 @@ class RcclGroup:
         F = store.data.shape[1]
         lost = {s: sorted(set(v)) for s, v in lost.items() if len(v)}
         pairs = [(s, f) for s in sorted(lost) for f in lost[s]]
-        _, dec = c_plan(lost, self.enc.DataShards, self.enc.ParityShards, self.world)
+        _, dec = c_plan(lost, self.enc.DataShards, self.enc.ParityShards, self.world,
+                        self.exchange)
         out = {p: torch.empty(F, dtype=torch.uint8, device=store.data.device)
                for p in pairs if dec[p] == self.rank}
         segs = (c_uint64 * max(1, len(pairs)))(*[s for s, _ in pairs])

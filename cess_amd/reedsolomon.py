@@ -292,6 +292,20 @@ class Encoder:
             p.ctypes.data_as(POINTER(c_uint8)), per_segment, 1 if data_only else 0,
             _stream_handle(stream)), "ReconstructBatch")
 
+    def ReconstructPartialBatch(self, d_data, d_parity, nseg: int, shard_len: int, present,
+                                held, data_only: bool = False, stream=None) -> None:
+        """Partial rebuild (cec_reconstruct_partial_batch): every missing shard of segment s gets
+        the contribution of the survivors of `present[s]` flagged in `held[s]` (both nseg x n).
+        XOR of the partials over a partition of the survivors = ReconstructBatch's result."""
+        p = np.ascontiguousarray(np.asarray(present, dtype=np.uint8))
+        h = np.ascontiguousarray(np.asarray(held, dtype=np.uint8))
+        if p.shape != (nseg, self.Shards) or h.shape != (nseg, self.Shards):
+            raise ValueError("present and held must be (nseg, k+m)")
+        check(self._lib.cec_reconstruct_partial_batch(
+            self._h, _dev_ptr(d_data), _dev_ptr(d_parity), nseg, shard_len,
+            p.ctypes.data_as(POINTER(c_uint8)), h.ctypes.data_as(POINTER(c_uint8)),
+            1 if data_only else 0, _stream_handle(stream)), "ReconstructPartialBatch")
+
     def Sha256Batch(self, d_data, d_parity, nseg: int, shard_len: int, d_hex,
                     stream=None) -> None:
         """Hex SHA-256 of every shard into d_hex ([nseg][k+m][64] bytes, device)."""
@@ -309,6 +323,13 @@ def fill_synthetic(d_out, seg_bytes: int, nseg: int, seg0: int, seed: int, strea
     """Counter-based synthetic segments in HBM (SURVEY.md §8d input generator)."""
     check(_lib.load().cec_fill_synthetic(_dev_ptr(d_out), seg_bytes, nseg, seg0, seed,
                                          _stream_handle(stream)), "fill_synthetic")
+
+
+def xor_batch(d_dst, d_src, nsrc: int, src_stride: int, length: int, stream=None) -> None:
+    """d_dst[:length] ^= XOR of nsrc buffers at d_src + j * src_stride (cec_xor_batch: GF(2^8)
+    addition of the partial rebuilds other GPUs sent)."""
+    check(_lib.load().cec_xor_batch(_dev_ptr(d_dst), _dev_ptr(d_src), nsrc, src_stride, length,
+                                    _stream_handle(stream)), "xor_batch")
 
 
 def sha256_hex_device(d_ptrs: Sequence[int], length: int) -> List[bytes]:

@@ -86,6 +86,21 @@ int cec_encode_batch(cec_codec* codec, const uint8_t* d_data, uint8_t* d_parity,
 int cec_reconstruct_batch(cec_codec* codec, uint8_t* d_data, uint8_t* d_parity, size_t nseg,
                           size_t shard_len, const uint8_t* present, int per_segment,
                           int data_only, void* hip_stream);
+/* Partial rebuild (the partial-product exchange of a multi-GPU degraded read):
+ * like cec_reconstruct_batch with per-segment patterns (present: nseg*(k+m) flags; survivors =
+ * the first k present shards of each segment), but every missing shard receives only the
+ * contribution of the survivors flagged in `held` (nseg*(k+m) flags; flags of non-survivors are
+ * ignored): out = XOR over held survivors i of D[out][i] * shard_i. Only held survivors are read.
+ * The rebuild is linear, so XOR-ing the partials of a partition of the survivors (one per GPU
+ * holding some of them, cec_xor_batch) gives the missing shard; a segment with no held survivor
+ * gets zeros. A GPU then sends one partial per lost fragment instead of its survivors. */
+int cec_reconstruct_partial_batch(cec_codec* codec, uint8_t* d_data, uint8_t* d_parity,
+                                  size_t nseg, size_t shard_len, const uint8_t* present,
+                                  const uint8_t* held, int data_only, void* hip_stream);
+/* GF(2^8) addition of device buffers: d_dst[0..len) ^= d_src[j*src_stride ..][0..len) for
+ * j < nsrc (src_stride >= len when nsrc > 1). Enqueued on hip_stream. */
+int cec_xor_batch(uint8_t* d_dst, const uint8_t* d_src, size_t nsrc, size_t src_stride,
+                  size_t len, void* hip_stream);
 /* SHA-256 of every shard of every segment in the batch layout, as 64 lowercase hex chars:
  * d_hex[(seg*(k+m) + shard)*64 ...]. d_parity may be NULL to hash the k data shards only, in
  * which case the index is seg*k + shard. */
@@ -232,20 +247,35 @@ int cec_dist_unique_id(uint8_t* id /* CEC_DIST_ID_BYTES */);
  * with the same id. The group keeps using `codec` until cec_dist_destroy. */
 int cec_dist_create(cec_codec* codec, const uint8_t* id, int world, int rank, cec_dist** out);
 void cec_dist_destroy(cec_dist* d);
-/* One survivor transfer of a plan: fragment `frag` of segment `seg` from rank src to rank dst
- * (src == dst: already local). */
+/* One transfer of a plan. kind CEC_DIST_SURVIVOR: fragment `frag` of segment `seg` from rank src
+ * to rank dst (src == dst: already local). kind CEC_DIST_PARTIAL: rank src's partial rebuild of
+ * lost fragment `frag` (from the survivors src holds, cec_reconstruct_partial_batch) to the
+ * decoder dst, which XORs the partials. */
+#define CEC_DIST_SURVIVOR 0
+#define CEC_DIST_PARTIAL 1
 typedef struct cec_dist_move {
   uint64_t seg;
   int32_t frag, src, dst;
+  int32_t kind;
 } cec_dist_move;
+/* Exchange of a degraded read (cec_dist_set_option CEC_DIST_OPT_EXCHANGE, cec_dist_plan_ex):
+ * 0 = survivors (the k survivors travel to the decoder; default), 1 = partials (every other rank
+ * holding survivors sends one partial per lost fragment), 2 = per segment whichever moves fewer
+ * fragments, survivors on a tie (a wide code spread over many GPUs with few erasures: RS(32,32)
+ * on 8 GPUs, one lost fragment, 7 partials instead of 27-28 survivors). */
+#define CEC_DIST_OPT_EXCHANGE 1
+int cec_dist_set_option(cec_dist* d, int option, int value);
 /* Host only: the plan a degraded read of the lost list runs. The list holds nlost (segment,
  * fragment) erasures, any order, duplicates allowed, at most m distinct per segment
- * (CEC_ETOOFEW otherwise; CEC_EINVAL for an index >= k+m). Writes the survivor moves in issue
- * order (*nmoves of them; CEC_EINVAL if more than moves_cap, moves may be NULL to count) and,
- * per lost entry, the rank that rebuilds it (decoder, may be NULL). */
+ * (CEC_ETOOFEW otherwise; CEC_EINVAL for an index >= k+m). Writes the moves in issue order
+ * (*nmoves of them; CEC_EINVAL if more than moves_cap, moves may be NULL to count) and, per lost
+ * entry, the rank that rebuilds it (decoder, may be NULL). cec_dist_plan = exchange 0. */
 int cec_dist_plan(int k, int m, int world, const uint64_t* lost_seg, const uint8_t* lost_frag,
                   size_t nlost, cec_dist_move* moves, size_t moves_cap, size_t* nmoves,
                   int32_t* decoder);
+int cec_dist_plan_ex(int k, int m, int world, int exchange, const uint64_t* lost_seg,
+                     const uint8_t* lost_frag, size_t nlost, cec_dist_move* moves,
+                     size_t moves_cap, size_t* nmoves, int32_t* decoder);
 /* Device address (shard_len bytes) of fragment (seg, frag) held by this rank, NULL if absent. */
 typedef const uint8_t* (*cec_locate_fn)(void* user, uint64_t seg, int frag);
 /* Degraded read. Collective: every rank passes the same lost list. Rank r sends the survivors

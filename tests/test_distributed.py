@@ -103,6 +103,122 @@ def test_degraded_gather_gloo(world, k, m):
     assert sum(n for _, _, n in res) == nseg
 
 
+def test_plan_exchange_choice():
+    """Partial-product exchange: 'auto' takes partials only where they move fewer
+    bytes; RS(32,32) on 8 GPUs with one lost fragment: 7 partials instead of 27-28 survivors."""
+    k, m, G, F = 32, 32, 8, 512 * 1024
+    lost = {s: [s % 64] for s in range(16)}
+    surv = D.plan_gather(lost, k, m, G, F)
+    auto = D.plan_gather(lost, k, m, G, F, exchange="auto")
+    assert not surv.partial and set(auto.partial) == set(lost) and not auto.moves
+    assert all(len(h) == G - 1 for h in auto.partial.values())
+    assert auto.bytes_moved == 16 * (G - 1) * F
+    # 27-28 survivors of 32 live off the decoder
+    want = sum(sum((s + f) % G != (2 * s) % G  # decoder: the lost fragment's home
+                   for f in [f for f in range(64) if f != s % 64][:32]) for s in range(16))
+    assert surv.bytes_moved == want * F and want >= 16 * 27
+    # RS(2,1) spread over >= 3 GPUs: 2 survivors vs 2 partials, a tie -> survivors
+    l21 = {s: [s % 3] for s in range(30)}
+    assert not D.plan_gather(l21, 2, 1, 8, F, exchange="auto").partial
+    # many erasures: partials cost e * holders and lose
+    many = {s: list(range(32)) for s in range(4)}
+    assert not D.plan_gather(many, k, m, G, F, exchange="auto").partial
+    forced = D.plan_gather(many, k, m, G, F, exchange="partials")
+    assert forced.bytes_moved == sum(32 * len(h) for h in forced.partial.values()) * F
+    with pytest.raises(ValueError):
+        D.plan_gather(lost, k, m, G, F, exchange="bogus")
+
+
+class _OracleEnc:
+    """CPU stand-in for the libcessec Encoder in the gloo tests: the oracle does the arithmetic
+    (the HIP kernels behind ReconstructBatch / ReconstructPartialBatch / xor_batch are checked
+    against the oracle in tests/test_gpu_partial.py); this exercises the exchange itself."""
+
+    def __init__(self, k, m):
+        from oracle import rs_oracle as o
+        self.o, self.rs = o, o.ReedSolomon(k, m)
+        self.DataShards, self.ParityShards = k, m
+
+    def _views(self, sd, sp, i):
+        k = self.DataShards
+        return [sd[i, f] if f < k else sp[i, f - k] for f in range(k + self.ParityShards)]
+
+    def ReconstructBatch(self, sd, sp, nseg, F, present, stream=None):
+        for i in range(nseg):
+            v = self._views(sd, sp, i)
+            rec = self.rs.reconstruct([v[f].numpy().copy() if present[i][f] else None
+                                       for f in range(len(v))])
+            for f in range(len(v)):
+                if not present[i][f]:
+                    v[f].copy_(torch.from_numpy(rec[f]))
+
+    def ReconstructPartialBatch(self, sd, sp, nseg, F, present, held, stream=None):
+        for i in range(nseg):
+            v = self._views(sd, sp, i)
+            surv, outs, rows = self.rs.decode_plan(present[i])
+            cols = [j for j, f in enumerate(surv) if held[i][f]]
+            vals = (self.o.code_rows([[r[j] for j in cols] for r in rows],
+                                     [v[surv[j]].numpy() for j in cols])
+                    if cols else [np.zeros(F, np.uint8) for _ in outs])
+            for o_, val in zip(outs, vals):
+                v[o_].copy_(torch.from_numpy(np.asarray(val, np.uint8)))
+
+
+def _xor_cpu(dst, src, nsrc, stride, length):
+    rows = torch.as_strided(src, (nsrc, length), (stride, 1), src.storage_offset())
+    d = dst.view(-1)[:length]
+    for j in range(nsrc):
+        d ^= rows[j]
+
+
+def _exchange_worker(rank, world, port, k, m, nseg, F, exchange, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import rs_oracle as o
+    rs = o.ReedSolomon(k, m)
+    n = k + m
+    rng = np.random.default_rng(11)
+    full = []
+    for s in range(nseg):
+        data = [rng.integers(0, 256, F, dtype=np.uint8) for _ in range(k)]
+        full.append(data + rs.encode(data))
+    mine = D.local_fragments(nseg, n, world, rank)
+    store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
+                            torch.from_numpy(np.stack([full[s][f] for s, f in mine])))
+    lost = {s: sorted(rng.choice(n, size=1 + (s % m), replace=False).tolist())
+            for s in range(nseg)}
+    plan = D.plan_gather(lost, k, m, world, F, exchange=exchange)
+    out = D.degraded_read(plan, store, _OracleEnc(k, m), rank, xor=_xor_cpu)
+    ok = all(np.array_equal(t.numpy(), full[s][f]) for (s, f), t in out.items())
+    q.put((rank, ok, len(out), len(plan.partial)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k,m,exchange", [(2, 2, 1, "partials"), (3, 4, 2, "auto"),
+                                                (3, 4, 2, "partials"), (2, 4, 2, "partials"),
+                                                (3, 10, 4, "auto")])
+def test_degraded_read_partials_gloo(world, k, m, exchange):
+    """degraded_read with the partial-product exchange at world 2/3 (gloo): every lost fragment
+    comes back equal to the oracle's codeword; 'auto' mixes both exchanges in one call."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    nseg, F = 9, 2048
+    procs = [ctx.Process(target=_exchange_worker,
+                         args=(r, world, port, k, m, nseg, F, exchange, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _, _ in res), res
+    assert sum(n for _, _, n, _ in res) == sum(1 + (s % m) for s in range(nseg))
+    assert all(npart > 0 for _, _, _, npart in res)
+
+
 @pytest.mark.parametrize("k,m", [(2, 1), (4, 2), (10, 4), (32, 32)])
 def test_c_plan_matches_python_plan(k, m):
     """cec_dist_plan (the plan libcessec's RCCL degraded read runs, cec_dist_degraded_read) equals
@@ -117,10 +233,20 @@ def test_c_plan_matches_python_plan(k, m):
             lost[s] = e + e[:1]  # a duplicate entry
         moves, dec = D.c_plan(lost, k, m, world)
         plan = D.plan_gather(lost, k, m, world, 1)
-        assert {(s, f): (src, dst) for s, f, src, dst in moves} == plan.moves
-        assert [(s, f) for s, f, _, _ in moves] == sorted(plan.moves)  # the issue order
+        assert {(s, f): (src, dst) for s, f, src, dst, _ in moves} == plan.moves
+        assert [(s, f) for s, f, _, _, _ in moves] == sorted(plan.moves)  # the issue order
+        assert all(kind == 0 for *_, kind in moves)
         for (s, f), r in dec.items():
             assert s in plan.segments[r]
+        for ex in ("partials", "auto"):  # the partial-product exchange
+            moves, dec = D.c_plan(lost, k, m, world, ex)
+            plan = D.plan_gather(lost, k, m, world, 1, exchange=ex)
+            assert {(s, f): (src, dst) for s, f, src, dst, kind in moves if kind == 0} \
+                == plan.moves
+            want = {(s, f, h, plan.decoder[s]) for s, hs in plan.partial.items()
+                    for h in hs for f in plan.lost[s]}
+            assert {(s, f, src, dst) for s, f, src, dst, kind in moves if kind == 1} == want
+            assert all(plan.decoder[s] == r for (s, _), r in dec.items())
     with pytest.raises(CecError):
         D.c_plan({3: [n]}, k, m, 2)  # index outside 0..n-1
     with pytest.raises(ErrTooFewShards):

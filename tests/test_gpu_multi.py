@@ -21,7 +21,7 @@ def _port():
     return p
 
 
-def _rank(rank, world, port, k, m, nseg, F, q):
+def _rank(rank, world, port, k, m, nseg, F, q, exchange="survivors"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch
@@ -44,7 +44,7 @@ def _rank(rank, world, port, k, m, nseg, F, q):
     store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
                             torch.from_numpy(np.stack([full[s][f] for s, f in mine])).to(dev))
     lost = {s: sorted(rng.choice(n, size=1 + s % m, replace=False).tolist()) for s in range(nseg)}
-    plan = D.plan_gather(lost, k, m, world, F)
+    plan = D.plan_gather(lost, k, m, world, F, exchange=exchange)
     out = D.degraded_read(plan, store, cess_amd.New(k, m, device=rank), rank)
     torch.cuda.synchronize(dev)
     ok = all(np.array_equal(t.cpu().numpy(), full[s][f]) for (s, f), t in out.items())
@@ -53,8 +53,9 @@ def _rank(rank, world, port, k, m, nseg, F, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k,m", [(2, 1), (4, 2)])
-def test_degraded_read_rccl(k, m):
+@pytest.mark.parametrize("k,m,exchange", [(2, 1, "survivors"), (4, 2, "survivors"),
+                                          (4, 2, "partials"), (10, 4, "auto")])
+def test_degraded_read_rccl(k, m, exchange):
     import torch
     import torch.multiprocessing as mp
     world = min(torch.cuda.device_count(), 4)
@@ -64,7 +65,7 @@ def test_degraded_read_rccl(k, m):
     q = ctx.Queue()
     port = _port()
     nseg, F = 12, 1 << 20
-    procs = [ctx.Process(target=_rank, args=(r, world, port, k, m, nseg, F, q))
+    procs = [ctx.Process(target=_rank, args=(r, world, port, k, m, nseg, F, q, exchange))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -75,6 +76,52 @@ def test_degraded_read_rccl(k, m):
     assert all(ok for _, ok, _, _ in res), res
     assert sum(n for _, _, n, _ in res) == sum(1 + s % m for s in range(nseg))
     assert res[0][3] > 0  # survivors crossed GPUs
+
+
+def _gloo_rank(rank, world, port, k, m, nseg, F, exchange, q):
+    """One rank of a multi-process degraded read whose ranks share GPU 0 and talk over gloo
+    (fragments staged through host memory): the product path of partial_exchange and
+    gather_survivors (libcessec partial rebuilds, XOR combine, survivor rebuilds) end to end on
+    the one-GPU box; only the transport differs from RCCL."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import cess_amd
+    from cess_amd import distributed as D
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    full, lost = _codewords(k, m, nseg, F, seed=5)
+    n = k + m
+    mine = D.local_fragments(nseg, n, world, rank)
+    store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
+                            torch.from_numpy(np.stack([full[s][f] for s, f in mine])).cuda())
+    plan = D.plan_gather(lost, k, m, world, F, exchange=exchange)
+    out = D.degraded_read(plan, store, cess_amd.New(k, m), rank)
+    torch.cuda.synchronize()
+    ok = all(np.array_equal(t.cpu().numpy(), full[s][f]) for (s, f), t in out.items())
+    q.put((rank, ok, len(out), len(plan.partial)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k,m,exchange", [(3, 4, 2, "partials"), (3, 10, 4, "auto"),
+                                                (2, 32, 32, "auto")])
+def test_degraded_read_partials_shared_gpu(world, k, m, exchange):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    nseg, F = 10, (1 << 16) + 32
+    procs = [ctx.Process(target=_gloo_rank, args=(r, world, port, k, m, nseg, F, exchange, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _, _ in res), res
+    assert sum(nr for _, _, nr, _ in res) == sum(1 + s % m for s in range(nseg))
+    assert all(npart > 0 for *_, npart in res)
 
 
 def _codewords(k, m, nseg, F, seed=7):
@@ -90,9 +137,13 @@ def _codewords(k, m, nseg, F, seed=7):
     return full, lost
 
 
-@pytest.mark.parametrize("k,m,nseg,F", [(2, 1, 12, (1 << 20) + 64), (4, 2, 12, (1 << 20) + 64),
-                                         (10, 4, 12, (1 << 20) + 64), (2, 1, 600, 65536)])
-def test_c_dist_degraded_read_world1(k, m, nseg, F):
+@pytest.mark.parametrize("k,m,nseg,F,exchange", [(2, 1, 12, (1 << 20) + 64, "survivors"),
+                                                  (4, 2, 12, (1 << 20) + 64, "survivors"),
+                                                  (10, 4, 12, (1 << 20) + 64, "survivors"),
+                                                  (2, 1, 600, 65536, "survivors"),
+                                                  (10, 4, 12, (1 << 20) + 64, "partials"),
+                                                  (4, 2, 600, 4096, "partials")])
+def test_c_dist_degraded_read_world1(k, m, nseg, F, exchange):
     """cec_dist_degraded_read (libcessec's own RCCL group, the C form of degraded_read) at world
     1: plan, agreement all-reduce, local survivor copies, per-segment rebuild and copy-out, every
     rebuilt fragment equal to the C oracle's codeword; a store missing a survivor fails with
@@ -107,7 +158,7 @@ def test_c_dist_degraded_read_world1(k, m, nseg, F):
     store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
                             torch.from_numpy(np.stack([full[s][f] for s, f in mine])).cuda())
     enc = cess_amd.New(k, m)
-    g = D.RcclGroup(enc, D.RcclGroup.unique_id(), 1, 0)
+    g = D.RcclGroup(enc, D.RcclGroup.unique_id(), 1, 0, exchange)
     try:
         out = g.degraded_read(lost, store)
         assert len(out) == sum(len(v) for v in lost.values())
@@ -124,7 +175,7 @@ def test_c_dist_degraded_read_world1(k, m, nseg, F):
         g.close()
 
 
-def _c_rank(rank, world, uid_path, k, m, nseg, F, q):
+def _c_rank(rank, world, uid_path, k, m, nseg, F, q, exchange="survivors"):
     os.environ.update(HSA_ENABLE_IPC_MODE_LEGACY="0")
     import time
     import torch
@@ -143,15 +194,16 @@ def _c_rank(rank, world, uid_path, k, m, nseg, F, q):
     mine = D.local_fragments(nseg, n, world, rank)
     store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
                             torch.from_numpy(np.stack([full[s][f] for s, f in mine])).cuda())
-    g = D.RcclGroup(cess_amd.New(k, m, device=rank), uid, world, rank)
+    g = D.RcclGroup(cess_amd.New(k, m, device=rank), uid, world, rank, exchange)
     out = g.degraded_read(lost, store)
     ok = all(np.array_equal(t.cpu().numpy(), full[s][f]) for (s, f), t in out.items())
     g.close()
     q.put((rank, ok, len(out)))
 
 
-@pytest.mark.parametrize("k,m", [(2, 1), (4, 2)])
-def test_c_dist_degraded_read_rccl(k, m, tmp_path):
+@pytest.mark.parametrize("k,m,exchange", [(2, 1, "survivors"), (4, 2, "survivors"),
+                                          (4, 2, "partials"), (10, 4, "auto")])
+def test_c_dist_degraded_read_rccl(k, m, exchange, tmp_path):
     """The C-ABI degraded read across 2..4 GPUs (one process each, the group id handed over
     through a file as a non-Python host would through its control plane)."""
     import torch
@@ -163,7 +215,7 @@ def test_c_dist_degraded_read_rccl(k, m, tmp_path):
     q = ctx.Queue()
     nseg, F = 12, 1 << 20
     uid = str(tmp_path / "uid")
-    procs = [ctx.Process(target=_c_rank, args=(r, world, uid, k, m, nseg, F, q))
+    procs = [ctx.Process(target=_c_rank, args=(r, world, uid, k, m, nseg, F, q, exchange))
              for r in range(world)]
     for p in procs:
         p.start()

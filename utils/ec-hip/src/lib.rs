@@ -91,8 +91,12 @@ pub mod sys {
         pub frag: i32,
         pub src: i32,
         pub dst: i32,
+        pub kind: i32,
     }
     pub const CEC_DIST_ID_BYTES: usize = 128;
+    pub const CEC_DIST_SURVIVOR: i32 = 0;
+    pub const CEC_DIST_PARTIAL: i32 = 1;
+    pub const CEC_DIST_OPT_EXCHANGE: c_int = 1;
     pub type cec_locate_fn = extern "C" fn(user: *mut c_void, seg: u64, frag: c_int) -> *const u8;
 
     extern "C" {
@@ -107,6 +111,12 @@ pub mod sys {
                                      nseg: usize, shard_len: usize, present: *const u8,
                                      per_segment: c_int, data_only: c_int,
                                      stream: *mut c_void) -> c_int;
+        pub fn cec_reconstruct_partial_batch(c: *mut cec_codec, d_data: *mut u8,
+                                             d_parity: *mut u8, nseg: usize, shard_len: usize,
+                                             present: *const u8, held: *const u8,
+                                             data_only: c_int, stream: *mut c_void) -> c_int;
+        pub fn cec_xor_batch(d_dst: *mut u8, d_src: *const u8, nsrc: usize, src_stride: usize,
+                             len: usize, stream: *mut c_void) -> c_int;
         pub fn cec_sha256_batch(c: *mut cec_codec, d_data: *const u8, d_parity: *const u8,
                                 nseg: usize, shard_len: usize, d_hex: *mut u8,
                                 stream: *mut c_void) -> c_int;
@@ -157,6 +167,11 @@ pub mod sys {
         pub fn cec_dist_plan(k: c_int, m: c_int, world: c_int, lost_seg: *const u64,
                              lost_frag: *const u8, nlost: usize, moves: *mut cec_dist_move,
                              moves_cap: usize, nmoves: *mut usize, decoder: *mut i32) -> c_int;
+        pub fn cec_dist_plan_ex(k: c_int, m: c_int, world: c_int, exchange: c_int,
+                                lost_seg: *const u64, lost_frag: *const u8, nlost: usize,
+                                moves: *mut cec_dist_move, moves_cap: usize, nmoves: *mut usize,
+                                decoder: *mut i32) -> c_int;
+        pub fn cec_dist_set_option(d: *mut cec_dist, option: c_int, value: c_int) -> c_int;
         pub fn cec_dist_degraded_read(d: *mut cec_dist, lost_seg: *const u64,
                                       lost_frag: *const u8, nlost: usize, shard_len: usize,
                                       locate: cec_locate_fn, user: *mut c_void,
@@ -192,6 +207,12 @@ impl<'c> DistGroup<'c> {
         let mut d = std::ptr::null_mut();
         check(unsafe { sys::cec_dist_create(codec.c, id.as_ptr(), world, rank, &mut d) })?;
         Ok(DistGroup { d, _codec: std::marker::PhantomData })
+    }
+
+    /// Exchange of later degraded reads: 0 survivors (default), 1 partial products, 2 per
+    /// segment whichever moves fewer fragments (the same value on every rank).
+    pub fn set_exchange(&mut self, exchange: i32) -> Result<(), Error> {
+        check(unsafe { sys::cec_dist_set_option(self.d, sys::CEC_DIST_OPT_EXCHANGE, exchange) })
     }
 
     /// Rebuild the `lost` (segment, fragment) list, the same on every rank; `locate(seg, frag)`
