@@ -707,9 +707,11 @@ def main() -> None:
         torch.cuda.synchronize(dev)
         cms = a.elapsed_time(b) / 20
         out["roofline"]["copy_ceiling"] = {
-            "GBps": round(2 * src.numel() / (cms * 1e-3) / GB, 1),
-            "what": "D2D copy of the 1 GiB data batch (torch copy_ = hipMemcpyAsync), "
-                    "read + write bytes / time"}
+            "guide_float4_copy_GBps": 6290.0,
+            "hipmemcpy_d2d_GBps": round(2 * src.numel() / (cms * 1e-3) / GB, 1),
+            "what": "measured-copy ceilings beside the 8 TB/s spec: the guide's float4 copy "
+                    "kernel (MI355X_MICROARCH.md) and, measured here, a D2D copy of the 1 GiB data "
+                    "batch through the HIP runtime (torch copy_), read + write bytes / time"}
         del dst
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -5,8 +5,12 @@
            64 rebuilt fragments on the GPU (one SHA-256 chain per fragment: latency bound);
   audit    (f3) the 47 challenged 8 KiB chunks of all 192 fragments of a 1 GiB batch: the gather
            (2 x chunk bytes moved) and gather + SHA-256 of every chunk;
-  fillers  (f4) 64 idle fillers of 8 MiB: generation in HBM and their SHA-256 hashes.
-usage: python tools/aux_bench.py [--reps 5]"""
+  fillers  (f4) 64 idle fillers of 8 MiB: generation in HBM and their SHA-256 hashes;
+  partial  (§8e) the two GPU steps of the partial-product exchange for RS(32,32) (64 segments of
+           512 KiB fragments, one lost each, placement (s + f) mod 8): one holder GPU's partial
+           rebuild from the survivors it holds, the decoder's XOR of 7 received partials, and the
+           full rebuild of the same segments beside them.
+usage: python tools/aux_bench.py [--reps 5] [--only partial]"""
 import argparse
 import json
 import os
@@ -22,6 +26,7 @@ GB = 1e9
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -43,6 +48,8 @@ def main():
             ts.append(time.perf_counter() - t0)
         return float(np.median(ts))
 
+    if args.only == "partial":
+        return partial_row(args, torch, np, cess_amd, dev)
     d = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
     p = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
     cess_amd.fill_synthetic(d, k * F, nseg, 0, 0xCE550002)
@@ -84,6 +91,53 @@ def main():
     print(json.dumps({"row": "f4 fillers", "fillers": nseg, "filler_bytes": F,
                       "generate_and_hash_s": round(t_f, 4),
                       "GBps": round(nseg * F / t_f / GB, 2)}), flush=True)
+    partial_row(args, torch, np, cess_amd, dev)
+
+
+def partial_row(args, torch, np, cess_amd, dev):
+    k, m, F, nseg, G = 32, 32, 512 << 10, 64, 8
+    n = k + m
+    enc = cess_amd.New(k, m)
+    d = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
+    p = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
+    cess_amd.fill_synthetic(d, k * F, nseg, 0, 0xCE550005)
+    enc.EncodeBatch(d, p, nseg, F)
+    present = np.ones((nseg, n), np.uint8)
+    present[np.arange(nseg), np.arange(nseg) % n] = 0
+    # survivors (first k present) held by rank 1 under (s + f) mod G
+    held = np.zeros_like(present)
+    for s in range(nseg):
+        surv = np.flatnonzero(present[s])[:k]
+        held[s, [f for f in surv if (s + f) % G == 1]] = 1
+    nheld = int(held.sum())
+
+    def ev_time(fn, reps):
+        fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps * 1e-3
+
+    reps = max(10, args.reps * 4)
+    t_part = ev_time(lambda: enc.ReconstructPartialBatch(d, p, nseg, F, present, held), reps)
+    t_full = ev_time(lambda: enc.ReconstructBatch(d, p, nseg, F, present), reps)
+    H = G - 1
+    acc = torch.empty((H + 1, nseg, F), dtype=torch.uint8, device=dev)
+    t_xor = ev_time(lambda: cess_amd.xor_batch(acc[0], acc[1], H, nseg * F, nseg * F), reps)
+    part_bytes = (nheld + nseg) * F  # held survivors read, one partial written per segment
+    print(json.dumps({
+        "row": "e partial exchange", "code": "RS(32,32)", "segments": nseg, "fragment_bytes": F,
+        "lost_per_segment": 1, "world_modelled": G,
+        "holder_partial_s": round(t_part, 7), "holder_inputs": nheld,
+        "holder_partial_GBps": round(part_bytes / t_part / GB, 1),
+        "decoder_xor_s": round(t_xor, 7),
+        "decoder_xor_GBps": round((H + 2) * nseg * F / t_xor / GB, 1),
+        "full_rebuild_s": round(t_full, 7),
+        "full_rebuild_GBps": round((k + 1) * nseg * F / t_full / GB, 1),
+        "xgmi_fragments_per_segment": {"survivors": "27-28", "partials": H}}), flush=True)
 
 
 if __name__ == "__main__":
