@@ -313,7 +313,10 @@ def main() -> None:
                     help="hash-queue tick prefetch depth (1 or 2; 0 = library default)")
     ap.add_argument("--rt-mode", type=int, default=0,
                     help="run-time kernel: 0 Horner over input groups, index-mode XORs (k <= 32), "
-                         "1 per-bit masks, 2 Horner with v_mov table reads")
+                         "1 per-bit masks, 2 Horner with v_mov table reads, 3 bit-plane "
+                         "accumulators (<= 4 outputs)")
+    ap.add_argument("--erasures", type=int, default=0,
+                    help="config 6: random erasures per segment (default m)")
     ap.add_argument("--erase", type=int, default=-1,
                     help="config 3: erased fragment index of every segment (-1: seg mod (k+m), "
                          "the BASELINE pattern)")
@@ -358,6 +361,8 @@ def main() -> None:
     torch.cuda.set_device(dev)
 
     k, m, F, nseg_cfg, desc = CONFIGS[args.config]
+    if args.config == 6 and args.erasures:
+        desc = desc.replace("32 random erasures", f"{args.erasures} random erasures")
     if args.segments:
         nseg_cfg = args.segments
         desc = f"{desc} [{args.segments} segments per GPU = {args.segments * k * F / 2**30:g} GiB]"
@@ -388,7 +393,7 @@ def main() -> None:
     elif args.config in (6, 7):
         rng = np.random.default_rng(seg0 + args.config)
         present = np.ones((nseg, k + m), np.uint8)
-        ne = m if args.config == 6 else 1
+        ne = (args.erasures or m) if args.config == 6 else 1
         for s_ in range(nseg):
             present[s_, rng.choice(k + m, size=ne, replace=False)] = 0
     d_hex = None
@@ -530,7 +535,8 @@ def main() -> None:
 
     # algorithmic bytes per segment: read k*F, write m*F (encode) or one erased fragment each
     # (config 7 repairs one fragment: (k+1)*F)
-    per_seg = (k + (1 if args.config == 7 else m)) * F
+    per_seg = (k + (1 if args.config == 7 else
+                    (args.erasures or m) if args.config == 6 else m)) * F
     bytes_step_gpu = nseg * per_seg
     value = world * bytes_step_gpu * args.steps / elapsed / GB
     achieved = bytes_step_gpu / (launch_ms * 1e-3) / GB
@@ -596,7 +602,7 @@ def main() -> None:
     if args.generic:
         kernel_name = "k_rthx" if k <= 32 else "k_rt"
     if args.rt_mode and (args.generic or args.config in (6, 7, 8)):
-        kernel_name = {1: "k_rt", 2: "k_rth"}[args.rt_mode]
+        kernel_name = {1: "k_rt", 2: "k_rth", 3: "k_rtb"}[args.rt_mode]
     traffic = load_traffic(tag, bytes_step_gpu, kernel_name)
     out = {
         "metric": METRIC,

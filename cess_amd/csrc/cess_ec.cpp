@@ -336,6 +336,12 @@ Layout batch_layout(const cec_codec* c, const uint8_t* d_data, const uint8_t* d_
 void launch_chunk(const KernelOpts& o, const Layout& L, const uint32_t* chunk,
                   const uint32_t* const* per_seg, int nin, int nob, const uint32_t* seg_list,
                   uint32_t nseg, hipStream_t st) {
+  // bit-plane accumulators for one or two outputs from a wide input set (RS(32,32) restoral:
+  // 5.92 vs 4.03 TB/s one lost fragment, 4.70 vs 3.75 two; three tie, four lose: 2.08 vs 3.33,
+  // bench.py --config 6 --erasures e, profiles/r02/rtb_sweep.txt)
+  if ((o.rt_mode == 3 || (o.rt_mode == 0 && nob <= 2 && nin >= 4)) &&
+      cec::launch_matvec_rtb(L, chunk, per_seg, nob, seg_list, nseg, st))
+    return;
   if (nin <= cec::kRthMaxIn &&
       cec::launch_matvec_rth(o, L, chunk, per_seg, nin, seg_list, nseg, st))
     return;
@@ -750,7 +756,7 @@ int cec_set_option(cec_codec* c, int option, int value) {
       c->opts.sha_mode = value;
       return CEC_OK;
     case CEC_OPT_RT_MODE:
-      if (value < 0 || value > 2) return set_err(CEC_EINVAL, "rt mode out of range");
+      if (value < 0 || value > 3) return set_err(CEC_EINVAL, "rt mode out of range");
       c->opts.rt_mode = value;
       return CEC_OK;
     case CEC_OPT_DECODE_CACHE:

@@ -46,7 +46,8 @@ struct KernelOpts {
   int ct_variant = -1;  // compile-time kernel variant: -1 = default; others only in tuning
                         // builds (libcessec_tune.so, -DCEC_TUNING)
   int rt_mode = 0;      // run-time kernel: 0 Horner + index-mode XORs (4..32 inputs), 1 per-bit
-                        // masks, 2 Horner + v_mov table reads
+                        // masks, 2 Horner + v_mov table reads, 3 bit-plane accumulators for
+                        // chunks of <= 4 outputs (k_rtb)
   int sha_mode = 0;     // one-shot SHA-256: 0 auto, 1 one wave, 2 two waves per 64 buffers
 };
 // Highest ct_variant this build instantiates (0 in the product library: default only).
@@ -80,6 +81,10 @@ int rt_bucket(int nout);
 // bucket `nob`). Chunks are device memory laid out as described at RtChunk above.
 void launch_matvec_rt(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
                       int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
+// Same product by bit-plane accumulators (k_rtb) for chunks of nob <= 4 outputs; false (nothing
+// launched) for a wider bucket.
+bool launch_matvec_rtb(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
+                       int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
 // Same product from the chunks' Horner sections (every chunk of the launch has nin <= nin_max
 // <= kRthMaxIn). Returns false (nothing launched) if the form is disabled by the variant knob.
 bool launch_matvec_rth(const KernelOpts& o, const Layout& L, const uint32_t* chunk,

@@ -855,6 +855,78 @@ __global__ __launch_bounds__(256) void k_rt(Layout L, const uint32_t* __restrict
     if (o < (int)nout) shard_ptr(L, (int)out_idx[o], seg)[i] = (uint8_t)acc[o][0];
 }
 
+// Bit-plane run-time matvec for few outputs (k_rtb): per output o and coefficient bit b one
+// accumulator t[o][b] = XOR of the inputs whose coefficient in row o has bit b set (one v_bitop3
+// per (input, output, bit) with the chunk's mask from an SGPR), then out_o by Horner over the
+// bits, ((t7 * 2 ^ t6) * 2 ^ ...) ^ t0: 7 xtimes per output where k_rt spends 7 per input. Inputs
+// stream through (the next column's load is issued before the current one is folded in), so the
+// registers are the 8 * NOB accumulators: decode of a few lost fragments of a wide code (the
+// restoral case) and partial rebuilds, where nout << nin.
+template <int NOB, class TV>
+__global__ __launch_bounds__(256) void k_rtb(Layout L, const uint32_t* __restrict__ chunk,
+                                             const uint32_t* const* __restrict__ per_seg,
+                                             const uint32_t* __restrict__ seg_list, uint32_t seg0,
+                                             int vec_ok) {
+  const uint32_t y = seg0 + blockIdx.y;
+  const uint32_t seg = seg_list ? seg_list[y] : y;
+  const cu32* __restrict__ P = as_const(per_seg ? as_const_ptr(per_seg, y) : chunk);
+  const uint32_t nin = P[0], nout = P[1];
+  const cu32* __restrict__ in_idx = P + 4;
+  const cu32* __restrict__ out_idx = P + 4 + 256;
+  const cu32* __restrict__ hbs = P + 4 + 512;
+  const cu32* __restrict__ masks = P + kRtHeaderWords;
+  auto fold = [&]<class T>(T (&t)[NOB][8], auto ld) CEC_AI {
+    T cur = ld(in_idx[0]), nxt = cur;
+    for (uint32_t j = 0; j < nin; ++j) {
+      if (j + 1 < nin) nxt = ld(in_idx[j + 1]);
+      const int hb = (int)hbs[j];
+      const cu32* __restrict__ mk = masks + j * 8 * NOB;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        if (b > hb) break;  // wave-uniform: no higher coefficient bit in this column
+#pragma unroll
+        for (int o = 0; o < NOB; ++o) t[o][b] = bitop3_xand(t[o][b], cur, mk[b * NOB + o]);
+      }
+      cur = nxt;
+    }
+  };
+  auto horner = [&]<class T>(const T (&t)[8]) CEC_AI -> T {
+    T r = t[7];
+#pragma unroll
+    for (int b = 6; b >= 0; --b) r = xt(r) ^ t[b];
+    return r;
+  };
+  constexpr int VB = sizeof(TV);
+  if (vec_ok) {
+    const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v < L.len / VB) {
+      TV t[NOB][8];
+#pragma unroll
+      for (int o = 0; o < NOB; ++o)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) t[o][b] = TV(0);
+      fold(t, [&](uint32_t sh) CEC_AI { return ld16<true, TV>(shard_ptr(L, (int)sh, seg) + v * VB); });
+#pragma unroll
+      for (int o = 0; o < NOB; ++o)
+        if (o < (int)nout) st16<true, TV>(shard_ptr(L, (int)out_idx[o], seg) + v * VB, horner(t[o]));
+    }
+    if (!(L.len % VB) || blockIdx.x != gridDim.x - 1) return;
+  }
+  // byte path: whole shard (vec_ok == 0, grid covers len) or the tail (last block)
+  const uint64_t i = vec_ok ? (L.len - L.len % VB) + threadIdx.x
+                            : (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= L.len) return;
+  uint32_t t[NOB][8];
+#pragma unroll
+  for (int o = 0; o < NOB; ++o)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) t[o][b] = 0;
+  fold(t, [&](uint32_t sh) CEC_AI -> uint32_t { return shard_ptr(L, (int)sh, seg)[i]; });
+#pragma unroll
+  for (int o = 0; o < NOB; ++o)
+    if (o < (int)nout) shard_ptr(L, (int)out_idx[o], seg)[i] = (uint8_t)horner(t[o]);
+}
+
 // Horner over input groups with run-time coefficients (k_rth): the compile-time k_hg scheme
 // with the per-(output, bit, group) combination index read from the chunk's Horner section
 // through the constant address space. Each group's 16 combinations (entry 0 = 0) live in one
@@ -1393,6 +1465,31 @@ void launch_matvec_rt(const Layout& L, const uint32_t* chunk, const uint32_t* co
     case 24: run_rt<24, 1, uint32_t>(L, chunk, per_seg, seg_list, nseg, st); break;
     default: run_rt<32, 1, uint32_t>(L, chunk, per_seg, seg_list, nseg, st); break;
   }
+}
+
+namespace {
+template <int NOB, class TV>
+void run_rtb(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
+             const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  const int vec_ok = layout_vec16_ok(L) ? 1 : 0;
+  uint64_t gx = vec_ok ? (L.len / sizeof(TV) + 255) / 256 : (L.len + 255) / 256;
+  if (gx == 0) gx = 1;
+  for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) {
+    hipLaunchKernelGGL((k_rtb<NOB, TV>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, chunk,
+                       per_seg, seg_list, s0, vec_ok);
+  });
+}
+}  // namespace
+
+bool launch_matvec_rtb(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
+                       int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  switch (nob) {
+    case 1: run_rtb<1, u32x4>(L, chunk, per_seg, seg_list, nseg, st); return true;
+    case 2: run_rtb<2, u32x4>(L, chunk, per_seg, seg_list, nseg, st); return true;
+    case 3: run_rtb<3, u32x2>(L, chunk, per_seg, seg_list, nseg, st); return true;
+    case 4: run_rtb<4, u32x2>(L, chunk, per_seg, seg_list, nseg, st); return true;
+  }
+  return false;
 }
 
 namespace {

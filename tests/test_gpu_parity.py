@@ -522,23 +522,26 @@ def test_c_abi_consumer(tmp_path):
     assert "cabi roundtrip ok" in r.stdout
 
 
-@pytest.mark.parametrize("k,m,ln", [(32, 32, 4096 + 3), (10, 4, 1000), (17, 3, 4099),
-                                    (33, 3, 515), (1, 1, 9), (5, 5, 64)])
-def test_runtime_kernels_agree(torch, cess, corc, k, m, ln):
-    """k_rth (Horner over input groups, run-time indices), k_rt (per-bit masks) and k_rthx
-    (Horner with index-mode XORs) against the C oracle: encode and per-segment random-erasure
-    reconstruct, vector body and byte tail."""
+@pytest.mark.parametrize("k,m,ln,ne", [(32, 32, 4096 + 3, 32), (10, 4, 1000, 4),
+                                       (17, 3, 4099, 3), (33, 3, 515, 3), (1, 1, 9, 1),
+                                       (5, 5, 64, 5), (32, 32, 4096 + 3, 1),
+                                       (32, 32, (1 << 16) + 16, 2), (10, 4, 4099, 1)])
+def test_runtime_kernels_agree(torch, cess, corc, k, m, ln, ne):
+    """k_rth (Horner over input groups, run-time indices), k_rt (per-bit masks), k_rthx
+    (Horner with index-mode XORs) and k_rtb (bit-plane accumulators, chunks of <= 4 outputs)
+    against the C oracle: encode and per-segment reconstruct of `ne` random erasures, vector body
+    and byte tail."""
     nseg = 3
-    rng = np.random.default_rng(k * 1000 + ln)
+    rng = np.random.default_rng(k * 1000 + ln + ne)
     data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
     want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
     present = np.ones((nseg, k + m), np.uint8)
     for s in range(nseg):
-        present[s, rng.choice(k + m, size=m, replace=False)] = 0
+        present[s, rng.choice(k + m, size=ne, replace=False)] = 0
     enc = cess.New(k, m)
     enc.set_option(1, 1)  # run-time coefficients for encode too
     try:
-        for mode in (0, 1, 2):
+        for mode in (0, 1, 2, 3):
             enc.set_option(4, mode)
             d_data = to_dev(torch, data)
             d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")

@@ -66,7 +66,7 @@ def _as_batch(buf, nseg, k, m, ln):
 @pytest.mark.parametrize("k,m,ln,nseg,P", [(2, 1, 4096, 9, 2), (4, 2, 1000, 7, 3),
                                            (10, 4, 4099, 6, 4), (32, 32, 4096, 5, 8),
                                            (32, 32, (1 << 16) + 16, 4, 8), (2, 1, 1, 3, 3)])
-@pytest.mark.parametrize("rt_mode", [0, 1])
+@pytest.mark.parametrize("rt_mode", [0, 1, 3])
 def test_partials_xor_to_codeword(torch, cess, corc, k, m, ln, nseg, P, rt_mode):
     """Fragment f of segment s held by part (s + f) mod P (the multi-GPU placement); XOR of the
     P partials = every lost fragment; data_only rebuilds the lost data fragments only."""
