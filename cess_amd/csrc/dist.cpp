@@ -153,7 +153,7 @@ int make_plan(int k, int m, int world, int exchange, const uint64_t* lost_seg,
 struct cec_dist {
   cec_codec* codec = nullptr;
   int k = 0, m = 0, device = 0, world = 0, rank = 0;
-  int exchange = 0;  // CEC_DIST_OPT_EXCHANGE
+  int exchange = 2;  // CEC_DIST_OPT_EXCHANGE (auto: the cheaper exchange per segment)
   ncclComm_t comm = nullptr;
   uint8_t* stage = nullptr;  // staging batch: data [nseg_d][k][F], then parity [nseg_d][m][F]
   size_t stage_bytes = 0;

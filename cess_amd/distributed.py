@@ -79,7 +79,7 @@ EXCHANGES = ("survivors", "partials", "auto")
 
 
 def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
-                frag_bytes: int, exchange: str = "survivors") -> GatherPlan:
+                frag_bytes: int, exchange: str = "auto") -> GatherPlan:
     """Plan the degraded read of `lost` = {segment: erased fragment indices}.
 
     The decoder of a segment is the home GPU of its first lost fragment (repair restores the
@@ -87,7 +87,7 @@ def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
     codec's survivor choice), so exactly k fragments per segment are read. `exchange`:
     "survivors" moves the survivors the decoder lacks; "partials" moves one partial rebuild per
     lost fragment from every other GPU holding survivors; "auto" takes, per segment, whichever
-    moves fewer bytes (survivors on a tie)."""
+    moves fewer bytes (survivors on a tie; the default: RS(2,1) over >= 3 GPUs always ties)."""
     if exchange not in EXCHANGES:
         raise ValueError(f"exchange must be one of {EXCHANGES}")
     n = k + m
@@ -278,7 +278,7 @@ def degraded_read(plan: GatherPlan, store: FragmentStore, enc, rank: int, group=
 # -- the same exchange through the C ABI (cec_dist_*, for hosts without torch.distributed) -------
 
 def c_plan(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
-           exchange: str = "survivors"):
+           exchange: str = "auto"):
     """cec_dist_plan_ex: (moves [(seg, frag, src, dst, kind)] in issue order, {(seg, frag):
     decoder rank}) of the plan libcessec's degraded read runs for `lost` (host only); kind 0 = a
     survivor fragment, 1 = a partial rebuild of lost fragment `frag`."""
@@ -313,7 +313,7 @@ class RcclGroup:
         check(_lib.load().cec_dist_unique_id(buf), "cec_dist_unique_id")
         return bytes(buf)
 
-    def __init__(self, enc, uid: bytes, world: int, rank: int, exchange: str = "survivors"):
+    def __init__(self, enc, uid: bytes, world: int, rank: int, exchange: str = "auto"):
         from ctypes import byref, c_void_p
         from . import _lib
         from .reedsolomon import check

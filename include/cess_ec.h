@@ -259,10 +259,11 @@ typedef struct cec_dist_move {
   int32_t kind;
 } cec_dist_move;
 /* Exchange of a degraded read (cec_dist_set_option CEC_DIST_OPT_EXCHANGE, cec_dist_plan_ex):
- * 0 = survivors (the k survivors travel to the decoder; default), 1 = partials (every other rank
- * holding survivors sends one partial per lost fragment), 2 = per segment whichever moves fewer
- * fragments, survivors on a tie (a wide code spread over many GPUs with few erasures: RS(32,32)
- * on 8 GPUs, one lost fragment, 7 partials instead of 27-28 survivors). */
+ * 0 = survivors (the k survivors travel to the decoder), 1 = partials (every other rank holding
+ * survivors sends one partial per lost fragment), 2 = per segment whichever moves fewer
+ * fragments, survivors on a tie (the default of a new group; RS(2,1) over >= 3 GPUs always ties;
+ * a wide code spread over many GPUs with few erasures: RS(32,32) on 8 GPUs, one lost fragment,
+ * 7 partials instead of 27-28 survivors). */
 #define CEC_DIST_OPT_EXCHANGE 1
 int cec_dist_set_option(cec_dist* d, int option, int value);
 /* Host only: the plan a degraded read of the lost list runs. The list holds nlost (segment,

@@ -66,7 +66,7 @@ def _worker(rank, world, port, k, m, nseg, F, q):
                             torch.from_numpy(np.stack([full[s][f] for s, f in mine])))
     lost = {s: sorted(rng.choice(n, size=1 + (s % m), replace=False).tolist())
             for s in range(nseg)}
-    plan = D.plan_gather(lost, k, m, world, F)
+    plan = D.plan_gather(lost, k, m, world, F, exchange="survivors")
     sd, sp, present, segs = D.gather_survivors(plan, store, k, m, rank)
     ok = True
     for i, s in enumerate(segs):
@@ -108,8 +108,8 @@ def test_plan_exchange_choice():
     bytes; RS(32,32) on 8 GPUs with one lost fragment: 7 partials instead of 27-28 survivors."""
     k, m, G, F = 32, 32, 8, 512 * 1024
     lost = {s: [s % 64] for s in range(16)}
-    surv = D.plan_gather(lost, k, m, G, F)
-    auto = D.plan_gather(lost, k, m, G, F, exchange="auto")
+    surv = D.plan_gather(lost, k, m, G, F, exchange="survivors")
+    auto = D.plan_gather(lost, k, m, G, F)  # the default
     assert not surv.partial and set(auto.partial) == set(lost) and not auto.moves
     assert all(len(h) == G - 1 for h in auto.partial.values())
     assert auto.bytes_moved == 16 * (G - 1) * F
@@ -231,8 +231,8 @@ def test_c_plan_matches_python_plan(k, m):
         for s in rng.choice(1000, size=40, replace=False).tolist():
             e = rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False).tolist()
             lost[s] = e + e[:1]  # a duplicate entry
-        moves, dec = D.c_plan(lost, k, m, world)
-        plan = D.plan_gather(lost, k, m, world, 1)
+        moves, dec = D.c_plan(lost, k, m, world, "survivors")
+        plan = D.plan_gather(lost, k, m, world, 1, exchange="survivors")
         assert {(s, f): (src, dst) for s, f, src, dst, _ in moves} == plan.moves
         assert [(s, f) for s, f, _, _, _ in moves] == sorted(plan.moves)  # the issue order
         assert all(kind == 0 for *_, kind in moves)
