@@ -862,7 +862,7 @@ __global__ __launch_bounds__(256) void k_rt(Layout L, const uint32_t* __restrict
 // stream through (the next column's load is issued before the current one is folded in), so the
 // registers are the 8 * NOB accumulators: decode of a few lost fragments of a wide code (the
 // restoral case) and partial rebuilds, where nout << nin.
-template <int NOB, class TV>
+template <int NOB, class TV, int PF>
 __global__ __launch_bounds__(256) void k_rtb(Layout L, const uint32_t* __restrict__ chunk,
                                              const uint32_t* const* __restrict__ per_seg,
                                              const uint32_t* __restrict__ seg_list, uint32_t seg0,
@@ -875,19 +875,28 @@ __global__ __launch_bounds__(256) void k_rtb(Layout L, const uint32_t* __restric
   const cu32* __restrict__ out_idx = P + 4 + 256;
   const cu32* __restrict__ hbs = P + 4 + 512;
   const cu32* __restrict__ masks = P + kRtHeaderWords;
+  // inputs stream through a ring of PF columns: column j + PF is loaded while column j folds
   auto fold = [&]<class T>(T (&t)[NOB][8], auto ld) CEC_AI {
-    T cur = ld(in_idx[0]), nxt = cur;
-    for (uint32_t j = 0; j < nin; ++j) {
-      if (j + 1 < nin) nxt = ld(in_idx[j + 1]);
-      const int hb = (int)hbs[j];
-      const cu32* __restrict__ mk = masks + j * 8 * NOB;
+    T ring[PF];
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        if (b > hb) break;  // wave-uniform: no higher coefficient bit in this column
+    for (int q = 0; q < PF; ++q)
+      if (q < (int)nin) ring[q] = ld(in_idx[q]);
+    for (uint32_t j0 = 0; j0 < nin; j0 += PF) {
 #pragma unroll
-        for (int o = 0; o < NOB; ++o) t[o][b] = bitop3_xand(t[o][b], cur, mk[b * NOB + o]);
+      for (int q = 0; q < PF; ++q) {
+        const uint32_t j = j0 + q;
+        if (j >= nin) break;  // wave-uniform
+        const T cur = ring[q];
+        if (j + PF < nin) ring[q] = ld(in_idx[j + PF]);
+        const int hb = (int)hbs[j];
+        const cu32* __restrict__ mk = masks + j * 8 * NOB;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          if (b > hb) break;  // wave-uniform: no higher coefficient bit in this column
+#pragma unroll
+          for (int o = 0; o < NOB; ++o) t[o][b] = bitop3_xand(t[o][b], cur, mk[b * NOB + o]);
+        }
       }
-      cur = nxt;
     }
   };
   auto horner = [&]<class T>(const T (&t)[8]) CEC_AI -> T {
@@ -1468,14 +1477,14 @@ void launch_matvec_rt(const Layout& L, const uint32_t* chunk, const uint32_t* co
 }
 
 namespace {
-template <int NOB, class TV>
+template <int NOB, class TV, int PF>
 void run_rtb(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
              const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
   const int vec_ok = layout_vec16_ok(L) ? 1 : 0;
   uint64_t gx = vec_ok ? (L.len / sizeof(TV) + 255) / 256 : (L.len + 255) / 256;
   if (gx == 0) gx = 1;
   for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) {
-    hipLaunchKernelGGL((k_rtb<NOB, TV>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, chunk,
+    hipLaunchKernelGGL((k_rtb<NOB, TV, PF>), dim3((unsigned)gx, ny), dim3(256), 0, st, L, chunk,
                        per_seg, seg_list, s0, vec_ok);
   });
 }
@@ -1484,10 +1493,10 @@ void run_rtb(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_
 bool launch_matvec_rtb(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
                        int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
   switch (nob) {
-    case 1: run_rtb<1, u32x4>(L, chunk, per_seg, seg_list, nseg, st); return true;
-    case 2: run_rtb<2, u32x4>(L, chunk, per_seg, seg_list, nseg, st); return true;
-    case 3: run_rtb<3, u32x2>(L, chunk, per_seg, seg_list, nseg, st); return true;
-    case 4: run_rtb<4, u32x2>(L, chunk, per_seg, seg_list, nseg, st); return true;
+    case 1: run_rtb<1, u32x4, 1>(L, chunk, per_seg, seg_list, nseg, st); return true;
+    case 2: run_rtb<2, u32x4, 1>(L, chunk, per_seg, seg_list, nseg, st); return true;
+    case 3: run_rtb<3, u32x2, 4>(L, chunk, per_seg, seg_list, nseg, st); return true;
+    case 4: run_rtb<4, u32x2, 4>(L, chunk, per_seg, seg_list, nseg, st); return true;
   }
   return false;
 }
