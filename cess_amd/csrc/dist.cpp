@@ -396,8 +396,10 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
     for (size_t i = r0; i < r1; ++i) {
       const Seg& g = plan[i];
       const bool pm = g.partial && prow.count(g.seg);
+      if (pm)  // every fragment not lost: the rebuild writes the lost ones only
+        for (int f = 0; f < n; ++f)
+          ppres[prow[g.seg] * n + f] = !std::binary_search(g.lost.begin(), g.lost.end(), f);
       for (int f : g.surv) {
-        if (pm) ppres[prow[g.seg] * n + f] = 1;
         if (owner(g.seg, f, world) != rank) continue;
         const uint8_t* p = src_ptr[si++];
         round_src.push_back(p);
@@ -461,9 +463,12 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
     }
     NC_TRY(r.group_end());
     if (!mine.empty()) {
+      // every fragment not lost is flagged present (the codec reads the first k, the gathered
+      // survivors): the rebuild writes only the lost fragments, not the unused survivors
       std::vector<uint8_t> present(mine.size() * n, 0);
       for (size_t i = 0; i < mine.size(); ++i)
-        for (int f : mine[i]->surv) present[i * n + f] = 1;
+        for (int f = 0; f < n; ++f)
+          present[i * n + f] = !std::binary_search(mine[i]->lost.begin(), mine[i]->lost.end(), f);
       rc = cec_reconstruct_batch(d->codec, st_data, st_par, mine.size(), F, present.data(), 1,
                                  0, st);
       if (rc) return rc;

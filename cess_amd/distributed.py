@@ -62,7 +62,9 @@ class GatherPlan:
     segments: Dict[int, List[int]]
     # (segment, survivor fragment) -> (source rank, destination rank)
     moves: Dict[Tuple[int, int], Tuple[int, int]]
-    # segment -> present flags (k+m) as seen by the decoder (survivors used + nothing else)
+    # segment -> present flags (k+m) the decoder passes: every fragment not erased. The codec
+    # reads only the first k of them (`survivors`), so only those are moved; flagging the unused
+    # ones present keeps the rebuild to the lost fragments alone (e outputs, not n - k)
     present: Dict[int, np.ndarray]
     # segment -> erased fragment indices
     lost: Dict[int, List[int]]
@@ -73,6 +75,8 @@ class GatherPlan:
     # segment -> decoding rank
     decoder: Dict[int, int] = field(default_factory=dict)
     world: int = 1
+    # segment -> the survivors the rebuild reads (first k present, index order)
+    survivors: Dict[int, List[int]] = field(default_factory=dict)
 
 
 EXCHANGES = ("survivors", "partials", "auto")
@@ -96,6 +100,7 @@ def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
     present = {}
     partial = {}
     decoder = {}
+    survivors = {}
     moved = 0
     for s in sorted(lost):
         erased = set(lost[s])
@@ -110,8 +115,9 @@ def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
         segs.setdefault(dec, []).append(s)
         decoder[s] = dec
         surv = [f for f in range(n) if f not in erased][:k]
-        flags = np.zeros(n, np.uint8)
-        flags[surv] = 1
+        survivors[s] = surv
+        flags = np.ones(n, np.uint8)
+        flags[sorted(erased)] = 0
         present[s] = flags
         holders = sorted({fragment_owner(s, f, world) for f in surv} - {dec})
         n_surv = sum(fragment_owner(s, f, world) != dec for f in surv)
@@ -126,7 +132,7 @@ def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
             if src != dec:
                 moved += frag_bytes
     return GatherPlan(segs, moves, present, {s: sorted(set(v)) for s, v in lost.items() if v},
-                      moved, partial, decoder, world)
+                      moved, partial, decoder, world, survivors)
 
 
 def _p2p(ops_spec, group, stage: bool):
@@ -161,7 +167,8 @@ def gather_survivors(plan: GatherPlan, store: FragmentStore, k: int, m: int, ran
     """Run the gather for this rank. Returns (staging_data [nseg_d][k][F],
     staging_parity [nseg_d][m][F], present [nseg_d][k+m], segment list) on the decoding rank;
     the staging tensors hold every used survivor at its shard index; the other slots are left
-    uninitialised (the rebuild writes every shard not marked present).
+    uninitialised (the lost ones are written by the rebuild, the unused survivors are flagged
+    present but never read: the codec reads the first k present).
     Non-decoding ranks only send and return None for the staging tensors."""
     import torch
     import torch.distributed as dist
@@ -221,10 +228,10 @@ def partial_exchange(plan: GatherPlan, store: FragmentStore, enc, rank: int, gro
     pres = np.stack([plan.present[s] for s in mine])
     held = np.zeros_like(pres)
     for s in mine:
-        for f in np.flatnonzero(plan.present[s]):
-            if fragment_owner(s, int(f), plan.world) == rank:
+        for f in plan.survivors[s]:
+            if fragment_owner(s, f, plan.world) == rank:
                 held[row[s], f] = 1
-                slot(s, int(f)).copy_(store.data[store.slots[(s, int(f))]])
+                slot(s, f).copy_(store.data[store.slots[(s, f)]])
     enc.ReconstructPartialBatch(sd, sp, len(mine), F, pres, held,
                                 stream=torch.cuda.current_stream(dev) if dev.type == "cuda"
                                 else None)
@@ -266,7 +273,6 @@ def degraded_read(plan: GatherPlan, store: FragmentStore, enc, rank: int, group=
         import torch
         enc.ReconstructBatch(sd, sp, len(segs), sd.shape[2], present,
                              stream=torch.cuda.current_stream(sd.device) if sd.is_cuda else None)
-        # unused survivors are rebuilt too (they are absent from the staging); return the lost
         for i, s in enumerate(segs):
             for f in plan.lost[s]:
                 out[(s, f)] = sd[i, f] if f < k else sp[i, f - k]

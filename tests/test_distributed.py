@@ -73,11 +73,12 @@ def _worker(rank, world, port, k, m, nseg, F, q):
         shards = []
         for f in range(n):
             got = (sd[i, f] if f < k else sp[i, f - k]).numpy()
-            if present[i][f]:
+            if f in plan.survivors[s]:
                 ok &= np.array_equal(got, full[s][f])
                 shards.append(got.copy())
             else:
-                shards.append(None)  # unused slot (uninitialised staging)
+                ok &= bool(present[i][f]) == (f not in lost[s])  # decoder flags: all but lost
+                shards.append(None)  # lost, or an unused survivor (uninitialised staging)
         rec = rs.reconstruct(shards)
         ok &= all(np.array_equal(rec[f], full[s][f]) for f in lost[s])
     q.put((rank, ok, len(segs)))
