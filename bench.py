@@ -265,6 +265,35 @@ def degraded_gather(enc, k: int, m: int, F: int, world: int, rank: int, dev, nse
     return run, verify, plan
 
 
+def cu_split_streams(c: int, dev):
+    """Two HIP streams on disjoint CU sets (hipExtStreamCreateWithCUMask): c CUs for the first,
+    the rest for the second. The c CUs are spread so that each group of 32 consecutive CU indices
+    and each residue class mod 8 gets an equal share (either XCD numbering)."""
+    import ctypes
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    groups = ncu // 32
+    q = c // groups
+    sel = set()
+    for x in range(groups):
+        for r in range(q):
+            sel.add(32 * x + (x + 8 * r + r // 4) % 32)
+    words = (ncu + 31) // 32
+    m1 = (ctypes.c_uint32 * words)()
+    m2 = (ctypes.c_uint32 * words)()
+    for i in range(ncu):
+        (m1 if i in sel else m2)[i // 32] |= 1 << (i % 32)
+    out = []
+    for m in (m1, m2):
+        h = ctypes.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(words), m)
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask: {rc}")
+        out.append(torch.cuda.ExternalStream(h.value, device=dev))
+    return out
+
+
 def load_valu_slots(tag: str):
     """Static VALU issue slots per 64-byte block of the hash-queue tick (profiles/valu_<tag>.json,
     written by tools/sha_slots.py from the built code object), or None."""
@@ -307,6 +336,9 @@ def main() -> None:
                          "per step, 96..192 -> 1.61-1.63)")
     ap.add_argument("--hash-stream", type=int, default=1,
                     help="config 5: 1 = hash queue on a second stream, 0 = after the encode")
+    ap.add_argument("--cu-split", type=int, default=0,
+                    help="config 5: run the encode on a stream masked to this many CUs (a multiple "
+                         "of 8, spread over the XCDs) and the hash ticks on the other CUs")
     ap.add_argument("--prio", type=int, default=0,
                     help="config 5: 1 = encode on a high-priority stream, hashing on a low one")
     ap.add_argument("--tick-pf", type=int, default=0,
@@ -417,7 +449,11 @@ def main() -> None:
         pipe_hex = [d_hex] + [torch.empty_like(d_hex) for _ in range(NB - 1)]
         # --hash-stream 1: hash queue on its own stream (ticks overlap the next encode);
         # 0: one stream, encode then tick (the tick keeps the whole chip)
-        if args.prio:
+        if args.cu_split:
+            # disjoint CU sets: the HBM-bound encode and the VALU-bound ticks side by side
+            torch.cuda.synchronize(dev)
+            stream, sha_stream = cu_split_streams(args.cu_split, dev)
+        elif args.prio:
             # the encode's waves are dispatched ahead of the tick's as CUs free up: the HBM-bound
             # encode and the VALU-bound ticks share the chip instead of taking turns
             torch.cuda.synchronize(dev)  # inputs were produced on the default stream
