@@ -294,3 +294,30 @@ def test_product_kernel_occupancy():
         for n, r in ks.items():
             assert int(r["vgpr_count"]) <= cap, (n, r["vgpr_count"])
             assert int(r["private_segment_fixed_size"]) == 0, n
+
+
+def test_host_code_under_sanitizers(tmp_path):
+    """host ASan + UBSan (GPU sanitizers are unavailable on the pool). libcessec's
+    host-only code (SCALE records, the degraded-read plan of every exchange, the GF(2^8) matrix
+    builder and decode plans for every erasure pattern of small codes) and the CPU codec (scalar,
+    AVX2, GFNI forms) run clean, leak checking on (tests/native/sanitize_host.cpp)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    san = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer",
+           "-O1", "-g"]
+    obj = tmp_path / "oracle.o"
+    subprocess.run(["gcc", "-c", *san, "-pthread", f"{root}/oracle/rs_oracle.c", "-o", str(obj)],
+                   check=True)
+    exe = tmp_path / "sanitize_host"
+    subprocess.run(["g++", "-std=c++20", *san, "-fconstexpr-ops-limit=4000000000",
+                    "-fconstexpr-loop-limit=100000000", "-D__HIP_PLATFORM_AMD__",
+                    "-I/opt/rocm/include", f"{root}/tests/native/sanitize_host.cpp",
+                    f"{root}/cess_amd/csrc/records.cpp", f"{root}/cess_amd/csrc/dist.cpp", str(obj),
+                    "-L/opt/rocm/lib", "-lamdhip64", "-ldl", "-pthread",
+                    "-Wl,-rpath,/opt/rocm/lib", "-o", str(exe)], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "sanitize host ok" in r.stdout
