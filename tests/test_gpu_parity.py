@@ -685,3 +685,49 @@ def test_config1_single_segment_host_api(cess, corc):
     cpu = [shards[0].copy(), shards[1].copy(), np.zeros(F, np.uint8)]
     corc.orc_segment_ops(k, m, ptrs(cpu), F, 4, 1)
     assert all(np.array_equal(a, b) for a, b in zip(cpu, shards))
+
+
+def test_codecs_on_threads_are_independent(torch, cess, corc):
+    """include/cess_ec.h: distinct codecs are independent. Four host threads (ctypes drops the
+    GIL inside the C calls), each with its own codec, code, kernel options, decode-cache capacity
+    and HIP stream, run encode + per-segment reconstruct loops at the same time; every result is
+    bit-exact against the C oracle."""
+    import concurrent.futures as cf
+    cases = [(2, 1, 4096 + 16, 0, 4096), (10, 4, 4099, 1, 2), (32, 32, 8192, 0, 3),
+             (4, 2, 1000, 2, 1)]
+
+    def work(case):
+        k, m, ln, rt_mode, cap = case
+        n = k + m
+        rng = np.random.default_rng(k * 31 + m)
+        nseg = 6
+        data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+        want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+        enc = cess.New(k, m)
+        enc.set_option(4, rt_mode)
+        enc.set_option(6, cap)
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            d_data = torch.from_numpy(data).cuda()
+            d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
+        for it in range(12):
+            enc.EncodeBatch(d_data, d_par, nseg, ln, stream=st)
+            st.synchronize()
+            if not np.array_equal(d_par.cpu().numpy(), want):
+                return (case, it, "encode")
+            present = np.ones((nseg, n), np.uint8)
+            for s in range(nseg):
+                present[s, rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False)] = 0
+            with torch.cuda.stream(st):
+                d_data.mul_(torch.from_numpy(present[:, :k, None]).cuda())
+                d_par.mul_(torch.from_numpy(present[:, k:, None]).cuda())
+            enc.ReconstructBatch(d_data, d_par, nseg, ln, present, stream=st)
+            st.synchronize()
+            if not (np.array_equal(d_data.cpu().numpy(), data)
+                    and np.array_equal(d_par.cpu().numpy(), want)):
+                return (case, it, "reconstruct")
+        return None
+
+    with cf.ThreadPoolExecutor(len(cases)) as ex:
+        bad = [r for r in ex.map(work, cases) if r is not None]
+    assert not bad, bad
