@@ -336,10 +336,10 @@ Layout batch_layout(const cec_codec* c, const uint8_t* d_data, const uint8_t* d_
 void launch_chunk(const KernelOpts& o, const Layout& L, const uint32_t* chunk,
                   const uint32_t* const* per_seg, int nin, int nob, const uint32_t* seg_list,
                   uint32_t nseg, hipStream_t st) {
-  // bit-plane accumulators for one or two outputs from a wide input set (RS(32,32) restoral:
-  // 5.92 vs 4.03 TB/s one lost fragment, 4.70 vs 3.75 two; three tie, four lose: 2.08 vs 3.33,
-  // bench.py --config 6 --erasures e, profiles/r02/rtb_sweep.txt)
-  if ((o.rt_mode == 3 || (o.rt_mode == 0 && nob <= 2 && nin >= 4)) &&
+  // bit-plane accumulators for one to three outputs from a wide input set (RS(32,32) rebuilds
+  // vs k_rthx: one lost fragment 5.84 vs 4.03 TB/s, two 4.89 vs 3.75, three 3.89 vs 3.55; four
+  // tie, 3.36 vs 3.33; bench.py --config 6 --erasures e, profiles/r02/rtb_sweep.txt)
+  if ((o.rt_mode == 3 || (o.rt_mode == 0 && nob <= 3 && nin >= 4)) &&
       cec::launch_matvec_rtb(L, chunk, per_seg, nob, seg_list, nseg, st))
     return;
   if (nin <= cec::kRthMaxIn &&

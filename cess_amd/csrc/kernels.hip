@@ -873,7 +873,6 @@ __global__ __launch_bounds__(256) void k_rtb(Layout L, const uint32_t* __restric
   const uint32_t nin = P[0], nout = P[1];
   const cu32* __restrict__ in_idx = P + 4;
   const cu32* __restrict__ out_idx = P + 4 + 256;
-  const cu32* __restrict__ hbs = P + 4 + 512;
   const cu32* __restrict__ masks = P + kRtHeaderWords;
   // inputs stream through a ring of PF columns: column j + PF is loaded while column j folds
   auto fold = [&]<class T>(T (&t)[NOB][8], auto ld) CEC_AI {
@@ -888,14 +887,13 @@ __global__ __launch_bounds__(256) void k_rtb(Layout L, const uint32_t* __restric
         if (j >= nin) break;  // wave-uniform
         const T cur = ring[q];
         if (j + PF < nin) ring[q] = ld(in_idx[j + PF]);
-        const int hb = (int)hbs[j];
+        // all 8 bits, no branch on the column's top bit: the 8 * NOB masks of a column then
+        // come in as one wide scalar load
         const cu32* __restrict__ mk = masks + j * 8 * NOB;
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          if (b > hb) break;  // wave-uniform: no higher coefficient bit in this column
+        for (int b = 0; b < 8; ++b)
 #pragma unroll
           for (int o = 0; o < NOB; ++o) t[o][b] = bitop3_xand(t[o][b], cur, mk[b * NOB + o]);
-        }
       }
     }
   };
