@@ -634,8 +634,8 @@ def main() -> None:
     tag = f"c{args.config}"
     kernel_name = {2: "k_ct<EncCT<2, 1>>", 3: "k_ct_dec1_mixed21 (Dec1CT<2, 1, e> / EncCT<2, 1> per segment)",
                    4: "k_ct<EncCT<2, 1>>", 5: "k_fft3232<true, true>",
-                   6: "k_rthx<8>" if (args.erasures or m) > 2 else "k_rtb",
-                   7: "k_rtb<1>", 8: "k_rthx<3>"}[args.config]
+                   6: "k_rthx<8>" if (args.erasures or m) > 4 else "k_rtb",
+                   7: "k_rtb<1>", 8: "k_rtb<4>"}[args.config]
     if args.generic:
         kernel_name = "k_rthx" if k <= 32 else "k_rt"
     if args.rt_mode and (args.generic or args.config in (6, 7, 8)):

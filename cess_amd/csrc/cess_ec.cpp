@@ -336,10 +336,11 @@ Layout batch_layout(const cec_codec* c, const uint8_t* d_data, const uint8_t* d_
 void launch_chunk(const KernelOpts& o, const Layout& L, const uint32_t* chunk,
                   const uint32_t* const* per_seg, int nin, int nob, const uint32_t* seg_list,
                   uint32_t nseg, hipStream_t st) {
-  // bit-plane accumulators for one to three outputs from a wide input set (RS(32,32) rebuilds
-  // vs k_rthx: one lost fragment 5.84 vs 4.03 TB/s, two 4.89 vs 3.75, three 3.89 vs 3.55; four
-  // tie, 3.36 vs 3.33; bench.py --config 6 --erasures e, profiles/r02/rtb_sweep.txt)
-  if ((o.rt_mode == 3 || (o.rt_mode == 0 && nob <= 3 && nin >= 4)) &&
+  // bit-plane accumulators for one to four outputs from a wide input set (RS(32,32) rebuilds
+  // vs k_rthx: one lost fragment 5.84 vs 4.03 TB/s, two 4.89 vs 3.75, three 3.89 vs 3.55, four
+  // 3.36 vs 3.33; RS(10,4) encode 3.54 vs 3.41; bench.py --config 6 --erasures e / --config 8,
+  // profiles/r02/rtb_sweep.txt)
+  if ((o.rt_mode == 3 || (o.rt_mode == 0 && nob <= 4 && nin >= 4)) &&
       cec::launch_matvec_rtb(L, chunk, per_seg, nob, seg_list, nseg, st))
     return;
   if (nin <= cec::kRthMaxIn &&
