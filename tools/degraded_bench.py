@@ -5,9 +5,11 @@ Fragment f of segment s lives on GPU (s + f) mod G (the miner spread of
 c-pallets/file-bank/src/functions.rs:187-283). Every segment loses fragment (s mod n); the k
 survivors are gathered on the lost fragment's home GPU with grouped point-to-point send/recv
 (RCCL over xGMI; RCCL has no XOR reduction) and the fragment is rebuilt there by libcessec.
-Reports gather bytes / time, decode time, and checks every rebuilt fragment.
+With --exchange partials (or auto) the GPUs holding survivors send partial rebuilds instead
+(SURVEY.md §8e). Reports exchanged bytes / time, decode time, and checks every rebuilt fragment.
 
     torchrun --nproc-per-node G tools/degraded_bench.py [--nseg 64] [--frag-mib 8]
+        [--data-shards 32 --parity-shards 32 --frag-kib 512] [--exchange survivors|partials|auto]
 """
 import argparse
 import json
@@ -25,6 +27,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nseg", type=int, default=64)
     ap.add_argument("--frag-mib", type=int, default=8)
+    ap.add_argument("--frag-kib", type=int, default=0, help="fragment size in KiB (overrides MiB)")
+    ap.add_argument("--exchange", choices=["survivors", "partials", "auto"], default="auto")
     ap.add_argument("--data-shards", type=int, default=2)
     ap.add_argument("--parity-shards", type=int, default=1)
     ap.add_argument("--reps", type=int, default=5)
@@ -45,7 +49,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    k, m, F, nseg = args.data_shards, args.parity_shards, args.frag_mib << 20, args.nseg
+    k, m, nseg = args.data_shards, args.parity_shards, args.nseg
+    F = args.frag_kib << 10 if args.frag_kib else args.frag_mib << 20
     n = k + m
     enc = cess_amd.New(k, m, device=local)
     # every rank regenerates the codewords deterministically and keeps the fragments it owns
@@ -62,7 +67,7 @@ def main():
                 store.data[store.slots[(s, f)]].copy_(seg_d[0, f] if f < k else seg_p[0, f - k])
     torch.cuda.synchronize()
     lost = {s: [s % n] for s in range(nseg)}
-    plan = D.plan_gather(lost, k, m, world, F)
+    plan = D.plan_gather(lost, k, m, world, F, exchange=args.exchange)
     times = []
     for _ in range(args.reps + 1):
         if world > 1:
@@ -97,6 +102,7 @@ def main():
     if rank == 0:
         print(json.dumps({"degraded_read": True, "gpus": world, "segments": nseg, "k": k, "m": m,
                           "fragment_bytes": F, "rebuilt": rebuilt, "bit_exact": ok,
+                          "exchange": args.exchange, "partial_segments": len(plan.partial),
                           "gather_bytes": plan.bytes_moved, "seconds": round(t, 5),
                           "gather_plus_decode_GBps": round(plan.bytes_moved / t / 1e9, 2)
                           if plan.bytes_moved else None,
