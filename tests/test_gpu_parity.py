@@ -525,7 +525,9 @@ def test_c_abi_consumer(tmp_path):
 @pytest.mark.parametrize("k,m,ln,ne", [(32, 32, 4096 + 3, 32), (10, 4, 1000, 4),
                                        (17, 3, 4099, 3), (33, 3, 515, 3), (1, 1, 9, 1),
                                        (5, 5, 64, 5), (32, 32, 4096 + 3, 1),
-                                       (32, 32, (1 << 16) + 16, 2), (10, 4, 4099, 1)])
+                                       (32, 32, (1 << 16) + 16, 2), (10, 4, 4099, 1),
+                                       (32, 32, 4096 + 3, 6), (32, 32, (1 << 16) + 16, 8),
+                                       (20, 10, 999, 5)])
 def test_runtime_kernels_agree(torch, cess, corc, k, m, ln, ne):
     """k_rth (Horner over input groups, run-time indices), k_rt (per-bit masks), k_rthx
     (Horner with index-mode XORs) and k_rtb (bit-plane accumulators, chunks of <= 4 outputs)
