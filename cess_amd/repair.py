@@ -54,13 +54,27 @@ def repair_fragment(enc: Encoder, survivors: Dict[int, np.ndarray], index: int,
     return out
 
 
+# Fragments to check at once from which the GPU's hash beats the host's: one SHA-256 chain per
+# fragment runs ~35 MB/s on a GPU lane (1.8 us per 64-byte block), so the GPU's time is flat up to
+# thousands of fragments (64 rebuilt 8 MiB fragments: 0.233 s), while the host's grows with the
+# count (8 threads: 0.140 s for the same 64, ~2.2 ms per fragment; the f2 row of
+# profiles/r02/aux_bench.jsonl, tools/aux_bench.py).
+AUTO_GPU_CHECK_FRAGMENTS = 128
+
+
 def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, present,
-                 expected: Optional[Sequence[Dict[int, bytes]]] = None, stream=None):
+                 expected: Optional[Sequence[Dict[int, bytes]]] = None, stream=None,
+                 hash_on: str = "auto", hash_threads: int = 16):
     """Rebuild every missing fragment of an HBM-resident batch in place (one launch for all
     erasure patterns) and, with `expected` ([{fragment index: recorded hash}] per segment),
-    return per-segment booleans: rebuilt fragments hash to the recorded values (all of them
-    hashed in one GPU launch, one chain per fragment, where they were rebuilt)."""
+    return per-segment booleans: rebuilt fragments hash to the recorded values. hash_on "gpu":
+    all of them hashed in one GPU launch, one chain per fragment, where they were rebuilt;
+    "host": copied out once and hashed by `hash_threads` host threads (OpenSSL via hashlib);
+    "auto": the host below AUTO_GPU_CHECK_FRAGMENTS fragments (a chain is serial, so a few
+    chains run faster on host cores), the GPU from there."""
     import torch
+    if hash_on not in ("gpu", "host", "auto"):
+        raise ValueError("hash_on must be 'gpu', 'host' or 'auto'")
     enc.ReconstructBatch(d_data, d_parity, nseg, shard_len, present, stream=stream)
     if expected is None:
         return None
@@ -70,8 +84,18 @@ def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, pres
         stream.synchronize()
     k = enc.DataShards
     which = [(s, i, bytes(h)) for s in range(nseg) for i, h in expected[s].items()]
-    ptrs = [(d_data[s, i] if i < k else d_parity[s, i - k]).data_ptr() for s, i, _ in which]
-    got = sha256_hex_device(ptrs, shard_len) if ptrs else []
+    frags = [d_data[s, i] if i < k else d_parity[s, i - k] for s, i, _ in which]
+    if hash_on == "auto":
+        hash_on = "gpu" if len(which) >= AUTO_GPU_CHECK_FRAGMENTS else "host"
+    if not which:
+        got = []
+    elif hash_on == "gpu":
+        got = sha256_hex_device([t.data_ptr() for t in frags], shard_len)
+    else:
+        import concurrent.futures as cf
+        host = torch.stack(frags).cpu().numpy()
+        with cf.ThreadPoolExecutor(max(1, hash_threads)) as ex:  # hashlib drops the GIL
+            got = list(ex.map(lambda a: hashlib.sha256(a).hexdigest().encode(), host))
     ok = [True] * nseg
     for (s, _, h), g in zip(which, got):
         ok[s] &= g == h

@@ -488,13 +488,17 @@ def test_repair_batch_wide(torch, cess, corc, orc):
     dd = to_dev(torch, data * present[:, :k, None])
     dp = to_dev(torch, par * present[:, k:, None])
     enc = cess.New(k, m)
-    ok = repair_batch(enc, dd, dp, nseg, F, present, expected)
-    assert ok == [True] * nseg
     # a recorded hash that the rebuilt fragment does not match flags that segment only
     wrong = [dict(e) for e in expected]
     i0 = next(iter(wrong[2]))
     wrong[2][i0] = b"0" * 64
-    assert repair_batch(enc, dd, dp, nseg, F, present, wrong) == [True, True, False, True, True]
+    for hash_on in ("gpu", "host", "auto"):  # the check on the GPU or on host cores
+        ok = repair_batch(enc, dd, dp, nseg, F, present, expected, hash_on=hash_on)
+        assert ok == [True] * nseg, hash_on
+        assert repair_batch(enc, dd, dp, nseg, F, present, wrong, hash_on=hash_on) == \
+            [True, True, False, True, True], hash_on
+    with pytest.raises(ValueError):
+        repair_batch(enc, dd, dp, nseg, F, present, expected, hash_on="tpu")
 
 
 def test_generate_fillers(torch, orc):
