@@ -349,6 +349,9 @@ def main() -> None:
                          "accumulators (<= 4 outputs)")
     ap.add_argument("--erasures", type=int, default=0,
                     help="config 6: random erasures per segment (default m)")
+    ap.add_argument("--lose-parity", action="store_true",
+                    help="config 6: every segment loses exactly its m parity shards (the rebuild "
+                         "is the encode)")
     ap.add_argument("--erase", type=int, default=-1,
                     help="config 3: erased fragment index of every segment (-1: seg mod (k+m), "
                          "the BASELINE pattern)")
@@ -427,7 +430,10 @@ def main() -> None:
         present = np.ones((nseg, k + m), np.uint8)
         ne = (args.erasures or m) if args.config == 6 else 1
         for s_ in range(nseg):
-            present[s_, rng.choice(k + m, size=ne, replace=False)] = 0
+            if args.lose_parity and args.config == 6:
+                present[s_, k:] = 0
+            else:
+                present[s_, rng.choice(k + m, size=ne, replace=False)] = 0
     d_hex = None
     gather = None
     if args.config == 4:

@@ -163,6 +163,7 @@ struct Program {
   std::vector<RtChunk> chunks;
   int nout = 0;     // total outputs
   int single = -1;  // the one missing shard when exactly one output (compile-time decode)
+  bool partial = false;  // rows restricted to held survivors (cec_reconstruct_partial_batch)
   uint8_t in_idx[cec::kMaxShards] = {};   // survivors read (host copy)
   uint8_t out_idx[cec::kMaxShards] = {};  // shards written (host copy)
 };
@@ -183,6 +184,7 @@ int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int 
   });
   prog->nout = nout;
   prog->single = nout == 1 && !partial ? out_idx[0] : -1;
+  prog->partial = partial;
   std::memcpy(prog->in_idx, in_idx, nin);
   std::memcpy(prog->out_idx, out_idx, nout);
   std::vector<std::vector<uint32_t>> hosts;
@@ -476,9 +478,23 @@ void evict_decode(cec_codec* c) {
   }
 }
 
+// "Every data shard present, every parity shard lost" is the encode itself: the compile-time
+// encode kernels (RS(32,32): the additive FFT, 5.8 TB/s) rebuild it, not a run-time program of m
+// outputs (k_rthx, ~2.7 TB/s at 32).
+bool is_reencode(const cec_codec* c, const Program& p) {
+  if (p.partial || p.nout != c->m) return false;
+  for (int o = 0; o < p.nout; ++o)
+    if (p.out_idx[o] != c->k + o) return false;
+  for (int j = 0; j < c->k; ++j)
+    if (p.in_idx[j] != j) return false;
+  return true;
+}
+
 int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* seg_list,
               uint32_t nseg, hipStream_t st) {
   if (p.nout == 0 || nseg == 0 || L.len == 0) return CEC_OK;
+  if (!c->force_generic && p.single < 0 && is_reencode(c, p))
+    return do_encode(c, L, seg_list, nseg, st);
   if (c->force_generic || p.single < 0 ||
       !cec::launch_decode_ct(c->opts, c->k, c->m, p.single, L, seg_list, nseg, st))
     run_program(c->opts, p, L, seg_list, nseg, st);
@@ -534,7 +550,7 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
     groups[it->second].second.push_back((uint32_t)s);
   }
   bool all_ct = !c->force_generic;
-  std::vector<std::pair<ProgPtr, const std::vector<uint32_t>*>> progs;
+  std::vector<std::pair<ProgPtr, const std::vector<uint32_t>*>> progs, reencode;
   for (auto& g : groups) {
     ProgPtr p;
     const uint8_t* flags = reinterpret_cast<const uint8_t*>(g.first.data());
@@ -544,12 +560,23 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
     plan->keys.push_back(partial ? partial_key(flags, flags + n, n, data_only)
                                  : pattern_key(flags, n, data_only));
     if (!p->nout) continue;
-    progs.push_back({p, &g.second});
     plan->progs.push_back(p);
+    if (!c->force_generic && p->single < 0 && is_reencode(c, *p)) {
+      reencode.push_back({p, &g.second});  // the encode kernels, whatever the other groups take
+      continue;
+    }
+    progs.push_back({p, &g.second});
     if (p->single < 0 || !cec::has_decode_ct(c->k, c->m, p->single)) all_ct = false;
   }
   std::vector<uint32_t> hl;
   std::vector<const uint32_t*> hp;
+  for (auto& pr : reencode) {
+    plan->ct.push_back({pr.first, {hl.size(), pr.second->size()}});
+    hl.insert(hl.end(), pr.second->begin(), pr.second->end());
+  }
+  // the run-time launches index the segment list and the chunk-pointer array with one offset:
+  // keep them aligned past the re-encode lists
+  hp.resize(hl.size(), nullptr);
   if (all_ct) {
     std::vector<uint32_t> tagged;
     for (auto& pr : progs) {

@@ -737,3 +737,36 @@ def test_codecs_on_threads_are_independent(torch, cess, corc):
     with cf.ThreadPoolExecutor(len(cases)) as ex:
         bad = [r for r in ex.map(work, cases) if r is not None]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("k,m,ln", [(32, 32, 4096), (32, 32, 4096 + 3), (10, 4, 2048), (4, 2, 999)])
+def test_all_parity_lost_is_reencoded(torch, cess, corc, k, m, ln):
+    """The pattern 'every data shard present, every parity shard lost' runs the encode kernels
+    (RS(32,32): the FFT) instead of a run-time decode program: one pattern for the batch, and
+    mixed into a per-segment batch beside other patterns; bit-exact vs the C oracle, data
+    untouched."""
+    nseg = 6
+    rng = np.random.default_rng(k + ln)
+    n = k + m
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    par = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    enc = cess.New(k, m)
+    allpar = np.array([1] * k + [0] * m, np.uint8)
+    d_data = to_dev(torch, data)
+    d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
+    enc.ReconstructBatch(d_data, d_par, nseg, ln, allpar)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_par.cpu().numpy(), par)
+    assert np.array_equal(d_data.cpu().numpy(), data)
+    present = np.ones((nseg, n), np.uint8)
+    for s in range(nseg):
+        if s % 2:
+            present[s, k:] = 0
+        else:
+            present[s, rng.choice(n, size=m, replace=False)] = 0
+    d_data = to_dev(torch, data * present[:, :k, None])
+    d_par = to_dev(torch, par * present[:, k:, None])
+    enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_data.cpu().numpy(), data)
+    assert np.array_equal(d_par.cpu().numpy(), par)
