@@ -718,11 +718,12 @@ def main() -> None:
         out.setdefault("extra", {})["degraded_gather"] = gather_leg(
             degraded_gather(enc, k, m, F, world, rank, dev, 64))
         # the wide code's single-fragment degraded read, both exchanges: RS(32,32)
-        # with 16 MiB segments (F = 512 KiB), 8 fragments per GPU at world 8
+        # with 16 MiB segments (F = 512 KiB), 8 fragments per GPU at world 8; 32 segments per GPU
+        # keep the survivor leg's grouped point-to-point batch under ~900 transfers per rank
         wk, wm, wF = CONFIGS[5][:3]
         wenc = cess_amd.New(wk, wm, device=local)
         out["extra"]["wide_degraded_gather"] = {
-            ex: gather_leg(degraded_gather(wenc, wk, wm, wF, world, rank, dev, 64, ex),
+            ex: gather_leg(degraded_gather(wenc, wk, wm, wF, world, rank, dev, 32, ex),
                            code=(wk, wF))
             for ex in ("survivors", "partials")}
         wenc.close()
