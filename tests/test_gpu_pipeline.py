@@ -107,3 +107,23 @@ def test_cli_encode_streams_fragments_and_scale(tmp_path, orc):
                         "--segment-size", "16384"], capture_output=True, text=True, timeout=300,
                        cwd=ROOT)
     assert r.returncode == 2 and "SegmentCount" in r.stdout
+
+
+def test_pipelines_on_threads(orc):
+    """The north_star's per-GPU sharding from one host: independent codecs each driving their own
+    C pipeline (pinned ring, three streams, GPU hash queue) on their own host thread at the same
+    time, here two per GPU; every SegmentList equals the oracle's."""
+    import concurrent.futures as cf
+    from cess_amd.pipeline import encode_file_records
+    jobs = [(4 * MiB + 3, MiB, 2, 1, 11), (3 * MiB + 100, MiB, 2, 1, 12),
+            (2 * MiB, MiB // 2, 4, 2, 13), (MiB + 1, 10 * 4096, 10, 4, 14)]
+
+    def run(job):
+        size, seg, k, m, seed = job
+        blob = np.random.default_rng(seed).integers(0, 256, size, dtype=np.uint8).tobytes()
+        rec, _ = encode_file_records(blob, k, m, seg, batch_segments=2, window=2)
+        return [(s.hash, s.fragment_list) for s in rec.segments] == orc.segment_list(blob, k, m,
+                                                                                    seg)
+
+    with cf.ThreadPoolExecutor(len(jobs)) as ex:
+        assert all(ex.map(run, jobs))
