@@ -174,9 +174,12 @@ using ProgPtr = std::shared_ptr<const Program>;
 // run on `upload` and are complete when this returns.
 // `partial`: the rows do not rebuild a shard by themselves (cec_reconstruct_partial_batch), so
 // the compile-time single-erasure kernels never stand in for the program.
+// With `keep`, the host images move there and the uploads are left in flight: the caller
+// synchronises `upload` once for a whole plan before launching or dropping `keep`.
+using HostImages = std::vector<std::vector<uint32_t>>;
 int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int nin,
                   const uint8_t* out_idx, int nout, const BigMat& coef, ProgPtr* out,
-                  bool partial = false) {
+                  bool partial = false, HostImages* keep = nullptr) {
   DevPool* pp = &pool;
   std::shared_ptr<Program> prog(new Program, [pp](Program* p) {
     for (auto& c : p->chunks) pp->retire(c.dev, c.bytes);
@@ -241,8 +244,12 @@ int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int 
     HIP_TRY(hipMemcpyAsync(c.dev, h.data(), c.bytes, hipMemcpyHostToDevice, upload));
   }
   // the block may be a reused one whose readers have completed; the upload must land before
-  // any caller-stream launch that reads it, and the host vectors die here
-  HIP_TRY(hipStreamSynchronize(upload));
+  // any caller-stream launch that reads it, and the host vectors die here (or with `keep`)
+  if (keep) {
+    for (auto& h : hosts) keep->push_back(std::move(h));
+  } else {
+    HIP_TRY(hipStreamSynchronize(upload));
+  }
   *out = std::move(prog);
   return CEC_OK;
 }
@@ -388,7 +395,8 @@ std::string partial_key(const uint8_t* present, const uint8_t* held, int n, bool
 // Decode program for one erasure pattern (LRU-cached). Nothing is evicted here: the caller
 // evicts after its launches are enqueued and marked (evict_decode), so a program resolved
 // earlier in the same call is never dropped under it.
-int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* out) {
+int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* out,
+               HostImages* keep = nullptr) {
   const int n = c->k + c->m;
   std::string key = pattern_key(present, n, data_only);
   auto it = c->decode_cache.find(key);
@@ -403,12 +411,12 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* ou
   auto work = std::make_unique<WorkMat>();
   uint8_t flags[cec::kMaxShards];
   for (int i = 0; i < n; ++i) flags[i] = key[i];
-  if (cec::gf_decode_plan(c->k, c->m, flags, data_only, *c->E, *plan, *sub, *inv, *work) != 0)
+  if (cec::gf_decode_plan_sys(c->k, c->m, flags, data_only, *c->E, *plan, *sub, *inv, *work) != 0)
     return set_err(CEC_ETOOFEW, "fewer than k shards present");
   ProgPtr prog;
   if (plan->nout > 0) {
     int rc = build_program(c->pool, c->stream, plan->in_idx, c->k, plan->out_idx, plan->nout,
-                           plan->coef, &prog);
+                           plan->coef, &prog, false, keep);
     if (rc) return rc;
   } else {
     prog = std::make_shared<const Program>();
@@ -426,7 +434,7 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* ou
 // column with zero coefficients), so the outputs are still written (as zeros). Cached in the
 // decode LRU under its own key.
 int get_partial(cec_codec* c, const uint8_t* present, const uint8_t* held, bool data_only,
-                ProgPtr* out) {
+                ProgPtr* out, HostImages* keep = nullptr) {
   const int n = c->k + c->m;
   std::string key = partial_key(present, held, n, data_only);
   auto it = c->decode_cache.find(key);
@@ -441,7 +449,7 @@ int get_partial(cec_codec* c, const uint8_t* present, const uint8_t* held, bool 
   auto work = std::make_unique<WorkMat>();
   uint8_t flags[cec::kMaxShards];
   for (int i = 0; i < n; ++i) flags[i] = present[i] ? 1 : 0;
-  if (cec::gf_decode_plan(c->k, c->m, flags, data_only, *c->E, *plan, *sub, *inv, *work) != 0)
+  if (cec::gf_decode_plan_sys(c->k, c->m, flags, data_only, *c->E, *plan, *sub, *inv, *work) != 0)
     return set_err(CEC_ETOOFEW, "fewer than k shards present");
   ProgPtr prog;
   if (plan->nout > 0) {
@@ -458,7 +466,7 @@ int get_partial(cec_codec* c, const uint8_t* present, const uint8_t* held, bool 
       nsub = 1;
     }
     int rc = build_program(c->pool, c->stream, in_sub, nsub, plan->out_idx, plan->nout, *coef,
-                           &prog, true);
+                           &prog, true, keep);
     if (rc) return rc;
   } else {
     prog = std::make_shared<const Program>();
@@ -551,11 +559,21 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
   }
   bool all_ct = !c->force_generic;
   std::vector<std::pair<ProgPtr, const std::vector<uint32_t>*>> progs, reencode;
+  // new patterns' program uploads stay in flight until the one synchronisation below (one per
+  // plan, not per pattern: 64 new RS(32,32) patterns cost ~1 ms of waits otherwise); every return
+  // path waits for them before their host images go
+  struct Uploads {
+    hipStream_t st;
+    HostImages images;
+    ~Uploads() {
+      if (!images.empty()) (void)hipStreamSynchronize(st);
+    }
+  } up{c->stream, {}};
   for (auto& g : groups) {
     ProgPtr p;
     const uint8_t* flags = reinterpret_cast<const uint8_t*>(g.first.data());
-    int rc = partial ? get_partial(c, flags, flags + n, data_only, &p)
-                     : get_decode(c, flags, data_only, &p);
+    int rc = partial ? get_partial(c, flags, flags + n, data_only, &p, &up.images)
+                     : get_decode(c, flags, data_only, &p, &up.images);
     if (rc) return rc;
     plan->keys.push_back(partial ? partial_key(flags, flags + n, n, data_only)
                                  : pattern_key(flags, n, data_only));
@@ -639,12 +657,13 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
   if (e == hipSuccess && !hp.empty())
     e = hipMemcpyAsync(plan->ptrs, hp.data(), hp.size() * sizeof(void*), hipMemcpyHostToDevice,
                        c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the programs' uploads too
   if (e != hipSuccess) {
     c->pool.retire(plan->list, plan->list_bytes);
     c->pool.retire(plan->ptrs, plan->ptrs_bytes);
     return set_err(CEC_EHIP, std::string("plan upload: ") + hipGetErrorString(e));
   }
+  up.images.clear();
   *out = std::move(plan);
   return CEC_OK;
 }

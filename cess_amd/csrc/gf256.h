@@ -172,6 +172,63 @@ constexpr int gf_decode_plan(int k, int m, const uint8_t* present, bool data_onl
   return 0;
 }
 
+// The same plan by the code's systematic structure (run time): the first k present shards are
+// the k - d present data shards and the first d present parity shards Ps, so only the d x d block
+// A = E[Ps][D] over the missing data D is inverted: x_D = inv(A) (y_Ps ^ E[Ps][C] x_C). d^3 + d^2 k
+// products instead of the k x 2k Gauss-Jordan; the decode map is unique, so the coefficients are
+// those of gf_decode_plan (checked on every pattern of small codes, tests/native/sanitize_host.cpp).
+// `a`, `ainv`, `work` are scratch (d <= m). Returns 0, or -1 if fewer than k shards survive.
+template <int R, int C, int R2, int C2>
+int gf_decode_plan_sys(int k, int m, const uint8_t* present, bool data_only, const Mat<R, C>& e,
+                       Plan<R, C>& plan, Mat<R, C>& a, Mat<R, C>& ainv, Mat<R2, C2>& work) {
+  const int n = k + m;
+  plan.k = k;
+  int got = 0;
+  for (int i = 0; i < n && got < k; ++i)
+    if (present[i]) plan.in_idx[got++] = (uint8_t)i;
+  if (got < k) return -1;
+  int miss[kMaxShards], d = 0;  // missing data shards
+  for (int i = 0; i < k; ++i)
+    if (!present[i]) miss[d++] = i;
+  const int nc = k - d;  // survivor positions [0, nc) are data, [nc, k) parity
+  a.rows = a.cols = d;
+  for (int r = 0; r < d; ++r)
+    for (int c = 0; c < d; ++c) a.v[r][c] = e.v[plan.in_idx[nc + r]][miss[c]];
+  if (d && !gf_invert(a, d, ainv, work)) return -1;  // cannot happen for this code (MDS)
+  // rows of the missing data over the k survivors, kept in a.v (a is no longer needed)
+  for (int r = 0; r < d; ++r) {
+    for (int p = 0; p < nc; ++p) {
+      const int col = plan.in_idx[p];
+      uint8_t acc = 0;
+      for (int b = 0; b < d; ++b) acc ^= gf_mul(ainv.v[r][b], e.v[plan.in_idx[nc + b]][col]);
+      a.v[r][p] = acc;
+    }
+    for (int b = 0; b < d; ++b) a.v[r][nc + b] = ainv.v[r][b];
+  }
+  int mrow[kMaxShards] = {};  // missing data shard -> its row in a
+  for (int r = 0; r < d; ++r) mrow[miss[r]] = r;
+  plan.nout = 0;
+  for (int i = 0; i < n; ++i) {
+    if (present[i] || (data_only && i >= k)) continue;
+    const int o = plan.nout++;
+    plan.out_idx[o] = (uint8_t)i;
+    if (i < k) {
+      for (int c = 0; c < k; ++c) plan.coef.v[o][c] = a.v[mrow[i]][c];
+      continue;
+    }
+    // a lost parity shard: its encode row over the data, the missing data substituted
+    for (int c = 0; c < k; ++c) plan.coef.v[o][c] = c < nc ? e.v[i][plan.in_idx[c]] : 0;
+    for (int r = 0; r < d; ++r) {
+      const uint8_t f = e.v[i][miss[r]];
+      if (!f) continue;
+      for (int c = 0; c < k; ++c) plan.coef.v[o][c] ^= gf_mul(f, a.v[r][c]);
+    }
+  }
+  plan.coef.rows = plan.nout;
+  plan.coef.cols = k;
+  return 0;
+}
+
 // ---- additive FFT over the subspace of the first 2^K field elements -------------------------
 // RS(2^K, 2^K) in this convention has data = f(0..2^K-1) and parity i = f(2^K + i) for the
 // unique f of degree < 2^K (E = V * inv(V_top), V[r][c] = r^c). The points 0..2^K-1 are the

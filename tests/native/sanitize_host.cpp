@@ -169,6 +169,27 @@ using Big = cec::Mat<cec::kMaxShards, cec::kMaxShards>;
 using Work = cec::Mat<cec::kMaxShards, 2 * cec::kMaxShards>;
 using BigPlan = cec::Plan<cec::kMaxShards, cec::kMaxShards>;
 
+// the systematic plan (run time, d x d inverse) equals the Gauss-Jordan plan (k x 2k)
+static void same_plans(int k, int m, const uint8_t* present, bool data_only, const Big& E) {
+  auto p1 = std::make_unique<BigPlan>();
+  auto p2 = std::make_unique<BigPlan>();
+  auto s1 = std::make_unique<Big>();
+  auto s2 = std::make_unique<Big>();
+  auto i1 = std::make_unique<Big>();
+  auto i2 = std::make_unique<Big>();
+  auto w = std::make_unique<Work>();
+  const int r1 = cec::gf_decode_plan(k, m, present, data_only, E, *p1, *s1, *i1, *w);
+  const int r2 = cec::gf_decode_plan_sys(k, m, present, data_only, E, *p2, *s2, *i2, *w);
+  CHECK(r1 == r2);
+  if (r1) return;
+  CHECK(p1->nout == p2->nout);
+  for (int j = 0; j < k; ++j) CHECK(p1->in_idx[j] == p2->in_idx[j]);
+  for (int o = 0; o < p1->nout; ++o) {
+    CHECK(p1->out_idx[o] == p2->out_idx[o]);
+    for (int c = 0; c < k; ++c) CHECK(p1->coef.v[o][c] == p2->coef.v[o][c]);
+  }
+}
+
 static void matrices() {
   const int codes[][2] = {{2, 1}, {4, 2}, {5, 5}, {10, 4}, {3, 3}};
   for (auto& km : codes) {
@@ -196,6 +217,25 @@ static void matrices() {
             acc ^= cec::gf_mul(plan->coef.v[o][j], E->v[plan->in_idx[j]][c]);
           CHECK(acc == E->v[plan->out_idx[o]][c]);
         }
+      for (int data_only = 0; data_only < 2; ++data_only) same_plans(k, m, present, data_only, *E);
+    }
+  }
+  // the wide codes: random patterns of every erasure count
+  std::mt19937 g(7);
+  const int wide[][2] = {{32, 32}, {200, 56}, {17, 3}};
+  for (auto& km : wide) {
+    const int k = km[0], m = km[1], n = k + m;
+    auto E = std::make_unique<Big>();
+    auto top = std::make_unique<Big>();
+    auto topinv = std::make_unique<Big>();
+    auto work = std::make_unique<Work>();
+    CHECK(cec::gf_encode_matrix(k, m, *E, *top, *topinv, *work));
+    for (int t = 0; t < 60; ++t) {
+      uint8_t present[cec::kMaxShards] = {};
+      for (int i = 0; i < n; ++i) present[i] = 1;
+      const int e = 1 + (int)(g() % m);
+      for (int q = 0; q < e; ++q) present[g() % n] = 0;
+      same_plans(k, m, present, t & 1, *E);
     }
   }
 }

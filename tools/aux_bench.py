@@ -50,6 +50,8 @@ def main():
 
     if args.only == "partial":
         return partial_row(args, torch, np, cess_amd, dev)
+    if args.only == "plan":
+        return plan_row(args, torch, np, cess_amd, dev)
     d = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
     p = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
     cess_amd.fill_synthetic(d, k * F, nseg, 0, 0xCE550002)
@@ -97,6 +99,40 @@ def main():
                       "generate_and_hash_s": round(t_f, 4),
                       "GBps": round(nseg * F / t_f / GB, 2)}), flush=True)
     partial_row(args, torch, np, cess_amd, dev)
+
+
+def plan_row(args, torch, np, cess_amd, dev):
+    """Host cost of a per-segment rebuild whose erasure patterns are new to the decode cache
+    (matrix inversions + program uploads) against the same call with a cached plan."""
+    k, m, F, nseg = 32, 32, 512 << 10, 64
+    n = k + m
+    enc = cess_amd.New(k, m)
+    d = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
+    p = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
+    cess_amd.fill_synthetic(d, k * F, nseg, 0, 0xCE550006)
+    enc.EncodeBatch(d, p, nseg, F)
+    rng = np.random.default_rng(1)
+
+    def fresh(e):
+        pres = np.ones((nseg, n), np.uint8)
+        for s in range(nseg):
+            pres[s, rng.choice(n, size=e, replace=False)] = 0
+        return pres
+
+    out = {"row": "plan build", "code": "RS(32,32)", "segments": nseg, "fragment_bytes": F}
+    for e in (1, 4, 16):
+        ts_new, ts_cached = [], []
+        for _ in range(max(3, args.reps)):
+            pres = fresh(e)
+            for ts in (ts_new, ts_cached):  # first call builds the plan, second reuses it
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                enc.ReconstructBatch(d, p, nseg, F, pres)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+        out[f"e{e}_new_patterns_ms"] = round(float(np.median(ts_new)) * 1e3, 3)
+        out[f"e{e}_cached_plan_ms"] = round(float(np.median(ts_cached)) * 1e3, 3)
+    print(json.dumps(out), flush=True)
 
 
 def partial_row(args, torch, np, cess_amd, dev):
