@@ -174,9 +174,50 @@ using ProgPtr = std::shared_ptr<const Program>;
 // run on `upload` and are complete when this returns.
 // `partial`: the rows do not rebuild a shard by themselves (cec_reconstruct_partial_batch), so
 // the compile-time single-erasure kernels never stand in for the program.
-// With `keep`, the host images move there and the uploads are left in flight: the caller
-// synchronises `upload` once for a whole plan before launching or dropping `keep`.
-using HostImages = std::vector<std::vector<uint32_t>>;
+// Page-locked staging for program images whose uploads stay in flight until one synchronisation
+// per plan: an upload from pinned memory is a DMA enqueue, one from pageable memory is staged by
+// the runtime (measured: 64 new RS(32,32) patterns per call cost ~0.9 ms of host time beyond the
+// kernel with pageable images). Blocks of >= 1 MiB, kept for reuse; reset() after the sync.
+class PinnedArena {
+ public:
+  ~PinnedArena() {
+    for (auto& b : blocks_) (void)hipHostFree(b.p);
+  }
+  // `bytes` of zeroed page-locked memory valid until reset(), or nullptr (caller falls back)
+  uint32_t* take(size_t bytes) {
+    bytes = (bytes + 255) & ~size_t(255);
+    for (; cur_ < blocks_.size(); ++cur_)
+      if (blocks_[cur_].used + bytes <= blocks_[cur_].cap) break;
+    if (cur_ == blocks_.size()) {
+      Block b{nullptr, std::max(bytes, size_t(1) << 20), 0};
+      if (hipHostMalloc(reinterpret_cast<void**>(&b.p), b.cap, hipHostMallocDefault) != hipSuccess)
+        return nullptr;
+      blocks_.push_back(b);
+    }
+    Block& b = blocks_[cur_];
+    uint8_t* p = b.p + b.used;
+    b.used += bytes;
+    std::memset(p, 0, bytes);
+    return reinterpret_cast<uint32_t*>(p);
+  }
+  void reset() {
+    for (auto& b : blocks_) b.used = 0;
+    cur_ = 0;
+  }
+  bool busy() const { return cur_ > 0 || (!blocks_.empty() && blocks_[0].used); }
+
+ private:
+  struct Block {
+    uint8_t* p;
+    size_t cap, used;
+  };
+  std::vector<Block> blocks_;
+  size_t cur_ = 0;
+};
+
+// With `keep`, the images are written into that arena and the uploads are left in flight: the
+// caller synchronises `upload` once for a whole plan before launching or resetting the arena.
+using HostImages = PinnedArena;
 int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int nin,
                   const uint8_t* out_idx, int nout, const BigMat& coef, ProgPtr* out,
                   bool partial = false, HostImages* keep = nullptr) {
@@ -190,21 +231,27 @@ int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int 
   prog->partial = partial;
   std::memcpy(prog->in_idx, in_idx, nin);
   std::memcpy(prog->out_idx, out_idx, nout);
-  std::vector<std::vector<uint32_t>> hosts;
+  std::vector<std::vector<uint32_t>> hosts;  // images when there is no arena (or it is full)
+  bool staged = keep != nullptr;
   for (int o0 = 0; o0 < nout; o0 += cec::kRtMaxOut) {
     RtChunk c;
     c.nin = nin;
     c.nout = std::min(cec::kRtMaxOut, nout - o0);
     c.nob = cec::rt_bucket(c.nout);
-    hosts.emplace_back(cec::rt_chunk_bytes(nin, c.nob) / sizeof(uint32_t), 0u);
-    std::vector<uint32_t>& h = hosts.back();
+    const size_t words = cec::rt_chunk_bytes(nin, c.nob) / sizeof(uint32_t);
+    uint32_t* h = keep ? keep->take(words * sizeof(uint32_t)) : nullptr;
+    if (!h) {
+      hosts.emplace_back(words, 0u);
+      h = hosts.back().data();
+      staged = false;  // a pageable image: synchronise before it dies
+    }
     h[0] = (uint32_t)nin;
     h[1] = (uint32_t)c.nout;
     h[2] = (uint32_t)c.nob;
     for (int j = 0; j < nin; ++j) h[4 + j] = in_idx[j];
     for (int o = 0; o < c.nout; ++o) h[4 + 256 + o] = out_idx[o0 + o];
-    uint32_t* hb = h.data() + 4 + 512;
-    uint32_t* mk = h.data() + cec::kRtHeaderWords;
+    uint32_t* hb = h + 4 + 512;
+    uint32_t* mk = h + cec::kRtHeaderWords;
     for (int j = 0; j < nin; ++j) {
       int top = -1;
       for (int o = 0; o < c.nout; ++o) {
@@ -222,7 +269,7 @@ int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int 
       // combination index of the group's inputs whose coefficient has that bit
       const size_t hoff = cec::kRtHeaderWords + (size_t)nin * 8 * c.nob;
       h[3] = (uint32_t)hoff;
-      uint32_t* top = h.data() + hoff;
+      uint32_t* top = h + hoff;
       uint32_t* ix = top + 32;
       for (int o = 0; o < c.nout; ++o) {
         int t = -1;
@@ -235,21 +282,18 @@ int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int 
             if (coef.v[o0 + o][j] >> b & 1) ix[((size_t)o * 8 + b) * 8 + j / 4] |= 1u << (j % 4);
       }
     }
-    c.bytes = h.size() * sizeof(uint32_t);
+    c.bytes = words * sizeof(uint32_t);
     void* d = nullptr;
     int rc = pool.alloc(c.bytes, &d);
     if (rc) return rc;  // prog's deleter retires the chunks built so far
     c.dev = static_cast<uint32_t*>(d);
     prog->chunks.push_back(c);
-    HIP_TRY(hipMemcpyAsync(c.dev, h.data(), c.bytes, hipMemcpyHostToDevice, upload));
+    HIP_TRY(hipMemcpyAsync(c.dev, h, c.bytes, hipMemcpyHostToDevice, upload));
   }
   // the block may be a reused one whose readers have completed; the upload must land before
-  // any caller-stream launch that reads it, and the host vectors die here (or with `keep`)
-  if (keep) {
-    for (auto& h : hosts) keep->push_back(std::move(h));
-  } else {
-    HIP_TRY(hipStreamSynchronize(upload));
-  }
+  // any caller-stream launch that reads it, and pageable images die here (arena images live
+  // until the caller's synchronisation)
+  if (!staged) HIP_TRY(hipStreamSynchronize(upload));
   *out = std::move(prog);
   return CEC_OK;
 }
@@ -298,6 +342,19 @@ struct cec_codec {
   std::list<std::string> lru;
   size_t cache_cap = kDefaultDecodeCache;
   std::unique_ptr<PsPlan> ps;
+  // decode-plan scratch, reused pattern after pattern (a codec is not re-entrant): allocating
+  // and zeroing these ~450 KB per new pattern was most of a new plan's host time
+  struct PlanScratch {
+    BigPlan plan;
+    BigMat a, ainv, coef;
+    WorkMat work;
+  };
+  std::unique_ptr<PlanScratch> scratch;
+  PinnedArena arena;  // program images of a plan being built (uploads in flight)
+  PlanScratch& plan_scratch() {
+    if (!scratch) scratch = std::make_unique<PlanScratch>();
+    return *scratch;
+  }
   // staging for the host-buffer API: [n][stride]
   uint8_t* stage = nullptr;
   size_t stage_bytes = 0;
@@ -405,13 +462,12 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* ou
     *out = it->second.prog;
     return CEC_OK;
   }
-  auto plan = std::make_unique<BigPlan>();
-  auto sub = std::make_unique<BigMat>();
-  auto inv = std::make_unique<BigMat>();
-  auto work = std::make_unique<WorkMat>();
+  auto& sc = c->plan_scratch();
+  auto* plan = &sc.plan;
   uint8_t flags[cec::kMaxShards];
   for (int i = 0; i < n; ++i) flags[i] = key[i];
-  if (cec::gf_decode_plan_sys(c->k, c->m, flags, data_only, *c->E, *plan, *sub, *inv, *work) != 0)
+  if (cec::gf_decode_plan_sys(c->k, c->m, flags, data_only, *c->E, *plan, sc.a, sc.ainv,
+                              sc.work) != 0)
     return set_err(CEC_ETOOFEW, "fewer than k shards present");
   ProgPtr prog;
   if (plan->nout > 0) {
@@ -443,25 +499,25 @@ int get_partial(cec_codec* c, const uint8_t* present, const uint8_t* held, bool 
     *out = it->second.prog;
     return CEC_OK;
   }
-  auto plan = std::make_unique<BigPlan>();
-  auto sub = std::make_unique<BigMat>();
-  auto inv = std::make_unique<BigMat>();
-  auto work = std::make_unique<WorkMat>();
+  auto& sc = c->plan_scratch();
+  auto* plan = &sc.plan;
   uint8_t flags[cec::kMaxShards];
   for (int i = 0; i < n; ++i) flags[i] = present[i] ? 1 : 0;
-  if (cec::gf_decode_plan_sys(c->k, c->m, flags, data_only, *c->E, *plan, *sub, *inv, *work) != 0)
+  if (cec::gf_decode_plan_sys(c->k, c->m, flags, data_only, *c->E, *plan, sc.a, sc.ainv,
+                              sc.work) != 0)
     return set_err(CEC_ETOOFEW, "fewer than k shards present");
   ProgPtr prog;
   if (plan->nout > 0) {
     uint8_t in_sub[cec::kMaxShards];
     int nsub = 0;
-    auto coef = std::make_unique<BigMat>();
+    auto* coef = &sc.coef;
+    for (int o = 0; o < plan->nout; ++o) std::memset(coef->v[o], 0, sizeof coef->v[o]);
     for (int j = 0; j < c->k; ++j)
       if (held[plan->in_idx[j]]) {
         for (int o = 0; o < plan->nout; ++o) coef->v[o][nsub] = plan->coef.v[o][j];
         in_sub[nsub++] = plan->in_idx[j];
       }
-    if (nsub == 0) {  // zero program: one column, zero coefficients (BigMat starts zeroed)
+    if (nsub == 0) {  // zero program: one column, zero coefficients (cleared above)
       in_sub[0] = plan->in_idx[0];
       nsub = 1;
     }
@@ -564,16 +620,17 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
   // path waits for them before their host images go
   struct Uploads {
     hipStream_t st;
-    HostImages images;
+    PinnedArena& arena;
     ~Uploads() {
-      if (!images.empty()) (void)hipStreamSynchronize(st);
+      if (arena.busy()) (void)hipStreamSynchronize(st);
+      arena.reset();
     }
-  } up{c->stream, {}};
+  } up{c->stream, c->arena};
   for (auto& g : groups) {
     ProgPtr p;
     const uint8_t* flags = reinterpret_cast<const uint8_t*>(g.first.data());
-    int rc = partial ? get_partial(c, flags, flags + n, data_only, &p, &up.images)
-                     : get_decode(c, flags, data_only, &p, &up.images);
+    int rc = partial ? get_partial(c, flags, flags + n, data_only, &p, &up.arena)
+                     : get_decode(c, flags, data_only, &p, &up.arena);
     if (rc) return rc;
     plan->keys.push_back(partial ? partial_key(flags, flags + n, n, data_only)
                                  : pattern_key(flags, n, data_only));
@@ -663,7 +720,7 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
     c->pool.retire(plan->ptrs, plan->ptrs_bytes);
     return set_err(CEC_EHIP, std::string("plan upload: ") + hipGetErrorString(e));
   }
-  up.images.clear();
+  up.arena.reset();  // its uploads have landed
   *out = std::move(plan);
   return CEC_OK;
 }
