@@ -363,11 +363,14 @@ def test_segment_list_auto_placement(torch, cess, orc, monkeypatch):
     se.close()
 
 
-def test_degraded_read_single_rank(torch, cess, corc):
+@pytest.mark.parametrize("k,m,exchange", [(2, 1, "survivors"), (2, 1, "partials"),
+                                          (10, 4, "partials"), (10, 4, "auto")])
+def test_degraded_read_single_rank(torch, cess, corc, k, m, exchange):
     """distributed.degraded_read end to end on one GPU (world 1: every survivor is local, so
-    no P2P op is issued; the decode runs through libcessec)."""
+    no P2P op is issued; the decode runs through libcessec). With the partial-product exchange
+    the decoder holds every survivor: its own partial is the whole rebuild, nothing to XOR."""
     from cess_amd import distributed as D
-    k, m, F, nseg = 2, 1, 1 << 16, 6
+    F, nseg = 1 << 16, 6
     rng = np.random.default_rng(11)
     full = []
     for s in range(nseg):
@@ -376,9 +379,10 @@ def test_degraded_read_single_rank(torch, cess, corc):
     mine = D.local_fragments(nseg, k + m, 1, 0)
     store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
                             torch.from_numpy(np.stack([full[s][f] for s, f in mine])).cuda())
-    lost = {s: [s % 3] for s in range(nseg)}
-    plan = D.plan_gather(lost, k, m, 1, F)
+    lost = {s: [s % (k + m)] for s in range(nseg)}
+    plan = D.plan_gather(lost, k, m, 1, F, exchange=exchange)
     assert plan.bytes_moved == 0
+    assert bool(plan.partial) == (exchange == "partials")
     out = D.degraded_read(plan, store, cess.New(k, m), 0)
     torch.cuda.synchronize()
     assert len(out) == nseg
