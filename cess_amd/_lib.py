@@ -55,6 +55,8 @@ SIGNATURES = {
     "cec_reconstruct_partial_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t,
                                               POINTER(c_uint8), POINTER(c_uint8), c_int,
                                               c_void_p]),
+    "cec_verify_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p,
+                                 c_void_p]),
     "cec_xor_batch": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_void_p]),
     "cec_sha256_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p,
                                  c_void_p]),

@@ -982,6 +982,42 @@ int cec_reconstruct_partial_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_pari
   return rc ? rc : mrc;
 }
 
+int cec_verify_batch(cec_codec* c, const uint8_t* d_data, const uint8_t* d_parity, size_t nseg,
+                     size_t shard_len, uint8_t* d_ok, void* hip_stream) {
+  if (!c || !d_ok || (nseg && (!d_data || !d_parity))) return set_err(CEC_EINVAL, "null");
+  if (shard_len == 0) return set_err(CEC_ESHARDLEN, "zero shard length");
+  if (nseg > 0xffffffffull) return set_err(CEC_EINVAL, "too many segments");
+  if (nseg == 0) return CEC_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = pick_stream(c, hip_stream);
+  if (!c->force_generic) {  // RS(2,1): recompute and compare in one read-only pass
+    Layout L = batch_layout(c, d_data, const_cast<uint8_t*>(d_parity), shard_len);
+    HIP_TRY(hipMemsetAsync(d_ok, 1, nseg, st));
+    if (cec::launch_verify_ct(c->k, c->m, L, d_ok, (uint32_t)nseg, st)) return check_launch();
+  }
+  // the parity recomputed into a scratch batch (the encode kernels: FFT for RS(32,32)), then
+  // compared segment by segment with the stored parity
+  const size_t pbytes = nseg * (size_t)c->m * shard_len;
+  void* scratch = nullptr;
+  int rc = c->pool.alloc(pbytes, &scratch);
+  if (rc) return rc;
+  Layout L = batch_layout(c, d_data, static_cast<uint8_t*>(scratch), shard_len);
+  hipError_t e = hipMemsetAsync(d_ok, 1, nseg, st);
+  if (e == hipSuccess) {
+    rc = do_encode(c, L, nullptr, (uint32_t)nseg, st);
+    if (!rc) {
+      cec::launch_cmp_segments(static_cast<const uint8_t*>(scratch), d_parity,
+                               (uint64_t)c->m * shard_len, nseg, d_ok, st);
+      rc = check_launch();
+    }
+  } else {
+    rc = set_err(CEC_EHIP, std::string("verify: ") + hipGetErrorString(e));
+  }
+  const int mrc = c->pool.mark(st);  // the scratch stays until these launches complete
+  c->pool.retire(scratch, pbytes);
+  return rc ? rc : mrc;
+}
+
 int cec_xor_batch(uint8_t* d_dst, const uint8_t* d_src, size_t nsrc, size_t src_stride,
                   size_t len, void* hip_stream) {
   if ((len && nsrc && (!d_dst || !d_src)) || nsrc > 0xffffffffull)

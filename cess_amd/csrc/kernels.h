@@ -66,6 +66,10 @@ bool launch_decode_ct(const KernelOpts& o, int k, int m, int missing, const Layo
 bool launch_decode1_mixed(const KernelOpts& o, int k, int m, const Layout& L,
                           const uint32_t* tagged, uint32_t nseg, hipStream_t st);
 
+// Verify fused with the recompute (RS(2,1)): ok[s] = 0 where the stored parity differs (ok preset
+// by the caller). False (nothing launched) for other codes or layouts.
+bool launch_verify_ct(int k, int m, const Layout& L, uint8_t* ok, uint32_t nseg, hipStream_t st);
+
 // RS(32,32) encode as an additive FFT on bit-sliced data (fft.hip). False (nothing launched)
 // when the layout does not fit (shard_len % 1024, 16-byte alignment).
 bool launch_fft_rs3232(const Layout& L, const uint32_t* seg_list, uint32_t nseg, int nt,
@@ -139,6 +143,10 @@ void launch_chunk_gather(const Layout& L, int nshards, uint64_t nfrag, const uin
 // XOR reduction (xor.hip): dst[0..len) ^= src[j * stride ..][0..len) for j < nsrc.
 void launch_xor_reduce(uint8_t* dst, const uint8_t* src, uint32_t nsrc, uint64_t stride,
                        uint64_t len, hipStream_t st);
+
+// ok[s] = 0 for every segment s whose seg_bytes of a and b differ (ok preset by the caller).
+void launch_cmp_segments(const uint8_t* a, const uint8_t* b, uint64_t seg_bytes, uint64_t nseg,
+                         uint8_t* ok, hipStream_t st);
 
 // Synthetic segment bytes: 64-bit word w of segment s = splitmix64(seed ^ (s << 32) ^ w),
 // little-endian; segments are seg_bytes long and contiguous from `out`.

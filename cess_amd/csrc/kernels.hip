@@ -1406,6 +1406,30 @@ bool launch_encode_ct(const KernelOpts& o, int k, int m, const Layout& L,
   return false;
 }
 
+// RS(2,1) verify fused into one pass (cec_verify_batch): the parity 2 (d0 ^ d1) ^ d0 recomputed in
+// registers and compared with the stored one, (k+m) F read per segment and nothing written but
+// the flag of a segment that differs.
+__global__ __launch_bounds__(256) void k_verify21(Layout L, uint8_t* __restrict__ ok,
+                                                  uint32_t seg0) {
+  const uint32_t seg = seg0 + blockIdx.y;
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v * 16 >= L.len) return;
+  const u32x4 d0 = ld16<true>(shard_ptr(L, 0, seg) + v * 16);
+  const u32x4 d1 = ld16<true>(shard_ptr(L, 1, seg) + v * 16);
+  const u32x4 p = ld16<true>(shard_ptr(L, 2, seg) + v * 16);
+  const u32x4 z = xt(d0 ^ d1) ^ d0 ^ p;
+  if (z.x | z.y | z.z | z.w) ok[seg] = 0;
+}
+
+bool launch_verify_ct(int k, int m, const Layout& L, uint8_t* ok, uint32_t nseg, hipStream_t st) {
+  if (k != 2 || m != 1 || !layout_vec16_ok(L) || (L.len & 15)) return false;
+  const uint64_t gx = (L.len / 16 + 255) / 256;
+  for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {
+    hipLaunchKernelGGL(k_verify21, dim3((unsigned)gx, ny), dim3(256), 0, st, L, ok, s0);
+  });
+  return true;
+}
+
 bool launch_decode1_mixed(const KernelOpts& o, int k, int m, const Layout& L,
                           const uint32_t* tagged, uint32_t nseg, hipStream_t st) {
   // the default variant only (a variant set for a sweep keeps the per-pattern launches)

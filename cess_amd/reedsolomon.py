@@ -306,6 +306,25 @@ class Encoder:
             p.ctypes.data_as(POINTER(c_uint8)), h.ctypes.data_as(POINTER(c_uint8)),
             1 if data_only else 0, _stream_handle(stream)), "ReconstructPartialBatch")
 
+    def VerifyBatch(self, d_data, d_parity, nseg: int, shard_len: int, d_ok=None,
+                    stream=None):
+        """klauspost Verify over an HBM batch (cec_verify_batch): with `d_ok` (device uint8
+        [nseg]) the per-segment flags are enqueued there; without, they are returned as a numpy
+        bool array (synchronous)."""
+        import torch
+        out = d_ok
+        if out is None:
+            out = torch.empty(max(1, nseg), dtype=torch.uint8,
+                              device=torch.device("cuda", self.device))
+        check(self._lib.cec_verify_batch(self._h, _dev_ptr(d_data), _dev_ptr(d_parity), nseg,
+                                         shard_len, _dev_ptr(out), _stream_handle(stream)),
+              "VerifyBatch")
+        if d_ok is not None:
+            return None
+        if stream is not None:
+            stream.synchronize()
+        return out[:nseg].cpu().numpy().astype(bool)
+
     def Sha256Batch(self, d_data, d_parity, nseg: int, shard_len: int, d_hex,
                     stream=None) -> None:
         """Hex SHA-256 of every shard into d_hex ([nseg][k+m][64] bytes, device)."""

@@ -97,6 +97,11 @@ int cec_reconstruct_batch(cec_codec* codec, uint8_t* d_data, uint8_t* d_parity, 
 int cec_reconstruct_partial_batch(cec_codec* codec, uint8_t* d_data, uint8_t* d_parity,
                                   size_t nseg, size_t shard_len, const uint8_t* present,
                                   const uint8_t* held, int data_only, void* hip_stream);
+/* Verify for a batch (klauspost Verify over HBM): d_ok[s] (device, nseg bytes) = 1 when the
+ * parity shards of segment s equal the encode of its data shards, else 0. The parity is
+ * recomputed into codec-owned scratch and compared; nothing in the batch is written. */
+int cec_verify_batch(cec_codec* codec, const uint8_t* d_data, const uint8_t* d_parity,
+                     size_t nseg, size_t shard_len, uint8_t* d_ok, void* hip_stream);
 /* GF(2^8) addition of device buffers: d_dst[0..len) ^= d_src[j*src_stride ..][0..len) for
  * j < nsrc (src_stride >= len when nsrc > 1). Enqueued on hip_stream. */
 int cec_xor_batch(uint8_t* d_dst, const uint8_t* d_src, size_t nsrc, size_t src_stride,

@@ -774,3 +774,33 @@ def test_all_parity_lost_is_reencoded(torch, cess, corc, k, m, ln):
     torch.cuda.synchronize()
     assert np.array_equal(d_data.cpu().numpy(), data)
     assert np.array_equal(d_par.cpu().numpy(), par)
+
+
+@pytest.mark.parametrize("k,m,ln,nseg", [(2, 1, 1 << 16, 9), (2, 1, 4099, 5), (4, 2, 1000, 7),
+                                         (10, 4, 4096, 6), (32, 32, 4096, 5)])
+def test_verify_batch(torch, cess, corc, k, m, ln, nseg):
+    """cec_verify_batch (klauspost Verify over an HBM batch): every segment whose stored parity
+    equals the C oracle's encode passes; one flipped byte anywhere in a segment's parity (or
+    data) fails that segment only; the batch itself is not modified."""
+    rng = np.random.default_rng(k * 13 + ln)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    par = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    enc = cess.New(k, m)
+    d_data, d_par = to_dev(torch, data), to_dev(torch, par)
+    assert enc.VerifyBatch(d_data, d_par, nseg, ln).all()
+    enc.set_option(1, 1)  # the generic recompute-and-compare path as well
+    assert enc.VerifyBatch(d_data, d_par, nseg, ln).all()
+    enc.set_option(1, 0)
+    bad = {1: ("p", m - 1, ln - 1), nseg - 1: ("d", 0, ln // 2)}
+    for s, (which, i, off) in bad.items():
+        t = d_par if which == "p" else d_data
+        t[s, i, off] ^= 0x5A
+    for generic in (0, 1):
+        enc.set_option(1, generic)
+        ok = enc.VerifyBatch(d_data, d_par, nseg, ln)
+        assert list(ok) == [s not in bad for s in range(nseg)], generic
+    enc.set_option(1, 0)
+    for s, (which, i, off) in bad.items():  # restore: the verify wrote nothing else
+        t = d_par if which == "p" else d_data
+        t[s, i, off] ^= 0x5A
+    assert np.array_equal(d_par.cpu().numpy(), par) and np.array_equal(d_data.cpu().numpy(), data)

@@ -52,6 +52,8 @@ def main():
         return partial_row(args, torch, np, cess_amd, dev)
     if args.only == "plan":
         return plan_row(args, torch, np, cess_amd, dev)
+    if args.only == "verify":
+        return verify_row(args, torch, np, cess_amd, dev)
     d = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
     p = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
     cess_amd.fill_synthetic(d, k * F, nseg, 0, 0xCE550002)
@@ -99,6 +101,34 @@ def main():
                       "generate_and_hash_s": round(t_f, 4),
                       "GBps": round(nseg * F / t_f / GB, 2)}), flush=True)
     partial_row(args, torch, np, cess_amd, dev)
+
+
+def verify_row(args, torch, np, cess_amd, dev):
+    """cec_verify_batch over a 1 GiB batch: parity recomputed into scratch, compared."""
+    for k, m, F in ((2, 1, 8 << 20), (32, 32, 512 << 10)):
+        nseg = 64
+        enc = cess_amd.New(k, m)
+        d = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
+        p = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
+        ok = torch.empty(nseg, dtype=torch.uint8, device=dev)
+        cess_amd.fill_synthetic(d, k * F, nseg, 0, 0xCE550007)
+        enc.EncodeBatch(d, p, nseg, F)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        enc.VerifyBatch(d, p, nseg, F, ok)
+        a.record()
+        for _ in range(20):
+            enc.VerifyBatch(d, p, nseg, F, ok)
+        b.record()
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / 20
+        assert bool(ok.all())
+        fused = (k, m) == (2, 1)  # one read-only pass; else recompute into scratch + compare
+        moved = nseg * ((k + m) if fused else (k + 3 * m)) * F
+        print(json.dumps({"row": "verify batch", "code": f"RS({k},{m})", "segments": nseg,
+                          "fragment_bytes": F, "ms": round(ms, 4),
+                          "path": "fused k_verify21" if fused else "encode to scratch + compare",
+                          "GBps_of_k_plus_m": round(nseg * (k + m) * F / (ms * 1e-3) / GB, 1),
+                          "GBps_moved": round(moved / (ms * 1e-3) / GB, 1)}), flush=True)
 
 
 def plan_row(args, torch, np, cess_amd, dev):

@@ -115,6 +115,9 @@ pub mod sys {
                                              d_parity: *mut u8, nseg: usize, shard_len: usize,
                                              present: *const u8, held: *const u8,
                                              data_only: c_int, stream: *mut c_void) -> c_int;
+        pub fn cec_verify_batch(c: *mut cec_codec, d_data: *const u8, d_parity: *const u8,
+                                nseg: usize, shard_len: usize, d_ok: *mut u8,
+                                stream: *mut c_void) -> c_int;
         pub fn cec_xor_batch(d_dst: *mut u8, d_src: *const u8, nsrc: usize, src_stride: usize,
                              len: usize, stream: *mut c_void) -> c_int;
         pub fn cec_sha256_batch(c: *mut cec_codec, d_data: *const u8, d_parity: *const u8,
