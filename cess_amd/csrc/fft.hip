@@ -168,8 +168,11 @@ __device__ __forceinline__ void st32(uint8_t* p, const uint32_t (&w)[8]) {
 // stores only, 3 = the same 4 shards at a time (few VGPRs, full occupancy); the outputs are then
 // not parity. They measure what the memory side alone costs at
 // this access pattern (with LDS > 0 at the kernel's own occupancy of 3 waves per SIMD).
-template <bool NT, bool NTS, int DIAG>
-__device__ __forceinline__ void fft_cols(const Layout& L, uint32_t seg, uint64_t col) {
+// VER: compare the parity with the stored one instead of writing it (cec_verify_batch: ok[seg]
+// = 0 where a byte differs).
+template <bool NT, bool NTS, int DIAG, bool VER = false>
+__device__ __forceinline__ void fft_cols(const Layout& L, uint32_t seg, uint64_t col,
+                                         uint8_t* ok = nullptr) {
   constexpr int K = 5;
   using T = Lch<K>;
   const uint32_t l = threadIdx.x & 1;
@@ -251,10 +254,43 @@ __device__ __forceinline__ void fft_cols(const Layout& L, uint32_t seg, uint64_t
     if constexpr (s != 0) mul_acc<s, false>(X[J], P, P);
   });
 
+  if constexpr (VER) {
+    uint32_t diff = 0;
+    sfor<16>([&](auto J) CEC_FFT_AI {
+      uint32_t Y[8];
+      ld32<NT>(dout + J * step, Y);
+      tr8(X[J]);
+      sfor<8>([&](auto Q) CEC_FFT_AI { diff |= X[J][Q] ^ Y[Q]; });
+    });
+    if (diff) ok[seg] = 0;
+    return;
+  }
   sfor<16>([&](auto J) CEC_FFT_AI {
     tr8(X[J]);
     st32<NTS>(dout + J * step, X[J]);
   });
+}
+
+// RS(32,32) verify: the encode's transform, compared with the stored parity (read-only).
+__global__ __launch_bounds__(256) void k_fft3232_verify(Layout L, uint8_t* __restrict__ ok,
+                                                        uint32_t seg0) {
+  const uint32_t seg = seg0 + blockIdx.y;
+  const uint64_t gp = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 1;  // lane pair
+  const uint64_t col = (gp >> 5) * 1024 + (gp & 31) * 16;
+  if (col >= L.len) return;
+  fft_cols<true, true, 0, true>(L, seg, col, ok);
+}
+
+bool launch_fft_rs3232_verify(const Layout& L, uint8_t* ok, uint32_t nseg, hipStream_t st) {
+  const uintptr_t bits = (uintptr_t)L.data | (uintptr_t)L.parity | L.shard_stride |
+                         L.data_seg_stride | L.par_seg_stride;
+  if ((bits & 15) || (L.len & 1023) || L.len == 0 || L.k != 32) return false;
+  const uint64_t gx = (L.len / 32 * 2 + 255) / 256;
+  for (uint32_t s0 = 0; s0 < nseg; s0 += 65535) {
+    const uint32_t ny = nseg - s0 < 65535 ? nseg - s0 : 65535;
+    hipLaunchKernelGGL(k_fft3232_verify, dim3((unsigned)gx, ny), dim3(256), 0, st, L, ok, s0);
+  }
+  return true;
 }
 
 // CPW (tuning build only, else 1): column blocks of 4 KiB per workgroup, walked in a loop, so the

@@ -66,14 +66,18 @@ bool launch_decode_ct(const KernelOpts& o, int k, int m, int missing, const Layo
 bool launch_decode1_mixed(const KernelOpts& o, int k, int m, const Layout& L,
                           const uint32_t* tagged, uint32_t nseg, hipStream_t st);
 
-// Verify fused with the recompute (RS(2,1)): ok[s] = 0 where the stored parity differs (ok preset
-// by the caller). False (nothing launched) for other codes or layouts.
+// Verify fused with the recompute (RS(2,1), RS(32,32)): ok[s] = 0 where the stored parity differs
+// (ok preset by the caller). False (nothing launched) for other codes or layouts.
 bool launch_verify_ct(int k, int m, const Layout& L, uint8_t* ok, uint32_t nseg, hipStream_t st);
 
 // RS(32,32) encode as an additive FFT on bit-sliced data (fft.hip). False (nothing launched)
 // when the layout does not fit (shard_len % 1024, 16-byte alignment).
 bool launch_fft_rs3232(const Layout& L, const uint32_t* seg_list, uint32_t nseg, int nt,
                        hipStream_t st);
+
+// RS(32,32) verify by the same transform, compared with the stored parity (ok preset by the
+// caller; ok[s] = 0 where segment s differs). False (nothing launched) where the layout does not fit.
+bool launch_fft_rs3232_verify(const Layout& L, uint8_t* ok, uint32_t nseg, hipStream_t st);
 
 // Whether a compile-time single-erasure decode kernel exists for (k, m, missing).
 bool has_decode_ct(int k, int m, int missing);

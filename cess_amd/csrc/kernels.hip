@@ -1422,6 +1422,7 @@ __global__ __launch_bounds__(256) void k_verify21(Layout L, uint8_t* __restrict_
 }
 
 bool launch_verify_ct(int k, int m, const Layout& L, uint8_t* ok, uint32_t nseg, hipStream_t st) {
+  if (k == 32 && m == 32) return launch_fft_rs3232_verify(L, ok, nseg, st);
   if (k != 2 || m != 1 || !layout_vec16_ok(L) || (L.len & 15)) return false;
   const uint64_t gx = (L.len / 16 + 255) / 256;
   for_seg_chunks(nseg, [&](uint32_t s0, uint32_t ny) CEC_AI {

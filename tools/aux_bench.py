@@ -122,11 +122,12 @@ def verify_row(args, torch, np, cess_amd, dev):
         torch.cuda.synchronize()
         ms = a.elapsed_time(b) / 20
         assert bool(ok.all())
-        fused = (k, m) == (2, 1)  # one read-only pass; else recompute into scratch + compare
+        fused = (k, m) in ((2, 1), (32, 32))  # one read-only pass (else scratch + compare)
         moved = nseg * ((k + m) if fused else (k + 3 * m)) * F
         print(json.dumps({"row": "verify batch", "code": f"RS({k},{m})", "segments": nseg,
                           "fragment_bytes": F, "ms": round(ms, 4),
-                          "path": "fused k_verify21" if fused else "encode to scratch + compare",
+                          "path": ("fused k_verify21" if k == 2 else "fused k_fft3232_verify")
+                          if fused else "encode to scratch + compare",
                           "GBps_of_k_plus_m": round(nseg * (k + m) * F / (ms * 1e-3) / GB, 1),
                           "GBps_moved": round(moved / (ms * 1e-3) / GB, 1)}), flush=True)
 
