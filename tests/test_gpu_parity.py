@@ -410,7 +410,7 @@ def test_max_shards_256(cess, corc):
 
 
 def test_more_segments_than_grid_y(torch, cess, corc):
-    """nseg > 65535 splits the launch over grid.y chunks (encode and per-segment decode)."""
+    """nseg > 65535 splits the launch over grid.y chunks (encode, verify, per-segment decode)."""
     k, m, ln, nseg = 2, 1, 32, 70000
     rng = np.random.default_rng(9)
     data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
@@ -423,6 +423,12 @@ def test_more_segments_than_grid_y(torch, cess, corc):
     want = np.zeros_like(par)
     corc.orc_encode_batch(k, m, data.ctypes.data, want.ctypes.data, nseg, ln, 8, 1)
     assert np.array_equal(par, want)
+    d_par[nseg - 2, 0, 5] ^= 1  # one bad segment in the last grid.y chunk
+    for generic in (0, 1):
+        enc.set_option(1, generic)
+        ok = enc.VerifyBatch(d_data, d_par, nseg, ln)
+        assert ok.sum() == nseg - 1 and not ok[nseg - 2], generic
+    enc.set_option(1, 0)
     present = np.ones((nseg, 3), np.uint8)
     present[np.arange(nseg), np.arange(nseg) % 3] = 0
     for generic in (0, 1):
@@ -432,6 +438,26 @@ def test_more_segments_than_grid_y(torch, cess, corc):
         enc.ReconstructBatch(dd, dp, nseg, ln, present)
         torch.cuda.synchronize()
         assert np.array_equal(dd.cpu().numpy(), data) and np.array_equal(dp.cpu().numpy(), want)
+
+
+def test_fft_more_segments_than_grid_y(torch, cess, corc):
+    """RS(32,32) (the FFT encode and the fused FFT verify) over 70,000 segments of 1 KiB
+    fragments: segments either side of each grid.y chunk boundary match the C oracle, and one
+    corrupted segment in the last chunk is the only one that fails verification."""
+    k, m, ln, nseg = 32, 32, 1024, 70000
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    d_data = torch.randint(0, 256, (nseg, k, ln), dtype=torch.uint8, device="cuda", generator=gen)
+    d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
+    enc = cess.New(k, m)
+    enc.EncodeBatch(d_data, d_par, nseg, ln)
+    torch.cuda.synchronize()
+    for s in (0, 65534, 65535, nseg - 1):
+        want = np.stack(c_encode(corc, k, m, list(d_data[s].cpu().numpy())))
+        assert np.array_equal(d_par[s].cpu().numpy(), want), s
+    assert enc.VerifyBatch(d_data, d_par, nseg, ln).all()
+    d_data[nseg - 3, 31, ln - 1] ^= 0x80
+    ok = enc.VerifyBatch(d_data, d_par, nseg, ln)
+    assert ok.sum() == nseg - 1 and not ok[nseg - 3]
 
 
 def test_encode_file_sharded_single_rank(tmp_path, orc):
