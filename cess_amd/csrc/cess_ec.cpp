@@ -407,7 +407,7 @@ void launch_chunk(const KernelOpts& o, const Layout& L, const uint32_t* chunk,
   // 3.36 vs 3.33; RS(10,4) encode 3.54 vs 3.41; bench.py --config 6 --erasures e / --config 8,
   // profiles/r02/rtb_sweep.txt)
   if ((o.rt_mode == 3 || (o.rt_mode == 0 && nob <= 4 && nin >= 4)) &&
-      cec::launch_matvec_rtb(L, chunk, per_seg, nob, seg_list, nseg, st))
+      cec::launch_matvec_rtb(L, chunk, per_seg, nob, seg_list, nseg, st, o.ct_variant))
     return;
   if (nin <= cec::kRthMaxIn &&
       cec::launch_matvec_rth(o, L, chunk, per_seg, nin, seg_list, nseg, st))

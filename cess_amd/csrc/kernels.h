@@ -92,7 +92,8 @@ void launch_matvec_rt(const Layout& L, const uint32_t* chunk, const uint32_t* co
 // Same product by bit-plane accumulators (k_rtb) for chunks of nob <= 4 outputs; false (nothing
 // launched) for a wider bucket.
 bool launch_matvec_rtb(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
-                       int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
+                       int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st,
+                       int variant = -1);
 // Same product from the chunks' Horner sections (every chunk of the launch has nin <= nin_max
 // <= kRthMaxIn). Returns false (nothing launched) if the form is disabled by the variant knob.
 bool launch_matvec_rth(const KernelOpts& o, const Layout& L, const uint32_t* chunk,

@@ -1394,7 +1394,7 @@ void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_
 }  // namespace
 
 #ifdef CEC_TUNING
-int max_ct_variant() { return 33; }
+int max_ct_variant() { return 45; }
 #else
 int max_ct_variant() { return 0; }
 #endif
@@ -1514,7 +1514,28 @@ void run_rtb(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_
 }  // namespace
 
 bool launch_matvec_rtb(const Layout& L, const uint32_t* chunk, const uint32_t* const* per_seg,
-                       int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+                       int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st,
+                       int variant) {
+#ifdef CEC_TUNING
+  // tuning build: 40-43 = two outputs as u32x2 PF1/PF2/PF4, u32x4 PF2; 44-45 = one output as
+  // u32x2 PF2, u32x4 PF2
+  if (nob == 2 && variant >= 40 && variant <= 43) {
+    switch (variant) {
+      case 40: run_rtb<2, u32x2, 1>(L, chunk, per_seg, seg_list, nseg, st); break;
+      case 41: run_rtb<2, u32x2, 2>(L, chunk, per_seg, seg_list, nseg, st); break;
+      case 42: run_rtb<2, u32x2, 4>(L, chunk, per_seg, seg_list, nseg, st); break;
+      default: run_rtb<2, u32x4, 2>(L, chunk, per_seg, seg_list, nseg, st); break;
+    }
+    return true;
+  }
+  if (nob == 1 && (variant == 44 || variant == 45)) {
+    if (variant == 44) run_rtb<1, u32x2, 2>(L, chunk, per_seg, seg_list, nseg, st);
+    else run_rtb<1, u32x4, 2>(L, chunk, per_seg, seg_list, nseg, st);
+    return true;
+  }
+#else
+  (void)variant;
+#endif
   switch (nob) {
     case 1: run_rtb<1, u32x4, 1>(L, chunk, per_seg, seg_list, nseg, st); return true;
     case 2: run_rtb<2, u32x4, 1>(L, chunk, per_seg, seg_list, nseg, st); return true;
