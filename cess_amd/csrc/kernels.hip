@@ -1394,7 +1394,7 @@ void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_
 }  // namespace
 
 #ifdef CEC_TUNING
-int max_ct_variant() { return 45; }
+int max_ct_variant() { return 49; }
 #else
 int max_ct_variant() { return 0; }
 #endif
@@ -1517,30 +1517,44 @@ bool launch_matvec_rtb(const Layout& L, const uint32_t* chunk, const uint32_t* c
                        int nob, const uint32_t* seg_list, uint32_t nseg, hipStream_t st,
                        int variant) {
 #ifdef CEC_TUNING
-  // tuning build: 40-43 = two outputs as u32x2 PF1/PF2/PF4, u32x4 PF2; 44-45 = one output as
-  // u32x2 PF2, u32x4 PF2
-  if (nob == 2 && variant >= 40 && variant <= 43) {
-    switch (variant) {
-      case 40: run_rtb<2, u32x2, 1>(L, chunk, per_seg, seg_list, nseg, st); break;
-      case 41: run_rtb<2, u32x2, 2>(L, chunk, per_seg, seg_list, nseg, st); break;
-      case 42: run_rtb<2, u32x2, 4>(L, chunk, per_seg, seg_list, nseg, st); break;
-      default: run_rtb<2, u32x4, 2>(L, chunk, per_seg, seg_list, nseg, st); break;
+  // tuning build (TV = column width per lane, PF = input columns in flight):
+  // two outputs 40-43 = u32x4 PF1 (the first default) / u32x2 PF8 / u32x4 PF2 / u32x2 PF2;
+  // one output 44-47 = u32x4 PF1 (the first default) / u32x2 PF2 / u32x2 PF1 / u32 PF4;
+  // three or four outputs 48-49 = u32 PF8 / u32x2 PF4 (the first default for four)
+  if (variant >= 40 && variant <= 49) {
+    const int v = variant;
+    if (nob == 2 && v <= 43) {
+      if (v == 40) run_rtb<2, u32x4, 1>(L, chunk, per_seg, seg_list, nseg, st);
+      else if (v == 41) run_rtb<2, u32x2, 8>(L, chunk, per_seg, seg_list, nseg, st);
+      else if (v == 42) run_rtb<2, u32x4, 2>(L, chunk, per_seg, seg_list, nseg, st);
+      else run_rtb<2, u32x2, 2>(L, chunk, per_seg, seg_list, nseg, st);
+      return true;
     }
-    return true;
-  }
-  if (nob == 1 && (variant == 44 || variant == 45)) {
-    if (variant == 44) run_rtb<1, u32x2, 2>(L, chunk, per_seg, seg_list, nseg, st);
-    else run_rtb<1, u32x4, 2>(L, chunk, per_seg, seg_list, nseg, st);
-    return true;
+    if (nob == 1 && v >= 44 && v <= 47) {
+      if (v == 44) run_rtb<1, u32x4, 1>(L, chunk, per_seg, seg_list, nseg, st);
+      else if (v == 45) run_rtb<1, u32x2, 2>(L, chunk, per_seg, seg_list, nseg, st);
+      else if (v == 46) run_rtb<1, u32x2, 1>(L, chunk, per_seg, seg_list, nseg, st);
+      else run_rtb<1, uint32_t, 4>(L, chunk, per_seg, seg_list, nseg, st);
+      return true;
+    }
+    if ((nob == 3 || nob == 4) && v >= 48) {
+      if (nob == 3 && v == 48) run_rtb<3, uint32_t, 8>(L, chunk, per_seg, seg_list, nseg, st);
+      else if (nob == 3) run_rtb<3, u32x2, 4>(L, chunk, per_seg, seg_list, nseg, st);
+      else if (v == 48) run_rtb<4, uint32_t, 8>(L, chunk, per_seg, seg_list, nseg, st);
+      else run_rtb<4, u32x2, 4>(L, chunk, per_seg, seg_list, nseg, st);
+      return true;
+    }
   }
 #else
   (void)variant;
 #endif
   switch (nob) {
-    case 1: run_rtb<1, u32x4, 1>(L, chunk, per_seg, seg_list, nseg, st); return true;
-    case 2: run_rtb<2, u32x4, 1>(L, chunk, per_seg, seg_list, nseg, st); return true;
+    // 8-byte columns, several in flight (profiles/r02/rtb_sweep.txt: one output u32x4 PF1 ->
+    // u32x2 PF4 0.199 -> 0.184 ms, four outputs PF4 -> PF8 0.296 -> 0.291)
+    case 1: run_rtb<1, u32x2, 4>(L, chunk, per_seg, seg_list, nseg, st); return true;
+    case 2: run_rtb<2, u32x2, 4>(L, chunk, per_seg, seg_list, nseg, st); return true;
     case 3: run_rtb<3, u32x2, 4>(L, chunk, per_seg, seg_list, nseg, st); return true;
-    case 4: run_rtb<4, u32x2, 4>(L, chunk, per_seg, seg_list, nseg, st); return true;
+    case 4: run_rtb<4, u32x2, 8>(L, chunk, per_seg, seg_list, nseg, st); return true;
   }
   return false;
 }

@@ -596,6 +596,29 @@ def test_runtime_kernels_agree(torch, cess, corc, k, m, ln, ne):
         enc.set_option(4, 0)
 
 
+@pytest.mark.parametrize("ne,ln", [(1, 4096 + 3), (2, (1 << 16) + 16), (3, 4096 + 3), (4, 999)])
+def test_rtb_tuning_shapes_agree(torch, cess, corc, ne, ln):
+    """The tuning build's k_rtb shapes (column width x columns in flight, variants 40-49)
+    rebuild RS(32,32) erasures bit-exact: vector body and byte tail."""
+    k, m, nseg = 32, 32, 3
+    rng = np.random.default_rng(77 + ne)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = np.ones((nseg, k + m), np.uint8)
+    for s in range(nseg):
+        present[s, rng.choice(k + m, size=ne, replace=False)] = 0
+    enc = cess.New(k, m, tuning=True)
+    enc.set_option(4, 3)
+    for v in [-1] + list(range(40, 50)):
+        enc.set_option(2, v)
+        d_data = to_dev(torch, data * present[:, :k, None])
+        d_par = to_dev(torch, want * present[:, k:, None])
+        enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_data.cpu().numpy(), data), v
+        assert np.array_equal(d_par.cpu().numpy(), want), v
+
+
 
 @pytest.mark.parametrize("k,m,ln", [(32, 32, 4096 + 4), (10, 4, 1000)])
 def test_decode_cache_eviction(torch, cess, corc, k, m, ln):
