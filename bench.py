@@ -10,6 +10,12 @@ Bytes counted per segment = (k+m) * F (k fragments read, m written; SURVEY.md §
     python bench.py [--gpus N --steps K --warmup W] [--config 1|2|3|4|5]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, weak scaling)
 
+`--gpus N` alone (no WORLD_SIZE in the environment) starts the N ranks itself: the process counts
+the visible GPUs without initialising HIP and runs torch.distributed.run as a child. Fewer GPUs
+than N, or WORLD_SIZE != N under an external launcher, exits with status 2 instead of measuring
+fewer GPUs than asked. Rehearsal on one GPU: CESS_DIST_BACKEND=gloo CESS_DEVICE=0 lets the ranks
+share device 0.
+
 Rank 0 prints one JSON line. `roofline` is the dominant kernel's algorithmic bytes per launch /
 its average launch time (HIP events on the launch stream); `cpu_baseline` times the C oracle
 (oracle/rs_oracle.c, kind "port": the reference ships no codec) on a bounded sample on rank 0.
@@ -318,6 +324,50 @@ def load_traffic(tag: str, algo_bytes: int, kernel: str):
     return t.get("bytes_per_launch")
 
 
+def traffic_source(tag: str) -> str:
+    return (f"profiles/traffic_{tag}.json (PMC FETCH_SIZE + WRITE_SIZE of the same launch, "
+            f"recorded by a rocprofv3 --pmc run of this bench; not measured in this run)")
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def world_check(gpus: int, env=os.environ, visible=None) -> tuple:
+    """What `--gpus N` means in this process: ("run", world) when the ranks already exist (under
+    torchrun WORLD_SIZE must equal N), ("launch", N) when this process must start N ranks itself,
+    ("error", message) otherwise. `visible` = GPUs this process could use (counted without
+    initialising HIP); ranks may share one GPU only in the rehearsal mode (CESS_DEVICE set)."""
+    if gpus < 1:
+        return "error", f"--gpus {gpus}: need at least one GPU"
+    if "WORLD_SIZE" in env:
+        ws = int(env["WORLD_SIZE"])
+        if ws != gpus:
+            return "error", (f"WORLD_SIZE={ws} but --gpus {gpus}: launch exactly --gpus ranks "
+                             f"(one per GPU)")
+        return "run", ws
+    if gpus == 1:
+        return "run", 1
+    if "CESS_DEVICE" not in env and (visible or 0) < gpus:
+        return "error", f"--gpus {gpus} but {visible or 0} GPU(s) visible"
+    return "launch", gpus
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start n rank processes (torch.distributed.run, one per GPU, rendezvous on 127.0.0.1) as a
+    child and wait for it. This process never initialises HIP: it only counted the devices."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+           str(n), "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -375,6 +425,17 @@ def main() -> None:
         return
 
     import torch
+    # --gpus N without an external launcher: start the N ranks here, before any HIP call
+    # (device_count does not initialise the GPU on this image)
+    what, val = world_check(args.gpus, os.environ,
+                            None if "WORLD_SIZE" in os.environ or args.gpus == 1
+                            else torch.cuda.device_count())
+    if what == "error":
+        print(f"bench.py: {val}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if what == "launch":
+        sys.exit(launch_ranks(val, sys.argv[1:]))
+
     import torch.distributed as dist
     import cess_amd
 
@@ -667,7 +728,9 @@ def main() -> None:
         "per_gpu_GBps": round(value / world, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": traffic, "launch_ms": round(launch_ms, 4),
+                     "traffic": traffic,
+                     "traffic_source": traffic_source(tag) if traffic is not None else None,
+                     "launch_ms": round(launch_ms, 4),
                      "algorithmic_bytes_per_launch": bytes_step_gpu},
     }
     if sha_note:

@@ -106,6 +106,17 @@ SIGNATURES = {
                                        c_size_t, LOCATE_FN, c_void_p, POINTER(c_void_p), c_void_p,
                                        POINTER(c_size_t)]),
     "cec_hash_from_shard_id": (c_int, [c_void_p, c_void_p]),
+    "cec_scale_upload_filler": (c_int, [c_void_p, POINTER(c_uint32), c_void_p, c_void_p, c_size_t,
+                                        c_void_p, c_size_t, POINTER(c_size_t)]),
+    "cec_scale_generate_restoral_order": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t,
+                                                  POINTER(c_size_t)]),
+    "cec_scale_claim_restoral_order": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(c_size_t)]),
+    "cec_scale_claim_restoral_exist_order": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p,
+                                                     c_size_t, POINTER(c_size_t)]),
+    "cec_scale_restoral_order_complete": (c_int, [c_void_p, c_void_p, c_size_t,
+                                                  POINTER(c_size_t)]),
+    "cec_audit_random_subject": (c_int, [c_void_p, c_uint32, c_void_p]),
+    "cec_audit_random_u64": (c_int, [c_void_p, c_size_t, POINTER(c_uint64)]),
 }
 
 CEC_OK = 0
@@ -122,6 +133,9 @@ CEC_ECALLBACK = -10
 CEC_CHUNK_COUNT = 1024
 CEC_SEGMENT_COUNT = 1000
 CEC_FRAGMENT_COUNT = 3
+CEC_UPLOAD_FILLER_LIMIT = 10
+CEC_FILLER_SIZE = 8 << 20
+CEC_AUDIT_PALLET_ID = b"rewardpt"
 
 CEC_OPT_FORCE_GENERIC = 1
 CEC_OPT_CT_VARIANT = 2
@@ -130,6 +144,7 @@ CEC_OPT_RT_MODE = 4
 CEC_OPT_DECODE_CACHE = 6
 CEC_STAT_DECODE_CACHED = 1
 CEC_STAT_RETIRED_PENDING = 2
+CEC_STAT_POOL_BYTES = 3
 CEC_HQOPT_TICK = 1
 CEC_DIST_ID_BYTES = 128
 CEC_DIST_SURVIVOR = 0

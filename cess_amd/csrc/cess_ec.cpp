@@ -68,6 +68,7 @@ class DevPool {
       return CEC_OK;
     }
     HIP_TRY(hipMalloc(out, (size_t)1 << c));
+    held_ += (size_t)1 << c;
     return CEC_OK;
   }
   // The last reference to a block was dropped; kernels enqueued so far may still read it.
@@ -123,10 +124,12 @@ class DevPool {
     for (auto& fl : free_)
       for (void* p : fl) (void)hipFree(p);
     free_.clear();
+    held_ = 0;
     for (hipEvent_t e : evpool_) (void)hipEventDestroy(e);
     evpool_.clear();
   }
   size_t pending() const { return dead_.size(); }
+  size_t held() const { return held_; }  // device bytes the pool has allocated (live + free)
 
  private:
   static int cls(size_t bytes) {
@@ -149,6 +152,19 @@ class DevPool {
   std::vector<hipEvent_t> evpool_;
   uint64_t seq_ = 0;   // marks recorded
   uint64_t done_ = 0;  // every mark <= done_ has completed
+  size_t held_ = 0;
+};
+
+// Batch-sized scratch (a verify's recomputed parity, an audit's gathered chunks) is not a pool
+// block: the pool rounds to powers of two and keeps blocks until the codec dies, so one verify of
+// ~94 GiB would pin 128 GiB of HBM to the codec. Above this size the scratch is stream-ordered
+// (hipMallocAsync / hipFreeAsync on the call's stream): exact size, returned once the stream
+// passes the launches that read it, no host wait.
+constexpr size_t kBigScratch = size_t(16) << 20;
+struct Scratch {
+  void* p = nullptr;
+  size_t bytes = 0;
+  bool async = false;
 };
 
 // A run-time program: chunks of up to kRtMaxOut outputs, each a device block in the layout of
@@ -367,9 +383,9 @@ struct cec_codec {
   }
   ~cec_codec() {
     (void)hipSetDevice(device);
-    // the encode program is never retired while the codec lives and batch encodes are not
-    // marked: let every queued launch finish before its blocks go
-    (void)hipDeviceSynchronize();
+    // no device-wide synchronisation: every launch that reads a pool block (a run-time encode
+    // or decode program, a plan's arrays, audit indices) is followed by a mark on its stream, and
+    // pool.drain() waits for those marks only; other codecs' streams keep running
     drop_plan();
     decode_cache.clear();
     lru.clear();
@@ -430,9 +446,32 @@ int check_launch() {
 int do_encode(cec_codec* c, const Layout& L, const uint32_t* seg_list, uint32_t nseg,
               hipStream_t st) {
   if (nseg == 0 || L.len == 0) return CEC_OK;
-  if (c->force_generic || !cec::launch_encode_ct(c->opts, c->k, c->m, L, seg_list, nseg, st))
+  if (c->force_generic || !cec::launch_encode_ct(c->opts, c->k, c->m, L, seg_list, nseg, st)) {
+    // the run-time program reads pool blocks (the encode program's chunks): mark the stream so
+    // the codec's destruction waits for this launch (compile-time kernels read none)
     run_program(c->opts, *c->encode, L, seg_list, nseg, st);
+    int rc = check_launch();
+    return rc ? rc : c->pool.mark(st);
+  }
   return check_launch();
+}
+
+int scratch_alloc(cec_codec* c, size_t bytes, hipStream_t st, Scratch* s) {
+  s->bytes = bytes;
+  if (bytes >= kBigScratch) {
+    s->async = true;
+    HIP_TRY(hipMallocAsync(&s->p, bytes, st));
+    return CEC_OK;
+  }
+  return c->pool.alloc(bytes, &s->p);
+}
+// after the launches reading the scratch are enqueued (and, for a pool block, marked)
+void scratch_release(cec_codec* c, const Scratch& s, hipStream_t st) {
+  if (!s.p) return;
+  if (s.async)
+    (void)hipFreeAsync(s.p, st);
+  else
+    c->pool.retire(s.p, s.bytes);
 }
 
 std::string pattern_key(const uint8_t* present, int n, bool data_only) {
@@ -877,6 +916,7 @@ int cec_get_stat(const cec_codec* c, int stat, uint64_t* value) {
   switch (stat) {
     case CEC_STAT_DECODE_CACHED: *value = c->decode_cache.size(); return CEC_OK;
     case CEC_STAT_RETIRED_PENDING: *value = c->pool.pending(); return CEC_OK;
+    case CEC_STAT_POOL_BYTES: *value = c->pool.held(); return CEC_OK;
   }
   return set_err(CEC_EINVAL, "unknown stat");
 }
@@ -998,9 +1038,10 @@ int cec_verify_batch(cec_codec* c, const uint8_t* d_data, const uint8_t* d_parit
   // the parity recomputed into a scratch batch (the encode kernels: FFT for RS(32,32)), then
   // compared segment by segment with the stored parity
   const size_t pbytes = nseg * (size_t)c->m * shard_len;
-  void* scratch = nullptr;
-  int rc = c->pool.alloc(pbytes, &scratch);
+  Scratch sc;
+  int rc = scratch_alloc(c, pbytes, st, &sc);
   if (rc) return rc;
+  void* scratch = sc.p;
   Layout L = batch_layout(c, d_data, static_cast<uint8_t*>(scratch), shard_len);
   hipError_t e = hipMemsetAsync(d_ok, 1, nseg, st);
   if (e == hipSuccess) {
@@ -1014,7 +1055,7 @@ int cec_verify_batch(cec_codec* c, const uint8_t* d_data, const uint8_t* d_parit
     rc = set_err(CEC_EHIP, std::string("verify: ") + hipGetErrorString(e));
   }
   const int mrc = c->pool.mark(st);  // the scratch stays until these launches complete
-  c->pool.retire(scratch, pbytes);
+  scratch_release(c, sc, st);
   return rc ? rc : mrc;
 }
 
@@ -1146,15 +1187,15 @@ int cec_audit_chunks(cec_codec* c, const uint8_t* d_data, const uint8_t* d_parit
     c->pool.retire(d_idx, idx_bytes);
     return set_err(CEC_EHIP, std::string("index upload: ") + hipGetErrorString(e));
   }
-  void* scratch = nullptr;
+  Scratch sc;
   const size_t gbytes = nfrag * nidx * chunk;
   if (!d_chunks) {
-    rc = c->pool.alloc(gbytes, &scratch);
+    rc = scratch_alloc(c, gbytes, st, &sc);
     if (rc) {
       c->pool.retire(d_idx, idx_bytes);
       return rc;
     }
-    d_chunks = static_cast<uint8_t*>(scratch);
+    d_chunks = static_cast<uint8_t*>(sc.p);
   }
   cec::launch_chunk_gather(L, nsh, nfrag, static_cast<const uint32_t*>(d_idx), nidx, chunk,
                            d_chunks, st);
@@ -1171,7 +1212,7 @@ int cec_audit_chunks(cec_codec* c, const uint8_t* d_data, const uint8_t* d_parit
   }
   const int mrc = c->pool.mark(st);  // the index array and scratch stay until these complete
   c->pool.retire(d_idx, idx_bytes);
-  if (scratch) c->pool.retire(scratch, gbytes);
+  scratch_release(c, sc, st);
   return rc ? rc : mrc;
 }
 

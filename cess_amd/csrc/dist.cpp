@@ -11,8 +11,9 @@
 // RCCL has no XOR reduction (rccl.h ncclRedOp_t), so survivors move by grouped point-to-point
 // send/recv; every rank issues the moves in the same (segment, fragment) order, which is what
 // pairs each send with its receive. Before any byte moves, the ranks agree (one 4-byte min
-// all-reduce) that every rank found its local survivors, so a caller error fails on all ranks
-// instead of leaving the others waiting in a receive.
+// all-reduce) that every rank found its local survivors and holds staging for the largest
+// round, and again before every round's transfers that each finished its local steps, so a
+// local error fails on all ranks instead of leaving the others waiting in a receive.
 //
 // RCCL is loaded at run time (dlopen): the rest of libcessec does not depend on it, and without
 // it the cec_dist_* entry points return CEC_ENCCL.
@@ -48,6 +49,7 @@ struct Rccl {
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;  // optional
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
@@ -81,6 +83,7 @@ const Rccl& rccl() {
     sym(r.group_end, "ncclGroupEnd");
     sym(r.error_string, "ncclGetErrorString");
     r.ok = all;
+    r.comm_abort = reinterpret_cast<decltype(&ncclCommAbort)>(dlsym(h, "ncclCommAbort"));
     if (!all) r.why = "librccl lacks an expected symbol";
   });
   return r;
@@ -162,6 +165,7 @@ struct cec_dist {
   uint8_t* pstage = nullptr;
   size_t pstage_bytes = 0;
   int* d_flag = nullptr;
+  bool broken = false;  // the communicator was aborted after a failure inside a transfer group
 };
 
 namespace {
@@ -330,64 +334,113 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
     ~Restore() { (void)hipSetDevice(dev); }
   } restore{prev};
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
-
-  // agree before any byte moves: min over ranks of `ok`
-  DI_TRY(hipMemcpyAsync(d->d_flag, &ok, sizeof(int), hipMemcpyHostToDevice, st));
-  NC_TRY(r.all_reduce(d->d_flag, d->d_flag, 1, ncclInt32, ncclMin, d->comm, st));
-  int all_ok = 0;
-  DI_TRY(hipMemcpyAsync(&all_ok, d->d_flag, sizeof(int), hipMemcpyDeviceToHost, st));
-  DI_TRY(hipStreamSynchronize(st));
-  if (!ok) return cec::set_error(CEC_EINVAL, "dist degraded read: " + why);
-  if (!all_ok)
-    return cec::set_error(CEC_EINVAL, "dist degraded read: another rank failed its checks");
+  if (d->broken) return cec::set_error(CEC_ENCCL, "dist degraded read: group aborted earlier");
 
   // Rounds of at most kRound segments of the plan (the same split on every rank) bound the
   // staging; rounds follow each other on the stream, so a round's receives land after the
   // previous round's rebuild has read the staging.
   constexpr size_t kRound = 256;
-  size_t rebuilt = 0, si = 0;
-  for (size_t r0 = 0; r0 < plan.size(); r0 += kRound) {
-    const size_t r1 = std::min(plan.size(), r0 + kRound);
+  struct Round {
     // survivor segments this rank rebuilds; partial segments it decodes or holds survivors of
     std::vector<const Seg*> mine, pmine;
     std::map<uint64_t, size_t> row, prow;
     size_t npairs = 0, H = 0;
     std::map<std::pair<uint64_t, int>, size_t> pair;  // (segment, lost fragment) -> acc row
+  };
+  auto classify = [&](size_t r0, size_t r1) {
+    Round R;
     for (size_t i = r0; i < r1; ++i) {
       const Seg& g = plan[i];
       if (!g.partial) {
         if (g.decoder == rank) {
-          row[g.seg] = mine.size();
-          mine.push_back(&g);
+          R.row[g.seg] = R.mine.size();
+          R.mine.push_back(&g);
         }
         continue;
       }
       const bool holder = std::binary_search(g.holders.begin(), g.holders.end(), rank);
       if (g.decoder != rank && !holder) continue;
-      prow[g.seg] = pmine.size();
-      pmine.push_back(&g);
+      R.prow[g.seg] = R.pmine.size();
+      R.pmine.push_back(&g);
       if (g.decoder == rank) {
-        H = std::max(H, g.holders.size());
-        for (int f : g.lost) pair[{g.seg, f}] = npairs++;
+        R.H = std::max(R.H, g.holders.size());
+        for (int f : g.lost) R.pair[{g.seg, f}] = R.npairs++;
       }
     }
-    rc = grow(&d->stage, &d->stage_bytes, mine.size() * (size_t)n * F, st);
-    if (rc) return rc;
+    return R;
+  };
+  // Staging for the largest round, allocated before the ranks agree: an allocation failure is
+  // then one rank's `ok = 0`, not a return while its peers wait in a receive.
+  if (ok) {
+    size_t need = 0, pneed = 0;
+    for (size_t r0 = 0; r0 < plan.size(); r0 += kRound) {
+      const Round R = classify(r0, std::min(plan.size(), r0 + kRound));
+      need = std::max(need, R.mine.size() * (size_t)n * F);
+      pneed = std::max(pneed, R.pmine.size() * (size_t)n * F + (R.H + 1) * R.npairs * F);
+    }
+    int grc = grow(&d->stage, &d->stage_bytes, need, st);
+    if (!grc) grc = grow(&d->pstage, &d->pstage_bytes, pneed, st);
+    if (grc) {
+      ok = 0;
+      why = std::string("staging allocation: ") + cec_last_error();
+    }
+  }
+
+  // min over ranks of a success flag; every rank calls it at the same points
+  auto agree = [&](int mine_ok, int* all_ok) -> int {
+    DI_TRY(hipMemcpyAsync(d->d_flag, &mine_ok, sizeof(int), hipMemcpyHostToDevice, st));
+    NC_TRY(r.all_reduce(d->d_flag, d->d_flag, 1, ncclInt32, ncclMin, d->comm, st));
+    DI_TRY(hipMemcpyAsync(all_ok, d->d_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    DI_TRY(hipStreamSynchronize(st));
+    return CEC_OK;
+  };
+  // agree before any byte moves
+  int all_ok = 0;
+  rc = agree(ok, &all_ok);
+  if (rc) return rc;
+  if (!ok) return cec::set_error(CEC_EINVAL, "dist degraded read: " + why);
+  if (!all_ok)
+    return cec::set_error(CEC_EINVAL, "dist degraded read: another rank failed its checks");
+
+  // A local failure after the agreement (a copy, the partial rebuild, the rebuild after a round)
+  // is held in `lrc` and the rank skips its remaining local work; the ranks agree again before
+  // every round's transfers, so all of them stop there together. An error inside a transfer group
+  // aborts the communicator (peers get an RCCL error instead of waiting for this rank).
+  int lrc = CEC_OK;
+  std::string lwhy;
+  auto local = [&](int code) {
+    if (code && !lrc) {
+      lrc = code;
+      lwhy = cec_last_error();
+    }
+    return code == CEC_OK;
+  };
+  auto hip_ok = [&](hipError_t e, const char* what) {
+    return local(e == hipSuccess ? CEC_OK
+                                 : cec::set_error(e == hipErrorOutOfMemory ? CEC_ENOMEM : CEC_EHIP,
+                                                  std::string(what) + ": " +
+                                                      hipGetErrorString(e)));
+  };
+  size_t rebuilt = 0, si = 0;
+  for (size_t r0 = 0; r0 < plan.size(); r0 += kRound) {
+    const size_t r1 = std::min(plan.size(), r0 + kRound);
+    Round R = classify(r0, r1);
+    auto& mine = R.mine;
+    auto& pmine = R.pmine;
+    const size_t npairs = R.npairs, H = R.H;
     const size_t pbatch = pmine.size() * (size_t)n * F, acc_row = npairs * F;
-    rc = grow(&d->pstage, &d->pstage_bytes, pbatch + (H + 1) * acc_row, st);
-    if (rc) return rc;
     uint8_t* const st_data = d->stage;
     uint8_t* const st_par = d->stage + mine.size() * (size_t)k * F;
     uint8_t* const p_data = d->pstage;
     uint8_t* const p_par = d->pstage + pmine.size() * (size_t)k * F;
     uint8_t* const acc = d->pstage + pbatch;
     auto slot = [&](uint64_t s, int f) {
-      return f < k ? st_data + (row.at(s) * (size_t)k + f) * F
-                   : st_par + (row.at(s) * (size_t)m + (f - k)) * F;
+      return f < k ? st_data + (R.row.at(s) * (size_t)k + f) * F
+                   : st_par + (R.row.at(s) * (size_t)m + (f - k)) * F;
     };
     auto pslot = [&](uint64_t s, int f) {
-      return f < k ? p_data + (prow.at(s) * (size_t)k + f) * F
-                   : p_par + (prow.at(s) * (size_t)m + (f - k)) * F;
+      return f < k ? p_data + (R.prow.at(s) * (size_t)k + f) * F
+                   : p_par + (R.prow.at(s) * (size_t)m + (f - k)) * F;
     };
     // local survivors into the survivor staging (decoder) or the partial batch (held), and
     // this rank's survivors of the round in plan order for the sends
@@ -395,40 +448,52 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
     std::vector<const uint8_t*> round_src;
     for (size_t i = r0; i < r1; ++i) {
       const Seg& g = plan[i];
-      const bool pm = g.partial && prow.count(g.seg);
+      const bool pm = g.partial && R.prow.count(g.seg);
       if (pm)  // every fragment not lost: the rebuild writes the lost ones only
         for (int f = 0; f < n; ++f)
-          ppres[prow[g.seg] * n + f] = !std::binary_search(g.lost.begin(), g.lost.end(), f);
+          ppres[R.prow[g.seg] * n + f] = !std::binary_search(g.lost.begin(), g.lost.end(), f);
       for (int f : g.surv) {
         if (owner(g.seg, f, world) != rank) continue;
         const uint8_t* p = src_ptr[si++];
         round_src.push_back(p);
+        if (lrc) continue;
         if (pm) {
-          pheld[prow[g.seg] * n + f] = 1;
-          DI_TRY(hipMemcpyAsync(pslot(g.seg, f), p, F, hipMemcpyDeviceToDevice, st));
+          pheld[R.prow[g.seg] * n + f] = 1;
+          hip_ok(hipMemcpyAsync(pslot(g.seg, f), p, F, hipMemcpyDeviceToDevice, st), "copy");
         } else if (!g.partial && g.decoder == rank) {
-          DI_TRY(hipMemcpyAsync(slot(g.seg, f), p, F, hipMemcpyDeviceToDevice, st));
+          hip_ok(hipMemcpyAsync(slot(g.seg, f), p, F, hipMemcpyDeviceToDevice, st), "copy");
         }
       }
     }
-    if (!pmine.empty()) {
-      rc = cec_reconstruct_partial_batch(d->codec, p_data, p_par, pmine.size(), F, ppres.data(),
-                                         pheld.data(), 0, st);
-      if (rc) return rc;
-      for (const auto& [key, i] : pair)
-        DI_TRY(hipMemcpyAsync(acc + i * F, pslot(key.first, key.second), F,
-                              hipMemcpyDeviceToDevice, st));
+    if (!pmine.empty() && !lrc &&
+        local(cec_reconstruct_partial_batch(d->codec, p_data, p_par, pmine.size(), F,
+                                            ppres.data(), pheld.data(), 0, st))) {
+      for (const auto& [key, i] : R.pair)
+        if (!hip_ok(hipMemcpyAsync(acc + i * F, pslot(key.first, key.second), F,
+                                   hipMemcpyDeviceToDevice, st), "copy"))
+          break;
       bool ragged = false;
       for (const Seg* g : pmine) ragged |= g->decoder == rank && g->holders.size() < H;
-      if (ragged) DI_TRY(hipMemsetAsync(acc + acc_row, 0, H * acc_row, st));
+      if (ragged && !lrc) hip_ok(hipMemsetAsync(acc + acc_row, 0, H * acc_row, st), "memset");
     }
+    // every rank reached this round's transfers with its local work in place
+    rc = agree(lrc == CEC_OK, &all_ok);
+    if (rc) return rc;
+    if (lrc) return cec::set_error(lrc, "dist degraded read: " + lwhy);
+    if (!all_ok)
+      return cec::set_error(CEC_EINVAL, "dist degraded read: another rank failed a local step");
     // one group: survivor moves, then partials, each in plan order (pairs every send with its
     // receive on the peer)
     NC_TRY(r.group_start());
     size_t rj = 0;
     auto fail = [&](ncclResult_t res, const char* what) {
-      r.group_end();
-      return nccl_err(res, what);
+      // a half-built group cannot be ended safely: abort the communicator so the peers' pending
+      // transfers fail instead of waiting for this rank
+      const int code = nccl_err(res, what);
+      if (r.comm_abort) r.comm_abort(d->comm);
+      d->comm = nullptr;
+      d->broken = true;
+      return code;
     };
     for (size_t i = r0; i < r1; ++i) {
       const Seg& g = plan[i];
@@ -450,7 +515,7 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
       if (g->decoder == rank) {
         for (size_t h = 0; h < g->holders.size(); ++h)
           for (int f : g->lost) {
-            ncclResult_t res = r.recv(acc + (h + 1) * acc_row + pair.at({g->seg, f}) * F, F,
+            ncclResult_t res = r.recv(acc + (h + 1) * acc_row + R.pair.at({g->seg, f}) * F, F,
                                       ncclUint8, g->holders[h], d->comm, st);
             if (res != ncclSuccess) return fail(res, "ncclRecv");
           }
@@ -461,7 +526,10 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
         }
       }
     }
-    NC_TRY(r.group_end());
+    {
+      ncclResult_t res = r.group_end();
+      if (res != ncclSuccess) return fail(res, "ncclGroupEnd");
+    }
     if (!mine.empty()) {
       // every fragment not lost is flagged present (the codec reads the first k, the gathered
       // survivors): the rebuild writes only the lost fragments, not the unused survivors
@@ -469,30 +537,30 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
       for (size_t i = 0; i < mine.size(); ++i)
         for (int f = 0; f < n; ++f)
           present[i * n + f] = !std::binary_search(mine[i]->lost.begin(), mine[i]->lost.end(), f);
-      rc = cec_reconstruct_batch(d->codec, st_data, st_par, mine.size(), F, present.data(), 1,
-                                 0, st);
-      if (rc) return rc;
-      for (const Seg* g : mine)
-        for (size_t i : entries[g->seg]) {
-          DI_TRY(hipMemcpyAsync(d_out[i], slot(g->seg, lost_frag[i]), F,
-                                hipMemcpyDeviceToDevice, st));
-          ++rebuilt;
-        }
-    }
-    if (npairs) {
-      if (H) {
-        rc = cec_xor_batch(acc, acc + acc_row, H, acc_row, acc_row, st);
-        if (rc) return rc;
-      }
-      for (const Seg* g : pmine)
-        if (g->decoder == rank)
+      if (local(cec_reconstruct_batch(d->codec, st_data, st_par, mine.size(), F, present.data(),
+                                      1, 0, st)))
+        for (const Seg* g : mine)
           for (size_t i : entries[g->seg]) {
-            DI_TRY(hipMemcpyAsync(d_out[i], acc + pair.at({g->seg, (int)lost_frag[i]}) * F, F,
-                                  hipMemcpyDeviceToDevice, st));
+            if (!hip_ok(hipMemcpyAsync(d_out[i], slot(g->seg, lost_frag[i]), F,
+                                       hipMemcpyDeviceToDevice, st), "copy"))
+              break;
             ++rebuilt;
           }
     }
+    if (npairs && !lrc) {
+      if (!H || local(cec_xor_batch(acc, acc + acc_row, H, acc_row, acc_row, st)))
+        for (const Seg* g : pmine)
+          if (g->decoder == rank)
+            for (size_t i : entries[g->seg]) {
+              if (!hip_ok(hipMemcpyAsync(d_out[i], acc + R.pair.at({g->seg, (int)lost_frag[i]}) * F,
+                                         F, hipMemcpyDeviceToDevice, st), "copy"))
+                break;
+              ++rebuilt;
+            }
+    }
   }
+  // a failure after the last round's transfers leaves no peer waiting
+  if (lrc) return cec::set_error(lrc, "dist degraded read: " + lwhy);
   DI_TRY(hipStreamSynchronize(st));
   if (nrebuilt) *nrebuilt = rebuilt;
   return CEC_OK;

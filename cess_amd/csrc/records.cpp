@@ -12,6 +12,17 @@
 //   FileBank = pallet index 60, upload_declaration = call index 0
 //                                                    runtime/src/lib.rs:1532, lib.rs:419
 //   from_shard_id: first 64 of 68 bytes               primitives/common/src/lib.rs:45-49
+//   upload_filler(tee_worker: AccountId, filler_list: Vec<FillerInfo>)   call_index(8)
+//                                                    lib.rs:795-833
+//   FillerInfo { block_num: u32, miner_address: AccountId, filler_hash: Hash }  types.rs:82-86
+//   UploadFillerLimit = 10                           runtime/src/lib.rs:1033
+//   generate_restoral_order(file_hash, restoral_fragment)            call_index(13) lib.rs:940-984
+//   claim_restoral_order(restoral_fragment)                          call_index(14) lib.rs:986-1014
+//   claim_restoral_exist_order(miner, file_hash, restoral_fragment)  call_index(15) lib.rs:1016-1070
+//   restoral_order_complete(fragment_hash)                           call_index(16) lib.rs:1072-1122
+//   Audit::random_number(seed): MyRandomness::random(&(MyPalletId, seed).encode()), then the
+//     output's first 8 bytes decoded as u64          c-pallets/audit/src/lib.rs:1067-1076
+//   audit MyPalletId = SegbkPalletId = PalletId(*b"rewardpt")   runtime/src/lib.rs:984,1004
 //
 // SCALE (parity-scale-codec): a fixed array [u8; N] is its N bytes; a Vec / BoundedVec is a
 // compact length then its items; a struct is its fields in order; AccountId32 is 32 bytes.
@@ -60,8 +71,11 @@ int deal_info(std::vector<uint8_t>& o, const uint8_t* seg_hex, const uint8_t* fr
   if (nseg > CEC_SEGMENT_COUNT)
     return cec::set_error(CEC_ESEGCOUNT, "deal_info holds at most SegmentCount = 1000 segments "
                                          "(16,000 MiB): split the file");
-  if (nfrag == 0 || nfrag > CEC_FRAGMENT_COUNT)
-    return cec::set_error(CEC_EINVAL, "fragment_list holds 1..FragmentCount = 3 hashes");
+  // check_file_spec (c-pallets/file-bank/src/functions.rs:4-11): every fragment_list holds
+  // exactly FragmentCount hashes, or upload_declaration fails with SpecError
+  if (nfrag != CEC_FRAGMENT_COUNT)
+    return cec::set_error(CEC_EINVAL, "fragment_list holds exactly FragmentCount = 3 hashes "
+                                      "(check_file_spec)");
   int rc = check_hex(seg_hex, nseg * 64);
   if (!rc) rc = check_hex(frag_hex, nseg * nfrag * 64);
   if (rc) return rc;
@@ -72,6 +86,25 @@ int deal_info(std::vector<uint8_t>& o, const uint8_t* seg_hex, const uint8_t* fr
     const uint8_t* f = frag_hex + s * nfrag * 64;
     o.insert(o.end(), f, f + nfrag * 64);
   }
+  return CEC_OK;
+}
+
+void put_u32(std::vector<uint8_t>& o, uint32_t v) {
+  for (int i = 0; i < 4; ++i) o.push_back((uint8_t)(v >> (8 * i)));
+}
+
+// a Hash argument: 64 lowercase hex bytes, no length prefix
+int put_hash(std::vector<uint8_t>& o, const uint8_t* hex) {
+  if (!hex) return cec::set_error(CEC_EINVAL, "null hash");
+  int rc = check_hex(hex, 64);
+  if (rc) return rc;
+  o.insert(o.end(), hex, hex + 64);
+  return CEC_OK;
+}
+
+int put_account(std::vector<uint8_t>& o, const uint8_t* acct) {
+  if (!acct) return cec::set_error(CEC_EINVAL, "null account");
+  o.insert(o.end(), acct, acct + 32);  // AccountId32: 32 bytes, no prefix
   return CEC_OK;
 }
 
@@ -128,6 +161,77 @@ int cec_scale_upload_declaration(const uint8_t* file_hash_hex, const uint8_t* se
   put_compact(o, (uint32_t)bucket_name_len);
   o.insert(o.end(), bucket_name, bucket_name + bucket_name_len);
   return emit(o, out, out_cap, out_len);
+}
+
+int cec_scale_upload_filler(const uint8_t* tee_worker, const uint32_t* block_num,
+                            const uint8_t* miners, const uint8_t* filler_hex, size_t n,
+                            uint8_t* out, size_t out_cap, size_t* out_len) {
+  if (n > CEC_UPLOAD_FILLER_LIMIT)
+    return cec::set_error(CEC_EINVAL, "filler_list holds at most UploadFillerLimit = 10 fillers "
+                                      "(LengthExceedsLimit)");
+  if (n && (!block_num || !miners || !filler_hex))
+    return cec::set_error(CEC_EINVAL, "null filler arrays");
+  std::vector<uint8_t> o;
+  o.push_back(CEC_FILEBANK_PALLET);
+  o.push_back(CEC_CALL_UPLOAD_FILLER);
+  int rc = put_account(o, tee_worker);
+  if (rc) return rc;
+  put_compact(o, (uint32_t)n);
+  for (size_t i = 0; i < n; ++i) {  // FillerInfo: block_num, miner_address, filler_hash
+    put_u32(o, block_num[i]);
+    put_account(o, miners + 32 * i);
+    if ((rc = put_hash(o, filler_hex + 64 * i))) return rc;
+  }
+  return emit(o, out, out_cap, out_len);
+}
+
+int cec_scale_generate_restoral_order(const uint8_t* file_hash_hex, const uint8_t* fragment_hex,
+                                      uint8_t* out, size_t out_cap, size_t* out_len) {
+  std::vector<uint8_t> o{CEC_FILEBANK_PALLET, CEC_CALL_GENERATE_RESTORAL_ORDER};
+  int rc = put_hash(o, file_hash_hex);
+  if (!rc) rc = put_hash(o, fragment_hex);
+  return rc ? rc : emit(o, out, out_cap, out_len);
+}
+
+int cec_scale_claim_restoral_order(const uint8_t* fragment_hex, uint8_t* out, size_t out_cap,
+                                   size_t* out_len) {
+  std::vector<uint8_t> o{CEC_FILEBANK_PALLET, CEC_CALL_CLAIM_RESTORAL_ORDER};
+  int rc = put_hash(o, fragment_hex);
+  return rc ? rc : emit(o, out, out_cap, out_len);
+}
+
+int cec_scale_claim_restoral_exist_order(const uint8_t* miner, const uint8_t* file_hash_hex,
+                                         const uint8_t* fragment_hex, uint8_t* out,
+                                         size_t out_cap, size_t* out_len) {
+  std::vector<uint8_t> o{CEC_FILEBANK_PALLET, CEC_CALL_CLAIM_RESTORAL_EXIST_ORDER};
+  int rc = put_account(o, miner);
+  if (!rc) rc = put_hash(o, file_hash_hex);
+  if (!rc) rc = put_hash(o, fragment_hex);
+  return rc ? rc : emit(o, out, out_cap, out_len);
+}
+
+int cec_scale_restoral_order_complete(const uint8_t* fragment_hex, uint8_t* out, size_t out_cap,
+                                      size_t* out_len) {
+  std::vector<uint8_t> o{CEC_FILEBANK_PALLET, CEC_CALL_RESTORAL_ORDER_COMPLETE};
+  int rc = put_hash(o, fragment_hex);
+  return rc ? rc : emit(o, out, out_cap, out_len);
+}
+
+int cec_audit_random_subject(const uint8_t* pallet_id, uint32_t seed, uint8_t* out12) {
+  if (!pallet_id || !out12) return cec::set_error(CEC_EINVAL, "null");
+  // SCALE of the tuple (PalletId, u32): PalletId([u8; 8]) is its 8 bytes, then u32 LE
+  std::memcpy(out12, pallet_id, 8);
+  for (int i = 0; i < 4; ++i) out12[8 + i] = (uint8_t)(seed >> (8 * i));
+  return CEC_OK;
+}
+
+int cec_audit_random_u64(const uint8_t* randomness, size_t len, uint64_t* out) {
+  if (!randomness || !out) return cec::set_error(CEC_EINVAL, "null");
+  if (len < 8) return cec::set_error(CEC_EINVAL, "u64 decode needs at least 8 bytes");
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; --i) v = v << 8 | randomness[i];
+  *out = v;
+  return CEC_OK;
 }
 
 int cec_shard_id(const uint8_t* hash_hex, uint32_t index, uint8_t* out68) {

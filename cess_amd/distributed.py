@@ -256,7 +256,14 @@ def partial_exchange(plan: GatherPlan, store: FragmentStore, enc, rank: int, gro
                 ops.append((True, slot(s, f), plan.decoder[s]))
     _p2p(ops, group, _staged(dev, group))
     if H and pairs:
-        xor(acc[0], acc[1], H, acc.stride(0), len(pairs) * F)
+        # on the current stream, after the received partials and before whoever reads acc[0]
+        # (torch side streams do not order against the null stream)
+        if dev.type == "cuda":
+            with torch.cuda.device(dev):
+                xor(acc[0], acc[1], H, acc.stride(0), len(pairs) * F,
+                    stream=torch.cuda.current_stream(dev))
+        else:
+            xor(acc[0], acc[1], H, acc.stride(0), len(pairs) * F)
     return {p: acc[0, i] for p, i in pidx.items()}
 
 

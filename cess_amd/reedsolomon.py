@@ -316,6 +316,8 @@ class Encoder:
         if out is None:
             out = torch.empty(max(1, nseg), dtype=torch.uint8,
                               device=torch.device("cuda", self.device))
+            if stream is None:  # read back below on torch's current stream: launch there too
+                stream = torch.cuda.current_stream(out.device)
         check(self._lib.cec_verify_batch(self._h, _dev_ptr(d_data), _dev_ptr(d_parity), nseg,
                                          shard_len, _dev_ptr(out), _stream_handle(stream)),
               "VerifyBatch")

@@ -7,10 +7,14 @@ Restoral flow on chain (reference c-pallets/file-bank/src/lib.rs):
     k surviving fragments of the same segment, and
   * `restoral_order_complete(fragment_hash)` (:1075-1122) marks it available again.
 The off-chain step is what this module does: rebuild one fragment and check that its SHA-256
-hex equals the `FragmentInfo.hash` recorded for it (types.rs:70-76) before reporting.
+hex equals the `FragmentInfo.hash` recorded for it (types.rs:70-76) before reporting. The report
+itself is the call data of `restoral_order_complete` (records.restoral_order_complete), emitted
+only for a fragment whose rebuilt hash matched.
 
-Idle fillers (`upload_filler`, lib.rs:798-833) are 8 MiB blocks whose content generator is not
-in the reference; here they are the splitmix64 counter stream of libcessec (parity unpinned).
+Idle fillers (`upload_filler`, lib.rs:795-833) are 8 MiB blocks whose content generator is not
+in the reference; here they are the splitmix64 counter stream of libcessec (content unpinned).
+Their on-chain record is pinned: `FillerInfo { block_num, miner_address, filler_hash }`
+(types.rs:82-86), at most UploadFillerLimit = 10 per `upload_filler` call (runtime/src/lib.rs:1033).
 """
 from __future__ import annotations
 
@@ -19,7 +23,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-from . import geometry
+from . import geometry, records
 from .reedsolomon import CecError, Encoder, ErrTooFewShards, sha256_hex_device
 
 
@@ -28,10 +32,14 @@ class ErrFragmentHashMismatch(CecError, ValueError):
 
 
 def repair_fragment(enc: Encoder, survivors: Dict[int, np.ndarray], index: int,
-                    expected_hash: Optional[bytes] = None) -> np.ndarray:
+                    expected_hash: Optional[bytes] = None, complete_call: bool = False):
     """Rebuild fragment `index` of one segment from `survivors` ({fragment index: bytes}, at
     least k of them) on the GPU. With `expected_hash` (64 hex chars), raise
-    ErrFragmentHashMismatch unless SHA-256(rebuilt) equals it."""
+    ErrFragmentHashMismatch unless SHA-256(rebuilt) equals it. With `complete_call` (needs
+    `expected_hash`) return (fragment, restoral_order_complete call data): the call exists only
+    for a fragment that passed the check."""
+    if complete_call and expected_hash is None:
+        raise ValueError("complete_call needs the recorded fragment hash")
     n = enc.Shards
     if not 0 <= index < n:
         raise ValueError("fragment index out of range")
@@ -51,6 +59,8 @@ def repair_fragment(enc: Encoder, survivors: Dict[int, np.ndarray], index: int,
         if got != bytes(expected_hash):
             raise ErrFragmentHashMismatch(f"fragment {index}: {got.decode()} != "
                                           f"{bytes(expected_hash).decode()}")
+    if complete_call:
+        return out, records.restoral_order_complete(bytes(expected_hash))
     return out
 
 
@@ -64,19 +74,23 @@ AUTO_GPU_CHECK_FRAGMENTS = 128
 
 def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, present,
                  expected: Optional[Sequence[Dict[int, bytes]]] = None, stream=None,
-                 hash_on: str = "auto", hash_threads: int = 16):
+                 hash_on: str = "auto", hash_threads: int = 16, complete_calls: bool = False):
     """Rebuild every missing fragment of an HBM-resident batch in place (one launch for all
     erasure patterns) and, with `expected` ([{fragment index: recorded hash}] per segment),
     return per-segment booleans: rebuilt fragments hash to the recorded values. hash_on "gpu":
     all of them hashed in one GPU launch, one chain per fragment, where they were rebuilt;
     "host": copied out once and hashed by `hash_threads` host threads (OpenSSL via hashlib);
     "auto": the host below AUTO_GPU_CHECK_FRAGMENTS fragments (a chain is serial, so a few
-    chains run faster on host cores), the GPU from there."""
+    chains run faster on host cores), the GPU from there. With `complete_calls`, return
+    (ok, calls): calls = {(segment, fragment index): restoral_order_complete call data} for
+    exactly the fragments whose rebuilt hash equals the recorded one."""
     import torch
     if hash_on not in ("gpu", "host", "auto"):
         raise ValueError("hash_on must be 'gpu', 'host' or 'auto'")
     enc.ReconstructBatch(d_data, d_parity, nseg, shard_len, present, stream=stream)
     if expected is None:
+        if complete_calls:
+            raise ValueError("complete_calls needs the recorded hashes (expected)")
         return None
     if stream is None:
         torch.cuda.current_stream(d_data.device).synchronize()
@@ -97,9 +111,12 @@ def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, pres
         with cf.ThreadPoolExecutor(max(1, hash_threads)) as ex:  # hashlib drops the GIL
             got = list(ex.map(lambda a: hashlib.sha256(a).hexdigest().encode(), host))
     ok = [True] * nseg
-    for (s, _, h), g in zip(which, got):
+    calls = {}
+    for (s, i, h), g in zip(which, got):
         ok[s] &= g == h
-    return ok
+        if complete_calls and g == h:
+            calls[(s, i)] = records.restoral_order_complete(h)
+    return (ok, calls) if complete_calls else ok
 
 
 def generate_fillers(n: int, seed: int = 0xF111E5, filler_size: int = geometry.FRAGMENT_SIZE,
@@ -115,3 +132,19 @@ def generate_fillers(n: int, seed: int = 0xF111E5, filler_size: int = geometry.F
     torch.cuda.synchronize(device)
     hashes = sha256_hex_device([d[i].data_ptr() for i in range(n)], filler_size) if n else []
     return d, hashes
+
+
+def filler_records(hashes: Sequence[bytes], miner: bytes, block_num: int):
+    """FillerInfo records (types.rs:82-86) of fillers with these SHA-256 hex hashes."""
+    return [records.FillerInfo(block_num, bytes(miner), bytes(h)) for h in hashes]
+
+
+def generate_filler_upload(n: int, miner: bytes, tee_worker: bytes, block_num: int,
+                           seed: int = 0xF111E5, first: int = 0, device: int = 0):
+    """n 8 MiB idle fillers generated and hashed on the GPU, with their on-chain records: returns
+    (device tensor [n][8 MiB], hashes, [FillerInfo], [upload_filler call data]) — one call per
+    UploadFillerLimit = 10 fillers (c-pallets/file-bank/src/lib.rs:795-833)."""
+    d, hashes = generate_fillers(n, seed=seed, filler_size=records.FILLER_SIZE, first=first,
+                                 device=device)
+    fillers = filler_records(hashes, miner, block_num)
+    return d, hashes, fillers, records.upload_filler_calls(tee_worker, fillers)

@@ -22,7 +22,8 @@
  * Conventions: GF(2^8), polynomial 0x11D, systematic Vandermonde matrix.
  * Shard i < k is data, i >= k parity. All functions return 0 or a negative CEC_E* code; no
  * exceptions cross the ABI. A codec is bound to one device and is not re-entrant; distinct
- * codecs are independent. Caller owns every shard / segment / hash buffer.
+ * codecs are independent (cec_destroy waits only for the codec's own queued launches, never for
+ * the device). Caller owns every shard / segment / hash buffer.
  */
 #ifndef CESS_EC_H
 #define CESS_EC_H
@@ -103,7 +104,8 @@ int cec_reconstruct_partial_batch(cec_codec* codec, uint8_t* d_data, uint8_t* d_
 int cec_verify_batch(cec_codec* codec, const uint8_t* d_data, const uint8_t* d_parity,
                      size_t nseg, size_t shard_len, uint8_t* d_ok, void* hip_stream);
 /* GF(2^8) addition of device buffers: d_dst[0..len) ^= d_src[j*src_stride ..][0..len) for
- * j < nsrc (src_stride >= len when nsrc > 1). Enqueued on hip_stream. */
+ * j < nsrc (src_stride >= len when nsrc > 1). Enqueued on hip_stream, which must belong to the
+ * device holding the buffers (no codec: the caller's current device and stream decide). */
 int cec_xor_batch(uint8_t* d_dst, const uint8_t* d_src, size_t nsrc, size_t src_stride,
                   size_t len, void* hip_stream);
 /* SHA-256 of every shard of every segment in the batch layout, as 64 lowercase hex chars:
@@ -315,7 +317,8 @@ int cec_scale_compact(uint32_t n, uint8_t* out, size_t out_cap, size_t* out_len)
 /* deal_info = compact(nseg) ++ per segment: hash ++ compact(nfrag) ++ nfrag hashes.
  * seg_hex: nseg * 64 bytes; frag_hex: nseg * nfrag * 64 (fragment index order).
  * CEC_ESEGCOUNT if nseg > CEC_SEGMENT_COUNT (the extrinsic would be rejected: split the file);
- * CEC_EINVAL if nfrag is 0 or > CEC_FRAGMENT_COUNT or a hash is not lowercase hex. */
+ * CEC_EINVAL if nfrag != CEC_FRAGMENT_COUNT (check_file_spec, c-pallets/file-bank/src/
+ * functions.rs:4-11, rejects any other count with SpecError) or a hash is not lowercase hex. */
 int cec_scale_deal_info(const uint8_t* seg_hex, const uint8_t* frag_hex, size_t nseg,
                         size_t nfrag, uint8_t* out, size_t out_cap, size_t* out_len);
 /* Call data of upload_declaration: pallet index, call index, file_hash, deal_info, user_brief
@@ -326,6 +329,46 @@ int cec_scale_upload_declaration(const uint8_t* file_hash_hex, const uint8_t* se
                                  size_t file_name_len, const uint8_t* bucket_name,
                                  size_t bucket_name_len, uint8_t* out, size_t out_cap,
                                  size_t* out_len);
+/* Idle fillers: FileBank::upload_filler(tee_worker: AccountId, filler_list: Vec<FillerInfo>),
+ * call_index(8) (c-pallets/file-bank/src/lib.rs:795-833); FillerInfo { block_num: u32,
+ * miner_address: AccountId, filler_hash: Hash } (types.rs:82-86); at most UploadFillerLimit = 10
+ * fillers per call (runtime/src/lib.rs:1033), each 8 MiB of idle space (lib.rs:821-825).
+ * Call data for n fillers: block_num[n], miners n * 32 bytes, filler_hex n * 64 hex chars.
+ * CEC_EINVAL past the limit (the chain's LengthExceedsLimit). */
+#define CEC_CALL_UPLOAD_FILLER 8
+#define CEC_UPLOAD_FILLER_LIMIT 10
+#define CEC_FILLER_SIZE (8u << 20)
+int cec_scale_upload_filler(const uint8_t* tee_worker, const uint32_t* block_num,
+                            const uint8_t* miners, const uint8_t* filler_hex, size_t n,
+                            uint8_t* out, size_t out_cap, size_t* out_len);
+/* Restoral (repair) calls, c-pallets/file-bank/src/lib.rs:940-1122: a miner that lost a fragment
+ * opens an order (13), another claims it (14; 15 for the fragments of an exiting miner,
+ * RestoralTarget), rebuilds the fragment off chain and reports it (16). Hashes are 64 hex chars,
+ * the miner an AccountId32. A repair service emits 16 only for a fragment whose rebuilt SHA-256
+ * equals the recorded fragment hash. */
+#define CEC_CALL_GENERATE_RESTORAL_ORDER 13
+#define CEC_CALL_CLAIM_RESTORAL_ORDER 14
+#define CEC_CALL_CLAIM_RESTORAL_EXIST_ORDER 15
+#define CEC_CALL_RESTORAL_ORDER_COMPLETE 16
+int cec_scale_generate_restoral_order(const uint8_t* file_hash_hex, const uint8_t* fragment_hex,
+                                      uint8_t* out, size_t out_cap, size_t* out_len);
+int cec_scale_claim_restoral_order(const uint8_t* fragment_hex, uint8_t* out, size_t out_cap,
+                                   size_t* out_len);
+int cec_scale_claim_restoral_exist_order(const uint8_t* miner, const uint8_t* file_hash_hex,
+                                         const uint8_t* fragment_hex, uint8_t* out,
+                                         size_t out_cap, size_t* out_len);
+int cec_scale_restoral_order_complete(const uint8_t* fragment_hex, uint8_t* out, size_t out_cap,
+                                      size_t* out_len);
+/* Audit randomness inputs (c-pallets/audit/src/lib.rs:1067-1076): random_number(seed) asks the
+ * chain's randomness for the subject (MyPalletId, seed).encode() = the 8 PalletId bytes ++ seed as
+ * u32 LE (12 bytes; the audit pallet's id is SegbkPalletId = b"rewardpt", runtime/src/lib.rs:
+ * 984,1004), and decodes the output's first 8 bytes as a little-endian u64. The randomness itself
+ * (pallet_rrsc::ParentBlockRandomness) is chain state: a host holding it reproduces the inputs of
+ * cec_challenge_indices with these two. */
+#define CEC_AUDIT_PALLET_ID "rewardpt"
+int cec_audit_random_subject(const uint8_t* pallet_id /* 8 bytes */, uint32_t seed,
+                             uint8_t* out12);
+int cec_audit_random_u64(const uint8_t* randomness, size_t len, uint64_t* out);
 /* 68-byte shard id = 64 hex chars ++ "-NNN" (index 0..999), the form Hash::from_shard_id reads
  * back (primitives/common/src/lib.rs:45-49; c-pallets/audit/src/tests.rs:267-269 builds
  * file_hash ++ "-001"). */
@@ -354,6 +397,9 @@ int cec_set_option(cec_codec* codec, int option, int value);
 #define CEC_STAT_DECODE_CACHED 1   /* erasure patterns in the decode cache */
 #define CEC_STAT_RETIRED_PENDING 2 /* device blocks retired but possibly still read by queued
                                       kernels (released once those complete) */
+#define CEC_STAT_POOL_BYTES 3      /* HBM held by the codec's block pool (programs, plans, small
+                                      scratch); batch-sized scratch is stream-ordered and is not
+                                      held after the call's launches complete */
 int cec_get_stat(const cec_codec* codec, int stat, uint64_t* value);
 
 #ifdef __cplusplus

@@ -40,6 +40,7 @@ int cec_reconstruct_partial_batch(cec_codec*, uint8_t*, uint8_t*, size_t, size_t
   return CEC_EINVAL;
 }
 int cec_xor_batch(uint8_t*, const uint8_t*, size_t, size_t, size_t, void*) { return CEC_EINVAL; }
+const char* cec_last_error(void) { return ""; }
 }
 
 static int fails = 0;

@@ -531,6 +531,68 @@ def test_repair_batch_wide(torch, cess, corc, orc):
         repair_batch(enc, dd, dp, nseg, F, present, expected, hash_on="tpu")
 
 
+def test_repair_emits_completion_only_for_matching_hash(torch, cess, corc, orc):
+    """The repair service reports a rebuilt fragment with restoral_order_complete(fragment_hash)
+    (call 16, c-pallets/file-bank/src/lib.rs:1072-1122) only when its SHA-256 matched the
+    recorded hash: a segment whose rebuild does not match yields no completion call."""
+    from cess_amd import records
+    from cess_amd.repair import ErrFragmentHashMismatch, repair_batch, repair_fragment
+    k, m, F, nseg = 2, 1, 1 << 16, 6
+    rng = np.random.default_rng(8)
+    data = rng.integers(0, 256, (nseg, k, F), dtype=np.uint8)
+    par = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = np.ones((nseg, k + m), np.uint8)
+    expected = []
+    for s in range(nseg):
+        present[s, s % 3] = 0
+        i = s % 3
+        expected.append({i: orc.sha256_hex(data[s, i] if i < k else par[s, i - k])})
+    dd = to_dev(torch, data * present[:, :k, None])
+    dp = to_dev(torch, par * present[:, k:, None])
+    dp_corrupt = dp.clone()
+    enc = cess.New(k, m)
+    # segment 4 lost data fragment 1; its surviving parity is corrupted -> rebuilt bytes differ
+    dp_corrupt[4, 0, 100] ^= 0x40
+    for hash_on in ("gpu", "host"):
+        ok, calls = repair_batch(enc, dd.clone(), dp.clone(), nseg, F, present, expected,
+                                 hash_on=hash_on, complete_calls=True)
+        assert ok == [True] * nseg
+        assert calls == {(s, s % 3): records.restoral_order_complete(expected[s][s % 3])
+                         for s in range(nseg)}
+        ok, calls = repair_batch(enc, dd.clone(), dp_corrupt.clone(), nseg, F, present,
+                                 expected, hash_on=hash_on, complete_calls=True)
+        assert ok == [s != 4 for s in range(nseg)], hash_on
+        assert (4, 1) not in calls and len(calls) == nseg - 1
+        assert all(c == bytes([60, 16]) + expected[s][i] for (s, i), c in calls.items())
+    full = [data[0, 0], data[0, 1], par[0, 0]]
+    frag, call = repair_fragment(enc, {1: full[1], 2: full[2]}, 0, expected[0][0],
+                                 complete_call=True)
+    assert np.array_equal(frag, full[0]) and call == records.restoral_order_complete(expected[0][0])
+    bad = full[2].copy()
+    bad[0] ^= 1
+    with pytest.raises(ErrFragmentHashMismatch):  # no call data on a mismatch
+        repair_fragment(enc, {1: full[1], 2: bad}, 0, expected[0][0], complete_call=True)
+
+
+def test_filler_upload_records(torch, orc):
+    """Idle fillers with their on-chain records: FillerInfo { block_num, miner_address,
+    filler_hash } (types.rs:82-86) from the GPU filler hashes, UploadFillerLimit = 10 per
+    upload_filler call (lib.rs:795-833, runtime/src/lib.rs:1033)."""
+    import struct
+    from cess_amd import records
+    from cess_amd.repair import generate_filler_upload
+    miner, tee = bytes(range(32)), bytes(range(100, 132))
+    d, hashes, fillers, calls = generate_filler_upload(12, miner, tee, block_num=77, first=3)
+    assert d.shape == (12, 8 << 20) and len(calls) == 2
+    for i in (0, 11):
+        want = orc.synthetic_segment(0xF111E5, 3 + i, 8 << 20)
+        assert hashes[i] == orc.sha256_hex(want)
+    assert [f.filler_hash for f in fillers] == hashes
+    assert calls[0] == bytes([60, 8]) + tee + bytes([10 << 2]) + b"".join(
+        struct.pack("<I", 77) + miner + h for h in hashes[:10])
+    assert calls[1] == records.upload_filler(tee, fillers[10:])
+
+
 def test_generate_fillers(torch, orc):
     from cess_amd.repair import generate_fillers
     d, hashes = generate_fillers(3, filler_size=1 << 16, first=7)
@@ -753,10 +815,13 @@ def test_codecs_on_threads_are_independent(torch, cess, corc):
     bit-exact against the C oracle."""
     import concurrent.futures as cf
     cases = [(2, 1, 4096 + 16, 0, 4096), (10, 4, 4099, 1, 2), (32, 32, 8192, 0, 3),
-             (4, 2, 1000, 2, 1)]
+             (4, 2, 1000, 2, 1), (10, 4, 4096, 0, 4)]
 
     def work(case):
         k, m, ln, rt_mode, cap = case
+        # the last case destroys and recreates its codec every iteration while the others run:
+        # cec_destroy waits for its own launches only (no device-wide synchronisation)
+        churn = case is cases[-1]
         n = k + m
         rng = np.random.default_rng(k * 31 + m)
         nseg = 6
@@ -770,6 +835,11 @@ def test_codecs_on_threads_are_independent(torch, cess, corc):
             d_data = torch.from_numpy(data).cuda()
             d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
         for it in range(12):
+            if churn and it:
+                enc.close()
+                enc = cess.New(k, m)
+                enc.set_option(4, rt_mode)
+                enc.set_option(6, cap)
             enc.EncodeBatch(d_data, d_par, nseg, ln, stream=st)
             st.synchronize()
             if not np.array_equal(d_par.cpu().numpy(), want):
@@ -785,6 +855,15 @@ def test_codecs_on_threads_are_independent(torch, cess, corc):
             if not (np.array_equal(d_data.cpu().numpy(), data)
                     and np.array_equal(d_par.cpu().numpy(), want)):
                 return (case, it, "reconstruct")
+            if churn:  # destroy right behind queued launches, then check what they wrote
+                enc.EncodeBatch(d_data, d_par, nseg, ln, stream=st)
+                enc.ReconstructBatch(d_data, d_par, nseg, ln, present, stream=st)
+                enc.close()
+                st.synchronize()
+                if not np.array_equal(d_par.cpu().numpy(), want):
+                    return (case, it, "destroy behind launches")
+                enc = cess.New(k, m)
+        enc.close()
         return None
 
     with cf.ThreadPoolExecutor(len(cases)) as ex:
@@ -823,6 +902,33 @@ def test_all_parity_lost_is_reencoded(torch, cess, corc, k, m, ln):
     torch.cuda.synchronize()
     assert np.array_equal(d_data.cpu().numpy(), data)
     assert np.array_equal(d_par.cpu().numpy(), par)
+
+
+def test_large_verify_scratch_not_retained(torch, cess, corc):
+    """Batch-sized scratch (a generic code's recomputed parity) is stream-ordered, not a pool
+    block: after a 128 MiB-scratch verify completes, the codec holds no more HBM than before
+    (the pool rounds to powers of two and keeps its blocks until the codec dies)."""
+    k, m, ln, nseg = 10, 4, 4 << 20, 8
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, (2, k, ln), dtype=np.uint8)
+    par = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(2)])
+    d_data = to_dev(torch, np.concatenate([data] * (nseg // 2)))
+    d_par = to_dev(torch, np.concatenate([par] * (nseg // 2)))
+    enc = cess.New(k, m)
+    before = enc.stat(3)
+    d_par[5, 3, 17] ^= 1
+    ok = enc.VerifyBatch(d_data, d_par, nseg, ln)
+    assert list(ok) == [s != 5 for s in range(nseg)]
+    torch.cuda.synchronize()
+    after = enc.stat(3)
+    assert after - before < (16 << 20), (before, after)
+    # the audit gather's scratch as well (hash only: the gathered chunks are scratch)
+    from cess_amd import audit
+    d_hex = torch.empty((nseg * (k + m), 512, 64), dtype=torch.uint8, device="cuda")
+    audit.audit_chunks(enc, d_data, d_par, nseg, ln, list(range(0, 1024, 2)), d_hex=d_hex)
+    torch.cuda.synchronize()
+    assert enc.stat(3) - before < (16 << 20)
+    enc.close()
 
 
 @pytest.mark.parametrize("k,m,ln,nseg", [(2, 1, 1 << 16, 9), (2, 1, 4099, 5), (4, 2, 1000, 7),

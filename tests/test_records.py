@@ -97,3 +97,83 @@ def test_shard_id_round_trip():
     import cess_amd
     with pytest.raises(cess_amd.CecError):
         records.shard_id(fh, 1000)
+
+
+def test_deal_info_requires_exactly_fragment_count():
+    """check_file_spec (c-pallets/file-bank/src/functions.rs:4-11) rejects any fragment_list whose
+    length is not FragmentCount = 3: such call data would always fail with SpecError."""
+    import cess_amd
+    for nfrag in (1, 2, 4):
+        with pytest.raises(cess_amd.CecError):
+            records.deal_info(seglists(2, nfrag=nfrag))
+    assert records.deal_info(seglists(2, nfrag=3)) == hand_deal_info(seglists(2, nfrag=3))
+
+
+def acct(i):
+    return bytes((i * 7 + j) & 0xFF for j in range(32))
+
+
+def test_upload_filler_call_data():
+    """FileBank::upload_filler(tee_worker: AccountId, filler_list: Vec<FillerInfo>), call_index(8)
+    (c-pallets/file-bank/src/lib.rs:795-833); FillerInfo { block_num: u32, miner_address:
+    AccountId, filler_hash: Hash } (types.rs:82-86), SCALE: u32 LE ++ 32 bytes ++ 64 bytes."""
+    tee = acct(9)
+    fl = [records.FillerInfo(1000 + i, acct(i), hx("filler", i)) for i in range(10)]
+    got = records.upload_filler(tee, fl)
+    want = bytes([60, 8]) + tee + compact(10) + b"".join(
+        struct.pack("<I", f.block_num) + f.miner_address + f.filler_hash for f in fl)
+    assert got == want
+    assert len(got) == 2 + 32 + 1 + 10 * (4 + 32 + 64)
+    assert records.upload_filler(tee, []) == bytes([60, 8]) + tee + compact(0)
+    import cess_amd
+    with pytest.raises(cess_amd.CecError):  # UploadFillerLimit = 10 (runtime/src/lib.rs:1033)
+        records.upload_filler(tee, fl + fl[:1])
+    calls = records.upload_filler_calls(tee, fl * 2 + fl[:3])
+    assert [c[34] for c in calls] == [compact(10)[0], compact(10)[0], compact(3)[0]]
+    assert calls[0] == got
+    bad = [records.FillerInfo(1, acct(1), b"Z" * 64)]
+    with pytest.raises(cess_amd.CecError):
+        records.upload_filler(tee, bad)
+
+
+def test_restoral_call_data():
+    """The restoral calls of c-pallets/file-bank/src/lib.rs:940-1122 (pallet 60): Hash arguments
+    are 64 bytes, AccountId 32, in declaration order."""
+    fh, fr, miner = hx("file", 3), hx("frag", 7), acct(5)
+    assert records.generate_restoral_order(fh, fr) == bytes([60, 13]) + fh + fr
+    assert records.claim_restoral_order(fr) == bytes([60, 14]) + fr
+    assert records.claim_restoral_exist_order(miner, fh, fr) == bytes([60, 15]) + miner + fh + fr
+    assert records.restoral_order_complete(fr) == bytes([60, 16]) + fr
+    import cess_amd
+    with pytest.raises(cess_amd.CecError):
+        records.restoral_order_complete(b"A" * 64)
+
+
+def test_audit_random_subject():
+    """Audit::random_number(seed) (c-pallets/audit/src/lib.rs:1067-1076) hands the chain's
+    randomness (T::MyPalletId::get(), seed).encode(): PalletId([u8; 8]) then u32 LE; the audit
+    pallet's MyPalletId is SegbkPalletId = PalletId(*b"rewardpt") (runtime/src/lib.rs:984,1004).
+    The output's first 8 bytes decode as u64 LE."""
+    assert records.AUDIT_PALLET_ID == b"rewardpt"
+    for seed in (0, 1, 47, 20220509, 0xFFFFFFFF):
+        assert records.audit_random_subject(seed) == b"rewardpt" + struct.pack("<I", seed)
+    assert records.audit_random_subject(5, b"py/trsry") == b"py/trsry" + struct.pack("<I", 5)
+    r = bytes(range(32))
+    assert records.audit_random_u64(r) == struct.unpack("<Q", r[:8])[0]
+    import cess_amd
+    with pytest.raises(cess_amd.CecError):
+        records.audit_random_u64(b"1234567")
+    # the challenge chain: randomness per seed -> u64 -> cec_challenge_indices (blake2b stands
+    # in for the chain randomness, which is chain state and not reproducible offline)
+    from cess_amd import audit
+    rnd = [hashlib.blake2b(records.audit_random_subject(s), digest_size=32).digest()
+           for s in range(1, 200)]
+    idx, used = audit.challenge_indices([records.audit_random_u64(x) for x in rnd])
+    want = []
+    for x in rnd:
+        i = struct.unpack("<Q", x[:8])[0] % 1024
+        if i not in want:
+            want.append(i)
+        if len(want) == 47:
+            break
+    assert list(idx) == want and used == 48

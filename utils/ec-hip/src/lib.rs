@@ -159,6 +159,24 @@ pub mod sys {
                                             out_cap: usize, out_len: *mut usize) -> c_int;
         pub fn cec_shard_id(hash_hex: *const u8, index: u32, out68: *mut u8) -> c_int;
         pub fn cec_hash_from_shard_id(shard_id68: *const u8, hash_hex_out: *mut u8) -> c_int;
+        pub fn cec_scale_upload_filler(tee_worker: *const u8, block_num: *const u32,
+                                       miners: *const u8, filler_hex: *const u8, n: usize,
+                                       out: *mut u8, out_cap: usize, out_len: *mut usize)
+                                       -> c_int;
+        pub fn cec_scale_generate_restoral_order(file_hash_hex: *const u8,
+                                                 fragment_hex: *const u8, out: *mut u8,
+                                                 out_cap: usize, out_len: *mut usize) -> c_int;
+        pub fn cec_scale_claim_restoral_order(fragment_hex: *const u8, out: *mut u8,
+                                              out_cap: usize, out_len: *mut usize) -> c_int;
+        pub fn cec_scale_claim_restoral_exist_order(miner: *const u8, file_hash_hex: *const u8,
+                                                    fragment_hex: *const u8, out: *mut u8,
+                                                    out_cap: usize, out_len: *mut usize)
+                                                    -> c_int;
+        pub fn cec_scale_restoral_order_complete(fragment_hex: *const u8, out: *mut u8,
+                                                 out_cap: usize, out_len: *mut usize) -> c_int;
+        pub fn cec_audit_random_subject(pallet_id: *const u8, seed: u32, out12: *mut u8)
+                                        -> c_int;
+        pub fn cec_audit_random_u64(randomness: *const u8, len: usize, out: *mut u64) -> c_int;
         pub fn cec_fill_synthetic(d_out: *mut u8, seg_bytes: usize, nseg: usize, seg0: u64,
                                   seed: u64, stream: *mut c_void) -> c_int;
         pub fn cec_set_option(c: *mut cec_codec, option: c_int, value: c_int) -> c_int;
@@ -465,4 +483,43 @@ pub fn deal_info(segments: &[SegmentList]) -> Result<Vec<u8>, Error> {
     check(unsafe { cec_scale_deal_info(seg.as_ptr(), frag.as_ptr(), segments.len(), nfrag,
                                        out.as_mut_ptr(), len, &mut len) })?;
     Ok(out)
+}
+
+/// Size-query-then-fill of a libcessec SCALE encoder (`f(out, cap, &mut len)`).
+fn scale_call(f: impl Fn(*mut u8, usize, *mut usize) -> c_int) -> Result<Vec<u8>, Error> {
+    let mut len = 0usize;
+    check(f(std::ptr::null_mut(), 0, &mut len))?;
+    let mut out = vec![0u8; len];
+    check(f(out.as_mut_ptr(), len, &mut len))?;
+    Ok(out)
+}
+
+/// `FillerInfo` of c-pallets/file-bank/src/types.rs:82-86.
+#[derive(Clone, Debug)]
+pub struct FillerInfo {
+    pub block_num: u32,
+    pub miner_address: [u8; 32],
+    pub filler_hash: [u8; 64],
+}
+
+/// Call data of `upload_filler(tee_worker, filler_list)` (call 8, at most 10 fillers).
+pub fn upload_filler(tee_worker: &[u8; 32], fillers: &[FillerInfo]) -> Result<Vec<u8>, Error> {
+    let blk: Vec<u32> = fillers.iter().map(|f| f.block_num).collect();
+    let miners: Vec<u8> = fillers.iter().flat_map(|f| f.miner_address).collect();
+    let hex: Vec<u8> = fillers.iter().flat_map(|f| f.filler_hash).collect();
+    scale_call(|o, c, l| unsafe {
+        sys::cec_scale_upload_filler(tee_worker.as_ptr(), blk.as_ptr(), miners.as_ptr(),
+                                     hex.as_ptr(), fillers.len(), o, c, l)
+    })
+}
+
+/// Call data of `restoral_order_complete(fragment_hash)` (call 16): emit it only after the
+/// rebuilt fragment's SHA-256 hex equals `fragment_hash`.
+pub fn restoral_order_complete(fragment_hash: &[u8; 64]) -> Result<Vec<u8>, Error> {
+    scale_call(|o, c, l| unsafe { sys::cec_scale_restoral_order_complete(fragment_hash.as_ptr(), o, c, l) })
+}
+
+/// Call data of `claim_restoral_order(restoral_fragment)` (call 14).
+pub fn claim_restoral_order(fragment_hash: &[u8; 64]) -> Result<Vec<u8>, Error> {
+    scale_call(|o, c, l| unsafe { sys::cec_scale_claim_restoral_order(fragment_hash.as_ptr(), o, c, l) })
 }
