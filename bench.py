@@ -397,6 +397,9 @@ def main() -> None:
                     help="run-time kernel: 0 Horner over input groups, index-mode XORs (k <= 32), "
                          "1 per-bit masks, 2 Horner with v_mov table reads, 3 bit-plane "
                          "accumulators (<= 4 outputs)")
+    ap.add_argument("--fftdec-min", type=int, default=-1,
+                    help="RS(32,32) rebuilds of at least this many shards run the FFT-domain "
+                         "decoder (CEC_OPT_FFTDEC_MIN; 0 = never; -1 = library default)")
     ap.add_argument("--erasures", type=int, default=0,
                     help="config 6: random erasures per segment (default m)")
     ap.add_argument("--lose-parity", action="store_true",
@@ -478,6 +481,9 @@ def main() -> None:
         enc.set_option(2, args.variant)
     enc.set_option(3, args.sha_mode)
     enc.set_option(4, args.rt_mode)
+    if args.fftdec_min >= 0:
+        enc.set_option(7, args.fftdec_min)
+    fftdec_min = args.fftdec_min if args.fftdec_min >= 0 else 5
     enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)  # valid parity for config 3
 
     present = None
@@ -701,7 +707,8 @@ def main() -> None:
     tag = f"c{args.config}"
     kernel_name = {2: "k_ct<EncCT<2, 1>>", 3: "k_ct_dec1_mixed21 (Dec1CT<2, 1, e> / EncCT<2, 1> per segment)",
                    4: "k_ct<EncCT<2, 1>>", 5: "k_fft3232<true, true>",
-                   6: "k_rthx<8>" if (args.erasures or m) > 4 else "k_rtb",
+                   6: ("k_fftdec_m" if 0 < fftdec_min <= (args.erasures or m)
+                       else "k_rthx<8>" if (args.erasures or m) > 4 else "k_rtb"),
                    7: "k_rtb<1>", 8: "k_rtb<4>"}[args.config]
     if args.generic:
         kernel_name = "k_rthx" if k <= 32 else "k_rt"

@@ -142,6 +142,7 @@ CEC_OPT_CT_VARIANT = 2
 CEC_OPT_SHA_MODE = 3
 CEC_OPT_RT_MODE = 4
 CEC_OPT_DECODE_CACHE = 6
+CEC_OPT_FFTDEC_MIN = 7
 CEC_STAT_DECODE_CACHED = 1
 CEC_STAT_RETIRED_PENDING = 2
 CEC_STAT_POOL_BYTES = 3

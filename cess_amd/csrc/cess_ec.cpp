@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/cess_ec.h"
+#include "fftdec_plan.h"
 #include "gf256.h"
 #include "kernels.h"
 
@@ -180,6 +181,10 @@ struct Program {
   int nout = 0;     // total outputs
   int single = -1;  // the one missing shard when exactly one output (compile-time decode)
   bool partial = false;  // rows restricted to held survivors (cec_reconstruct_partial_batch)
+  // RS(32,32): the same rebuild as an FFT-domain decode plan (fftdec_plan.h), a pool block
+  uint32_t* fd = nullptr;
+  size_t fd_bytes = 0;
+  int fd_side = 0;
   uint8_t in_idx[cec::kMaxShards] = {};   // survivors read (host copy)
   uint8_t out_idx[cec::kMaxShards] = {};  // shards written (host copy)
 };
@@ -236,10 +241,12 @@ class PinnedArena {
 using HostImages = PinnedArena;
 int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int nin,
                   const uint8_t* out_idx, int nout, const BigMat& coef, ProgPtr* out,
-                  bool partial = false, HostImages* keep = nullptr) {
+                  bool partial = false, HostImages* keep = nullptr,
+                  const cec::FftDecPlan* fdp = nullptr) {
   DevPool* pp = &pool;
   std::shared_ptr<Program> prog(new Program, [pp](Program* p) {
     for (auto& c : p->chunks) pp->retire(c.dev, c.bytes);
+    pp->retire(p->fd, p->fd_bytes);
     delete p;
   });
   prog->nout = nout;
@@ -306,6 +313,24 @@ int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int 
     prog->chunks.push_back(c);
     HIP_TRY(hipMemcpyAsync(c.dev, h, c.bytes, hipMemcpyHostToDevice, upload));
   }
+  if (fdp) {  // the FFT-domain decode plan of the same pattern
+    const size_t bytes = fdp->w.size() * sizeof(uint32_t);
+    uint32_t* h = keep ? keep->take(bytes) : nullptr;
+    if (!h) {
+      hosts.emplace_back(fdp->w);
+      h = hosts.back().data();
+      staged = false;
+    } else {
+      std::memcpy(h, fdp->w.data(), bytes);
+    }
+    void* d = nullptr;
+    int rc = pool.alloc(bytes, &d);
+    if (rc) return rc;
+    prog->fd = static_cast<uint32_t*>(d);
+    prog->fd_bytes = bytes;
+    prog->fd_side = fdp->side;
+    HIP_TRY(hipMemcpyAsync(prog->fd, h, bytes, hipMemcpyHostToDevice, upload));
+  }
   // the block may be a reused one whose readers have completed; the upload must land before
   // any caller-stream launch that reads it, and pageable images die here (arena images live
   // until the caller's synchronisation)
@@ -335,6 +360,11 @@ struct PsPlan {
   std::vector<std::pair<ProgPtr, std::pair<size_t, size_t>>> ct;
   std::vector<PsLaunch> rt;
   size_t mixed_off = 0, mixed_count = 0;  // tagged list (segment | erased << 30), count 0: none
+  struct FdLaunch {
+    int side;
+    size_t off, count;  // segments list + per-segment FFT-domain plans (pointer array)
+  };
+  std::vector<FdLaunch> fd;
 };
 
 constexpr size_t kDefaultDecodeCache = 4096;
@@ -347,6 +377,8 @@ struct cec_codec {
   hipStream_t stream = nullptr;  // private: uploads and the host-buffer API
   KernelOpts opts;
   bool force_generic = false;
+  // RS(32,32) patterns with at least this many outputs take the FFT-domain decoder (0: never)
+  int fftdec_min = 5;
   DevPool pool;  // declared before every holder of pool blocks: destroyed after them
   ProgPtr encode;
   // decode programs by erasure pattern (n presence flags + data_only), least recently used last
@@ -510,8 +542,13 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* ou
     return set_err(CEC_ETOOFEW, "fewer than k shards present");
   ProgPtr prog;
   if (plan->nout > 0) {
+    // RS(32,32) rebuilds of several shards: also the FFT-domain plan (picked at launch by the
+    // codec's CEC_OPT_FFTDEC_MIN and the layout)
+    cec::FftDecPlan fdp;
+    const bool fd = c->k == 32 && c->m == 32 && plan->nout >= 2 &&
+                    cec::fftdec_plan_m(flags, data_only, &fdp);
     int rc = build_program(c->pool, c->stream, plan->in_idx, c->k, plan->out_idx, plan->nout,
-                           plan->coef, &prog, false, keep);
+                           plan->coef, &prog, false, keep, fd ? &fdp : nullptr);
     if (rc) return rc;
   } else {
     prog = std::make_shared<const Program>();
@@ -593,11 +630,18 @@ bool is_reencode(const cec_codec* c, const Program& p) {
   return true;
 }
 
+bool use_fftdec(const cec_codec* c, const Program& p) {
+  return !c->force_generic && p.fd && c->fftdec_min > 0 && p.nout >= c->fftdec_min;
+}
+
 int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* seg_list,
               uint32_t nseg, hipStream_t st) {
   if (p.nout == 0 || nseg == 0 || L.len == 0) return CEC_OK;
   if (!c->force_generic && p.single < 0 && is_reencode(c, p))
     return do_encode(c, L, seg_list, nseg, st);
+  if (use_fftdec(c, p) &&
+      cec::launch_fftdec(L, p.fd_side, p.fd, nullptr, seg_list, nseg, st))
+    return check_launch();
   if (c->force_generic || p.single < 0 ||
       !cec::launch_decode_ct(c->opts, c->k, c->m, p.single, L, seg_list, nseg, st))
     run_program(c->opts, p, L, seg_list, nseg, st);
@@ -635,7 +679,7 @@ Layout stage_layout(cec_codec* c, size_t len) {
 // partial: pkey holds 2n flags per segment (present, then held) and the programs are partial
 // (cec_reconstruct_partial_batch).
 int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_only,
-                  std::unique_ptr<PsPlan>* out, bool partial = false) {
+                  std::unique_ptr<PsPlan>* out, bool partial = false, bool fdok = false) {
   const int n = c->k + c->m;
   const int per = partial ? 2 * n : n;
   auto plan = std::make_unique<PsPlan>();
@@ -653,7 +697,7 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
     groups[it->second].second.push_back((uint32_t)s);
   }
   bool all_ct = !c->force_generic;
-  std::vector<std::pair<ProgPtr, const std::vector<uint32_t>*>> progs, reencode;
+  std::vector<std::pair<ProgPtr, const std::vector<uint32_t>*>> progs, reencode, fdg[2];
   // new patterns' program uploads stay in flight until the one synchronisation below (one per
   // plan, not per pattern: 64 new RS(32,32) patterns cost ~1 ms of waits otherwise); every return
   // path waits for them before their host images go
@@ -679,6 +723,10 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
       reencode.push_back({p, &g.second});  // the encode kernels, whatever the other groups take
       continue;
     }
+    if (fdok && use_fftdec(c, *p)) {  // RS(32,32) wide rebuilds: the FFT-domain decoder
+      fdg[p->fd_side].push_back({p, &g.second});
+      continue;
+    }
     progs.push_back({p, &g.second});
     if (p->single < 0 || !cec::has_decode_ct(c->k, c->m, p->single)) all_ct = false;
   }
@@ -691,6 +739,17 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
   // the run-time launches index the segment list and the chunk-pointer array with one offset:
   // keep them aligned past the re-encode lists
   hp.resize(hl.size(), nullptr);
+  for (int side = 0; side < 2; ++side) {
+    if (fdg[side].empty()) continue;
+    PsPlan::FdLaunch f{side, hl.size(), 0};
+    for (auto& pr : fdg[side])
+      for (uint32_t sg : *pr.second) {
+        hl.push_back(sg);
+        hp.push_back(pr.first->fd);
+        ++f.count;
+      }
+    plan->fd.push_back(f);
+  }
   if (all_ct) {
     std::vector<uint32_t> tagged;
     for (auto& pr : progs) {
@@ -774,6 +833,13 @@ int launch_ps_plan(cec_codec* c, const PsPlan& p, const Layout& L, hipStream_t s
     if (rc) return rc;
   }
   const uint32_t* const* ptrs = static_cast<const uint32_t* const*>(p.ptrs);
+  for (const auto& f : p.fd) {
+    if (!cec::launch_fftdec(L, f.side, nullptr, ptrs + f.off, p.list + f.off, (uint32_t)f.count,
+                            st))
+      return set_err(CEC_EINVAL, "FFT-domain decode plan on a layout it does not fit");
+    int rc = check_launch();
+    if (rc) return rc;
+  }
   for (const auto& l : p.rt) {
     launch_chunk(c->opts, L, nullptr, ptrs + l.off, l.nin, l.nob, p.list + l.off,
                  (uint32_t)l.count, st);
@@ -902,6 +968,10 @@ int cec_set_option(cec_codec* c, int option, int value) {
       if (value < 0 || value > 3) return set_err(CEC_EINVAL, "rt mode out of range");
       c->opts.rt_mode = value;
       return CEC_OK;
+    case CEC_OPT_FFTDEC_MIN:
+      if (value < 0 || value > 64) return set_err(CEC_EINVAL, "fftdec min outputs in 0..64");
+      c->fftdec_min = value;
+      return CEC_OK;
     case CEC_OPT_DECODE_CACHE:
       if (value < 1) return set_err(CEC_EINVAL, "decode cache capacity must be >= 1");
       c->cache_cap = (size_t)value;
@@ -960,9 +1030,12 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
     for (auto& ch : pkey) ch = ch ? 1 : 0;
     pkey.push_back(data_only ? 1 : 0);
     pkey.push_back(c->force_generic ? 1 : 0);
+    const bool fdok = cec::fftdec_layout_ok(L);
+    pkey.push_back(fdok ? 1 : 0);
+    pkey.push_back((char)c->fftdec_min);
     if (!c->ps || c->ps->key != pkey) {
       std::unique_ptr<PsPlan> plan;
-      rc = build_ps_plan(c, pkey, nseg, data_only != 0, &plan);
+      rc = build_ps_plan(c, pkey, nseg, data_only != 0, &plan, false, fdok);
       if (rc) return rc;
       c->drop_plan();  // the old plan's arrays are retired: launches already enqueued keep them
       c->ps = std::move(plan);

@@ -1,0 +1,177 @@
+// Host-side plans of the RS(32,32) erasure decoder on the additive FFT (fftdec.hip). Host only,
+// header-inlined so the CPU model test (tests/native/fftdec_model.cpp) builds the same plans.
+//
+// The code (gf256.h): data shard t = f(t), parity shard t = f(32 ^ t) for the unique f of degree
+// < 32. The plan takes one coset as A (its present shards are read, its erased shards zeroed)
+// and the other as B:
+//   T1   q = FFT_B(IFFT_A(A values, erased zeroed)): the polynomial f_q agreeing with f on A's
+//        present points and vanishing on A's erased set D, evaluated on B;
+//   h    = f - f_q has degree < 32 and vanishes on A \ D, so it is fixed by its values u on D, and
+//        its values on B are linear in u: h(x) = sum_{c in D} u_c l_c(x), l_c the Lagrange basis
+//        of the coset A. At d = |D| present points R of B the syndromes s = p_R ^ q_R = h(R) give
+//        u = inv(L[R][D]) s (any d points of B work: the code is MDS);
+//   out  erased c in D: u_c; erased e in B: q_e ^ h(e) = q_e ^ L[e][D] inv(L[R][D]) s.
+// Mode M (matvec) applies those rows to the syndromes as bit-plane masks in the kernel: cost
+// (outputs) x (slots holding R), so the plan takes A = the coset with fewer erasures and packs R
+// into as few lane-pair slots (positions 2j, 2j + 1) as the present shards allow.
+#pragma once
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "gf256.h"
+
+namespace cec {
+
+// Word layout of a decode plan in HBM (uint32 words).
+struct FftDecLayout {
+  static constexpr int kFlags = 0;   // bit 0: side (0: A = data coset, 1: A = parity coset);
+                                     // bits 8..15: mode (0 = M)
+  static constexpr int kPresA = 1;   // bit t: shard t of coset A is read (present)
+  static constexpr int kR = 2;       // bit t: shard t of coset B is a syndrome row (read)
+  static constexpr int kEB = 3;      // bit t: shard t of coset B is erased
+  static constexpr int kDA = 4;      // bit t: shard t of coset A is erased
+  static constexpr int kNout = 5;    // outputs written
+  static constexpr int kRslots = 6;  // bit j: slot j (positions 2j, 2j + 1 of B) holds R rows
+  static constexpr int kPslots = 7;  // bit j: slot j is packed (R or an erased B output)
+  static constexpr int kOuts = 8;    // [32]: output o = t | (on B) << 5
+  static constexpr int kMasks = 64;  // [nout][popcount(rslots)][8 q][8 p]
+  static size_t words(int nout, int nrslots) { return kMasks + (size_t)nout * nrslots * 64; }
+};
+
+struct FftDecPlan {
+  std::vector<uint32_t> w;  // the device image
+  int side = 0, nout = 0, nrslots = 0;
+};
+
+namespace fdp {
+
+inline int popc(uint32_t x) { return __builtin_popcount(x); }
+
+// l_c(x) for the Lagrange basis of the coset {base ^ t}: prod_{a != c} (x ^ a) / (c ^ a)
+inline uint8_t lagrange(unsigned base, unsigned c, unsigned x) {
+  uint8_t num = 1, den = 1;
+  for (unsigned t = 0; t < 32; ++t) {
+    const unsigned a = base ^ t;
+    if (a == c) continue;
+    num = gf_mul(num, (uint8_t)(x ^ a));
+    den = gf_mul(den, (uint8_t)(c ^ a));
+  }
+  return gf_mul(num, gf_inv(den));
+}
+
+}  // namespace fdp
+
+// Build the mode-M plan for RS(32,32) erasure pattern `present` (64 flags, shards 0..31 data,
+// 32..63 parity); data_only drops parity outputs. Returns false when the pattern has more than
+// 32 erasures (the caller reports ETOOFEW) or nothing to write.
+inline bool fftdec_plan_m(const uint8_t* present, bool data_only, FftDecPlan* out) {
+  uint32_t erd = 0, erp = 0;  // erased data / parity
+  for (int t = 0; t < 32; ++t) {
+    if (!present[t]) erd |= 1u << t;
+    if (!present[32 + t]) erp |= 1u << t;
+  }
+  const int nd = fdp::popc(erd), np = fdp::popc(erp);
+  if (nd + np > 32 || nd + np == 0) return false;
+  // A = the coset with fewer erasures (fewer syndrome rows); data on a tie
+  const int side = np < nd ? 1 : 0;
+  const unsigned baseA = side ? 32u : 0u, baseB = side ? 0u : 32u;
+  const uint32_t DA = side ? erp : erd, EB = side ? erd : erp;
+  const int d = fdp::popc(DA);
+  // R: d present points of B packed into few slots: whole present slots first, then a lone
+  // present position of a slot that is packed anyway (it holds an erased output), then any
+  uint32_t R = 0;
+  int need = d;
+  for (int j = 0; j < 16 && need >= 2; ++j)
+    if (!(EB >> (2 * j) & 3)) {
+      R |= 3u << (2 * j);
+      need -= 2;
+    }
+  for (int pass = 0; pass < 2 && need > 0; ++pass)
+    for (int t = 0; t < 32 && need > 0; ++t) {
+      if ((EB >> t & 1) || (R >> t & 1)) continue;
+      const bool packed = (EB >> (t ^ 1) & 1) || (R >> (t ^ 1) & 1);
+      if (pass == 0 && !packed) continue;
+      R |= 1u << t;
+      --need;
+    }
+  if (need) return false;  // cannot happen with <= 32 erasures
+  uint32_t rslots = 0, pslots = 0;
+  for (int j = 0; j < 16; ++j) {
+    if (R >> (2 * j) & 3) rslots |= 1u << j;
+    if ((R | EB) >> (2 * j) & 3) pslots |= 1u << j;
+  }
+  // outputs: erased data always; erased parity unless data_only
+  std::vector<uint32_t> outs;
+  for (int t = 0; t < 32; ++t) {
+    if (DA >> t & 1 && !(data_only && side == 1)) outs.push_back((uint32_t)t);
+    if (EB >> t & 1 && !(data_only && side == 0)) outs.push_back((uint32_t)t | 32u);
+  }
+  if (outs.empty()) return false;
+  // u = inv(L[R][D]) s;  h(e) = L[e][D] u
+  std::vector<unsigned> Dl, Rl;
+  for (int t = 0; t < 32; ++t) {
+    if (DA >> t & 1) Dl.push_back(baseA ^ (unsigned)t);
+    if (R >> t & 1) Rl.push_back(baseB ^ (unsigned)t);
+  }
+  using M64 = Mat<32, 32>;
+  using W64 = Mat<32, 64>;
+  M64 lr, linv;
+  W64 work;
+  for (int r = 0; r < d; ++r)
+    for (int c = 0; c < d; ++c) lr.v[r][c] = fdp::lagrange(baseA, Dl[c], Rl[r]);
+  if (d && !gf_invert(lr, d, linv, work)) return false;  // cannot happen (MDS)
+  const int nrs = fdp::popc(rslots);
+  FftDecPlan p;
+  p.side = side;
+  p.nout = (int)outs.size();
+  p.nrslots = nrs;
+  p.w.assign(FftDecLayout::words(p.nout, nrs), 0u);
+  uint32_t* w = p.w.data();
+  w[FftDecLayout::kFlags] = (uint32_t)side;
+  w[FftDecLayout::kPresA] = ~DA;
+  w[FftDecLayout::kR] = R;
+  w[FftDecLayout::kEB] = EB;
+  w[FftDecLayout::kDA] = DA;
+  w[FftDecLayout::kNout] = (uint32_t)p.nout;
+  w[FftDecLayout::kRslots] = rslots;
+  w[FftDecLayout::kPslots] = pslots;
+  // syndrome index of each R position (column of the rows below)
+  int ridx[32];
+  for (int i = 0, t = 0; t < 32; ++t) ridx[t] = (R >> t & 1) ? i++ : -1;
+  for (int o = 0; o < p.nout; ++o) {
+    const uint32_t od = outs[o];
+    w[FftDecLayout::kOuts + o] = od;
+    const unsigned t = od & 31;
+    uint8_t row[32] = {};  // coefficients over the syndromes
+    if (!(od & 32)) {      // an erased point of A: row of inv(L[R][D])
+      const int di = (int)(std::find(Dl.begin(), Dl.end(), baseA ^ t) - Dl.begin());
+      for (int r = 0; r < d; ++r) row[r] = linv.v[di][r];
+    } else {  // an erased point of B: L[e][D] inv(L[R][D])
+      const unsigned e = baseB ^ t;
+      for (int c = 0; c < d; ++c) {
+        const uint8_t le = fdp::lagrange(baseA, Dl[c], e);
+        if (!le) continue;
+        for (int r = 0; r < d; ++r) row[r] ^= gf_mul(le, linv.v[c][r]);
+      }
+    }
+    uint32_t* mk = w + FftDecLayout::kMasks + (size_t)o * nrs * 64;
+    for (int j = 0; j < 16; ++j) {
+      if (!(rslots >> j & 1)) continue;
+      const int lo = ridx[2 * j], hi = ridx[2 * j + 1];
+      const BitMatrix ml = gf_bitmatrix(lo >= 0 ? row[lo] : 0);
+      const BitMatrix mh = gf_bitmatrix(hi >= 0 ? row[hi] : 0);
+      for (int q = 0; q < 8; ++q)
+        for (int pp = 0; pp < 8; ++pp)
+          mk[q * 8 + pp] = ((ml.row[q] >> pp & 1) ? 0x0F0F0F0Fu : 0u) |
+                           ((mh.row[q] >> pp & 1) ? 0xF0F0F0F0u : 0u);
+      mk += 64;
+    }
+  }
+  *out = std::move(p);
+  return true;
+}
+
+}  // namespace cec

@@ -392,6 +392,8 @@ int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t s
                                    the per-bit mask kernel, 2 = Horner with v_mov table reads */
 #define CEC_OPT_DECODE_CACHE 6  /* capacity (>= 1) of the decode-program LRU cache, one entry
                                    per erasure pattern (default 4096) */
+#define CEC_OPT_FFTDEC_MIN 7    /* RS(32,32): rebuilds of at least this many shards per segment
+                                   run the FFT-domain erasure decoder (0 = never; default 5) */
 int cec_set_option(cec_codec* codec, int option, int value);
 /* Counters (tests / monitoring). */
 #define CEC_STAT_DECODE_CACHED 1   /* erasure patterns in the decode cache */

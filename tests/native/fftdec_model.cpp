@@ -1,0 +1,139 @@
+// CPU model of the RS(32,32) FFT-domain erasure decoder (cess_amd/csrc/fftdec.hip) on the plans
+// the library builds (cess_amd/csrc/fftdec_plan.h): per byte column, T1 (IFFT over coset A with
+// its erased shards zeroed, FFT onto coset B), the syndromes at the plan's R rows, and every output
+// from the plan's bit-plane masks exactly as the kernel applies them (low / high nibble = the
+// slot's even / odd position). Compared with the codeword of the product's own encode matrix for
+// random erasure patterns of 1..32 shards, both sides, with and without data_only.
+// Build: g++ -std=c++20 -O1 -fconstexpr-ops-limit=2000000000 fftdec_model.cpp
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../../cess_amd/csrc/fftdec_plan.h"
+
+using namespace cec;
+
+static void ifft(uint8_t* v, unsigned beta) {
+  const LchSkews<5> S = lch_skews<5>((uint8_t)beta);
+  for (int i = 0; i < 5; ++i) {
+    const int h = 1 << i;
+    for (int b0 = 0; b0 < 32; b0 += 2 * h)
+      for (int t = b0; t < b0 + h; ++t) {
+        v[t + h] ^= v[t];
+        v[t] ^= gf_mul(S.s[i][b0 >> (i + 1)], v[t + h]);
+      }
+  }
+}
+static void fft(uint8_t* v, unsigned beta) {
+  const LchSkews<5> S = lch_skews<5>((uint8_t)beta);
+  for (int i = 4; i >= 0; --i) {
+    const int h = 1 << i;
+    for (int b0 = 0; b0 < 32; b0 += 2 * h)
+      for (int t = b0; t < b0 + h; ++t) {
+        v[t] ^= gf_mul(S.s[i][b0 >> (i + 1)], v[t + h]);
+        v[t + h] ^= v[t];
+      }
+  }
+}
+// x -> the byte the kernel's masks produce for one nibble half (0: low, 1: high)
+static uint8_t apply_masks(const uint32_t* mk, uint8_t x, int half) {
+  const uint32_t sel = half ? 0xF0F0F0F0u : 0x0F0F0F0Fu;
+  uint8_t r = 0;
+  for (int q = 0; q < 8; ++q) {
+    int bit = 0;
+    for (int p = 0; p < 8; ++p) bit ^= ((mk[q * 8 + p] & sel) == sel) & (x >> p & 1);
+    r |= (uint8_t)(bit << q);
+  }
+  return r;
+}
+
+int main() {
+  using Big = Mat<64, 64>;
+  using BigW = Mat<64, 128>;
+  static Big E, top, topinv;
+  static BigW work;
+  if (!gf_encode_matrix(32, 32, E, top, topinv, work)) return 2;
+  std::mt19937_64 rng(12345);
+  int fails = 0, cases = 0;
+  for (int trial = 0; trial < 600; ++trial) {
+    const int e = trial < 64 ? 1 + trial % 32 : 1 + (int)(rng() % 32);
+    uint8_t present[64];
+    for (int i = 0; i < 64; ++i) present[i] = 1;
+    int left = e;
+    while (left) {
+      const int i = (int)(rng() % 64);
+      if (present[i]) {
+        present[i] = 0;
+        --left;
+      }
+    }
+    if (trial % 7 == 3)  // a structured pattern: the first e shards of one coset
+      for (int i = 0; i < 64; ++i) present[i] = !(i >= (trial & 32) && i < (trial & 32) + e);
+    const bool data_only = trial % 3 == 1;
+    FftDecPlan p;
+    bool any_out = false;
+    for (int i = 0; i < 64; ++i) any_out |= !present[i] && (!data_only || i < 32);
+    if (!fftdec_plan_m(present, data_only, &p)) {
+      if (any_out) {
+        std::printf("plan refused a decodable pattern, trial %d\n", trial);
+        ++fails;
+      }
+      continue;
+    }
+    const uint32_t* w = p.w.data();
+    const unsigned baseA = p.side ? 32 : 0, baseB = p.side ? 0 : 32;
+    const uint32_t R = w[FftDecLayout::kR], rslots = w[FftDecLayout::kRslots];
+    for (int col = 0; col < 8; ++col) {
+      uint8_t cw[64];
+      for (int c = 0; c < 32; ++c) cw[c] = (uint8_t)rng();
+      for (int r = 32; r < 64; ++r) {
+        uint8_t a = 0;
+        for (int c = 0; c < 32; ++c) a ^= gf_mul(E.v[r][c], cw[c]);
+        cw[r] = a;
+      }
+      uint8_t v[32];
+      for (int t = 0; t < 32; ++t)
+        v[t] = (w[FftDecLayout::kPresA] >> t & 1) ? cw[baseA ^ t] : 0;
+      ifft(v, baseA);
+      fft(v, baseB);  // q on B
+      uint8_t s[32] = {};
+      for (int t = 0; t < 32; ++t)
+        if (R >> t & 1) s[t] = (uint8_t)(cw[baseB ^ t] ^ v[t]);
+      const int nrs = __builtin_popcount(rslots);
+      for (int o = 0; o < p.nout; ++o) {
+        const uint32_t od = w[FftDecLayout::kOuts + o];
+        const unsigned t = od & 31;
+        uint8_t acc = (od & 32) ? v[t] : 0;
+        const uint32_t* mk = w + FftDecLayout::kMasks + (size_t)o * nrs * 64;
+        for (int j = 0; j < 16; ++j) {
+          if (!(rslots >> j & 1)) continue;
+          acc ^= apply_masks(mk, s[2 * j], 0) ^ apply_masks(mk, s[2 * j + 1], 1);
+          mk += 64;
+        }
+        const unsigned pos = ((od & 32) ? baseB : baseA) ^ t;
+        ++cases;
+        if (acc != cw[pos] || present[pos] || (data_only && pos >= 32)) {
+          if (fails < 10)
+            std::printf("mismatch trial %d e %d side %d out %u: %u != %u\n", trial, e, p.side,
+                        pos, acc, cw[pos]);
+          ++fails;
+        }
+      }
+    }
+    // every requested erasure is an output
+    int want = 0;
+    for (int i = 0; i < 64; ++i) want += !present[i] && (!data_only || i < 32);
+    if (want != p.nout) {
+      std::printf("trial %d: %d outputs, %d erasures requested\n", trial, p.nout, want);
+      ++fails;
+    }
+    if (p.nrslots > (e + 1) / 2 + 0 && p.nrslots > __builtin_popcount(w[FftDecLayout::kDA])) {
+      std::printf("trial %d: %d syndrome slots for %d rows\n", trial, p.nrslots,
+                  __builtin_popcount(w[FftDecLayout::kDA]));
+      ++fails;
+    }
+  }
+  std::printf("fftdec model: %d outputs checked, %d failures\n", cases, fails);
+  return fails ? 1 : 0;
+}

@@ -658,6 +658,57 @@ def test_runtime_kernels_agree(torch, cess, corc, k, m, ln, ne):
         enc.set_option(4, 0)
 
 
+def _wide_patterns(rng, nseg, ne):
+    """RS(32,32) erasure patterns: random, all on one coset, split evenly, per segment."""
+    present = np.ones((nseg, 64), np.uint8)
+    for s in range(nseg):
+        kind = s % 4
+        if kind == 0 or ne > 32:
+            present[s, rng.choice(64, size=ne, replace=False)] = 0
+        elif kind == 1:  # data only lost (the side with more erasures is data)
+            present[s, rng.choice(32, size=min(ne, 32), replace=False)] = 0
+        elif kind == 2:  # parity mostly
+            present[s, 32 + rng.choice(32, size=min(ne, 32), replace=False)] = 0
+        else:  # half and half
+            a = ne // 2
+            present[s, rng.choice(32, size=a, replace=False)] = 0
+            present[s, 32 + rng.choice(32, size=ne - a, replace=False)] = 0
+    return present
+
+
+@pytest.mark.parametrize("ne", [2, 3, 5, 8, 13, 16, 24, 31, 32])
+@pytest.mark.parametrize("ln", [1024, 8192, 3 * 1024 + 512 * 2])
+def test_fftdec_matches_oracle(torch, cess, corc, ne, ln):
+    """RS(32,32) rebuilds on the FFT-domain erasure decoder (fftdec.hip: T1 transform, syndromes,
+    bit-plane run-time rows) are bit-exact with the C oracle's codeword: per-segment patterns on
+    both sides (data / parity / mixed erasures), one pattern for the whole batch, data_only, and
+    the same bytes as the run-time matrix kernels (CEC_OPT_FFTDEC_MIN = 0)."""
+    k = m = 32
+    nseg = 8
+    rng = np.random.default_rng(ne * 7 + ln)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = _wide_patterns(rng, nseg, ne)
+    enc = cess.New(k, m)
+    for fmin in (2, 0):  # the FFT-domain decoder from two outputs, then never
+        enc.set_option(7, fmin)
+        d_data = to_dev(torch, data * present[:, :k, None])
+        d_par = to_dev(torch, want * present[:, k:, None])
+        enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_data.cpu().numpy(), data), ("per-segment data", fmin)
+        assert np.array_equal(d_par.cpu().numpy(), want), ("per-segment parity", fmin)
+        # one pattern for every segment, and data_only (parity stays erased)
+        one = present[3]
+        d_data = to_dev(torch, data * one[None, :k, None])
+        d_par = to_dev(torch, want * one[None, k:, None])
+        enc.ReconstructBatch(d_data, d_par, nseg, ln, one, data_only=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_data.cpu().numpy(), data), ("data_only", fmin)
+        assert np.array_equal(d_par.cpu().numpy(), want * one[None, k:, None]), ("data_only p", fmin)
+    enc.set_option(7, 5)
+
+
 @pytest.mark.parametrize("ne,ln", [(1, 4096 + 3), (2, (1 << 16) + 16), (3, 4096 + 3), (4, 999)])
 def test_rtb_tuning_shapes_agree(torch, cess, corc, ne, ln):
     """The tuning build's k_rtb shapes (column width x columns in flight, variants 40-49)

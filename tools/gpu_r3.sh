@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round-3 GPU session: new parity tests, the --gpus 2 rehearsal, FFT-domain decoder A/B.
+# usage (on the GPU box via gpurun): bash tools/gpu_r3.sh <step...>
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 \
+        --timeout-method thread -m gpu \
+        -k "fftdec or runtime_kernels or decode_cache or all_parity or threads or repair or filler or large_verify or verify_batch or fillers" \
+        > gpurun_out/t_r3.log 2>&1 || exit 1 ;;
+    gpus2)
+      CESS_DIST_BACKEND=gloo CESS_DEVICE=0 timeout -k 10 300 python -u bench.py --gpus 2 \
+        --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/b_gpus2.json 2> gpurun_out/b_gpus2.err \
+        || exit 1 ;;
+    c6)
+      for e in 5 8 16 32; do
+        for f in 0 5; do
+          timeout -k 10 120 python -u bench.py --config 6 --erasures $e --fftdec-min $f --steps 50 \
+            --warmup 5 --no-cpu-baseline >> gpurun_out/c6_ab.jsonl 2>> gpurun_out/c6_ab.err || exit 1
+        done
+      done ;;
+  esac
+done
