@@ -400,6 +400,9 @@ def main() -> None:
     ap.add_argument("--fftdec-min", type=int, default=-1,
                     help="RS(32,32) rebuilds of at least this many shards run the FFT-domain "
                          "decoder (CEC_OPT_FFTDEC_MIN; 0 = never; -1 = library default)")
+    ap.add_argument("--fftdec-mode", type=int, default=0, choices=[0, 1],
+                    help="RS(32,32) rebuilds: 0 = FFT-domain decoder where its cost model beats "
+                         "k_rthx (library default), 1 = always (CEC_OPT_FFTDEC_MODE)")
     ap.add_argument("--erasures", type=int, default=0,
                     help="config 6: random erasures per segment (default m)")
     ap.add_argument("--lose-parity", action="store_true",
@@ -483,7 +486,7 @@ def main() -> None:
     enc.set_option(4, args.rt_mode)
     if args.fftdec_min >= 0:
         enc.set_option(7, args.fftdec_min)
-    fftdec_min = args.fftdec_min if args.fftdec_min >= 0 else 5
+    enc.set_option(8, args.fftdec_mode)
     enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)  # valid parity for config 3
 
     present = None
@@ -603,6 +606,7 @@ def main() -> None:
                               "GBps": round(nseg * per_seg / med / 1e6, 1)}), flush=True)
         return
 
+    fd_seg0 = enc.stat(4)  # segments the FFT-domain decoder rebuilt before this run
     for _ in range(args.warmup):
         step()
     drain()  # the timed region starts with an empty hash window and ends with it drained
@@ -633,6 +637,7 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    fd_seg1 = enc.stat(4)
 
     launch_ms = (float(np.mean([a.elapsed_time(b) for a, b in ev])) if per_step
                  else ev[0][0].elapsed_time(ev[0][1]) / args.steps)
@@ -704,11 +709,18 @@ def main() -> None:
                 "valu_instr_per_block": slots["valu_instr_per_block"],
                 "basis": "whole step (hash ticks share the chip with the encode); peak at 2.4 GHz"}
 
+    # share of the timed rebuilds the library sent to the FFT-domain decoder (CEC_STAT 4)
+    fd_frac = None
+    if args.config == 6:
+        fd_frac = (fd_seg1 - fd_seg0) / max(1, nseg * (args.steps + args.warmup))
+        fd_frac = round(min(1.0, fd_frac), 4)
     tag = f"c{args.config}"
     kernel_name = {2: "k_ct<EncCT<2, 1>>", 3: "k_ct_dec1_mixed21 (Dec1CT<2, 1, e> / EncCT<2, 1> per segment)",
                    4: "k_ct<EncCT<2, 1>>", 5: "k_fft3232<true, true>",
-                   6: ("k_fftdec_m" if 0 < fftdec_min <= (args.erasures or m)
-                       else "k_rthx<8>" if (args.erasures or m) > 4 else "k_rtb"),
+                   6: ("k_fftdec_m" if fd_frac == 1 else
+                       "k_rthx<8>" if fd_frac == 0 and (args.erasures or m) > 4 else
+                       "k_rtb" if fd_frac == 0 else
+                       f"k_fftdec_m ({fd_frac:.0%} of segments) + k_rthx<8> (by pattern cost)"),
                    7: "k_rtb<1>", 8: "k_rtb<4>"}[args.config]
     if args.generic:
         kernel_name = "k_rthx" if k <= 32 else "k_rt"

@@ -143,9 +143,11 @@ CEC_OPT_SHA_MODE = 3
 CEC_OPT_RT_MODE = 4
 CEC_OPT_DECODE_CACHE = 6
 CEC_OPT_FFTDEC_MIN = 7
+CEC_OPT_FFTDEC_MODE = 8
 CEC_STAT_DECODE_CACHED = 1
 CEC_STAT_RETIRED_PENDING = 2
 CEC_STAT_POOL_BYTES = 3
+CEC_STAT_FFTDEC_SEGMENTS = 4
 CEC_HQOPT_TICK = 1
 CEC_DIST_ID_BYTES = 128
 CEC_DIST_SURVIVOR = 0

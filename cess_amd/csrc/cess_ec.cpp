@@ -185,6 +185,7 @@ struct Program {
   uint32_t* fd = nullptr;
   size_t fd_bytes = 0;
   int fd_side = 0;
+  int fd_nrs = 0;  // syndrome slots of the plan (its row cost: outputs x slots)
   uint8_t in_idx[cec::kMaxShards] = {};   // survivors read (host copy)
   uint8_t out_idx[cec::kMaxShards] = {};  // shards written (host copy)
 };
@@ -329,6 +330,7 @@ int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int 
     prog->fd = static_cast<uint32_t*>(d);
     prog->fd_bytes = bytes;
     prog->fd_side = fdp->side;
+    prog->fd_nrs = fdp->nrslots;
     HIP_TRY(hipMemcpyAsync(prog->fd, h, bytes, hipMemcpyHostToDevice, upload));
   }
   // the block may be a reused one whose readers have completed; the upload must land before
@@ -379,6 +381,8 @@ struct cec_codec {
   bool force_generic = false;
   // RS(32,32) patterns with at least this many outputs take the FFT-domain decoder (0: never)
   int fftdec_min = 5;
+  int fftdec_mode = 0;  // 0: by the cost model (fftdec_cheaper), 1: every such rebuild
+  uint64_t fd_segments = 0;  // segments rebuilt by the FFT-domain decoder (CEC_STAT_FFTDEC_SEGMENTS)
   DevPool pool;  // declared before every holder of pool blocks: destroyed after them
   ProgPtr encode;
   // decode programs by erasure pattern (n presence flags + data_only), least recently used last
@@ -630,8 +634,16 @@ bool is_reencode(const cec_codec* c, const Program& p) {
   return true;
 }
 
+// The FFT-domain decoder costs T1 plus (outputs x syndrome slots) Horner rows; k_rthx costs
+// about the same per output at every pattern. Fitted to RS(32,32) rebuilds of 64 segments of
+// 512 KiB, random patterns (bench.py --config 6 --erasures e, profiles/r03/fd_dispatch.jsonl, r03 first-pass rows):
+// k_fftdec_m ~ 0.315 ms + 3.76 us per (output, slot), k_rthx ~ 0.235 ms + 33.9 us per output, so
+// the decoder wins where 84 + outputs x slots < 62.5 + 9 outputs.
+bool fftdec_cheaper(int nout, int nrs) { return 2 * (84 + nout * nrs) < 2 * 62 + 1 + 18 * nout; }
+
 bool use_fftdec(const cec_codec* c, const Program& p) {
-  return !c->force_generic && p.fd && c->fftdec_min > 0 && p.nout >= c->fftdec_min;
+  if (c->force_generic || !p.fd || c->fftdec_min <= 0 || p.nout < c->fftdec_min) return false;
+  return c->fftdec_mode == 1 || fftdec_cheaper(p.nout, p.fd_nrs);
 }
 
 int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* seg_list,
@@ -640,8 +652,10 @@ int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* s
   if (!c->force_generic && p.single < 0 && is_reencode(c, p))
     return do_encode(c, L, seg_list, nseg, st);
   if (use_fftdec(c, p) &&
-      cec::launch_fftdec(L, p.fd_side, p.fd, nullptr, seg_list, nseg, st))
+      cec::launch_fftdec(L, p.fd_side, p.fd, nullptr, seg_list, nseg, st)) {
+    c->fd_segments += nseg;
     return check_launch();
+  }
   if (c->force_generic || p.single < 0 ||
       !cec::launch_decode_ct(c->opts, c->k, c->m, p.single, L, seg_list, nseg, st))
     run_program(c->opts, p, L, seg_list, nseg, st);
@@ -837,6 +851,7 @@ int launch_ps_plan(cec_codec* c, const PsPlan& p, const Layout& L, hipStream_t s
     if (!cec::launch_fftdec(L, f.side, nullptr, ptrs + f.off, p.list + f.off, (uint32_t)f.count,
                             st))
       return set_err(CEC_EINVAL, "FFT-domain decode plan on a layout it does not fit");
+    c->fd_segments += f.count;
     int rc = check_launch();
     if (rc) return rc;
   }
@@ -972,6 +987,10 @@ int cec_set_option(cec_codec* c, int option, int value) {
       if (value < 0 || value > 64) return set_err(CEC_EINVAL, "fftdec min outputs in 0..64");
       c->fftdec_min = value;
       return CEC_OK;
+    case CEC_OPT_FFTDEC_MODE:
+      if (value < 0 || value > 1) return set_err(CEC_EINVAL, "fftdec mode is 0 (auto) or 1 (always)");
+      c->fftdec_mode = value;
+      return CEC_OK;
     case CEC_OPT_DECODE_CACHE:
       if (value < 1) return set_err(CEC_EINVAL, "decode cache capacity must be >= 1");
       c->cache_cap = (size_t)value;
@@ -987,6 +1006,7 @@ int cec_get_stat(const cec_codec* c, int stat, uint64_t* value) {
     case CEC_STAT_DECODE_CACHED: *value = c->decode_cache.size(); return CEC_OK;
     case CEC_STAT_RETIRED_PENDING: *value = c->pool.pending(); return CEC_OK;
     case CEC_STAT_POOL_BYTES: *value = c->pool.held(); return CEC_OK;
+    case CEC_STAT_FFTDEC_SEGMENTS: *value = c->fd_segments; return CEC_OK;
   }
   return set_err(CEC_EINVAL, "unknown stat");
 }
@@ -1033,6 +1053,7 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
     const bool fdok = cec::fftdec_layout_ok(L);
     pkey.push_back(fdok ? 1 : 0);
     pkey.push_back((char)c->fftdec_min);
+    pkey.push_back((char)c->fftdec_mode);
     if (!c->ps || c->ps->key != pkey) {
       std::unique_ptr<PsPlan> plan;
       rc = build_ps_plan(c, pkey, nseg, data_only != 0, &plan, false, fdok);

@@ -178,7 +178,10 @@ __device__ __forceinline__ void ifft32(uint32_t (&X)[16][8], uint32_t em) {
 
 // FFT onto the coset BETA ^ {0..31}: coefficients -> values. Layer i: a ^= s*b; b ^= a
 // (i = 4 .. 0). em / om = even / odd-lane masks.
-template <unsigned BETA>
+// SER: each slot's last-layer butterfly starts once the previous slot's is done (for callers that
+// keep every output slot live after the transform: interleaved, the layer's temporaries of many
+// slots add up)
+template <unsigned BETA, bool SER = false>
 __device__ __forceinline__ void fft32(uint32_t (&X)[16][8], uint32_t em, uint32_t om) {
   using T = Skews<BETA>;
   sfor<4>([&](auto I4) CEC_FFT_AI {
@@ -196,6 +199,7 @@ __device__ __forceinline__ void fft32(uint32_t (&X)[16][8], uint32_t em, uint32_
   sfor<16>([&](auto J) CEC_FFT_AI {
     constexpr unsigned s = T::s.s[0][J];
     uint32_t P[8];
+    if constexpr (SER && J > 0) asm volatile("" : "+v"(X[J][0]) : "v"(X[J - 1][7]));
     sfor<8>([&](auto Q) CEC_FFT_AI {
       const uint32_t y = partner(X[J][Q]);
       P[Q] = FFT_BOP3(em, y, X[J][Q], kSel);

@@ -11,15 +11,31 @@
 // applied in bit-plane form with per-segment masks from HBM (scalar loads): the two positions of a
 // lane-pair slot are first packed into the nibble halves of each plane (lane 0 keeps its
 // columns 0-15, lane 1 its columns 16-31, of both positions), so a mask word carries the
-// coefficient bits of both positions and every lane applies the same SGPR mask: one v_bitop3 per
-// (plane, plane) pair and slot, 2 VALU per byte per (output, syndrome pair). Cost: T1 + the
-// transposes (~4 VALU per byte of 64 shards) + 64 x outputs x syndrome slots per lane pair.
+// coefficient bits of both positions and every lane applies the same SGPR mask. A row is applied by
+// Horner over its coefficient bits (out = 2 out ^ T_b, T_b = XOR of the syndromes whose coefficient
+// has bit b): one v_bitop3 per (plane, bit) and slot, 8 scalar masks per (row, slot), 2 VALU per
+// byte per (output, syndrome pair) plus 3 per output and bit for the doubling. The R slots are
+// first swapped to the front of the register array (uniform branches, once per column block), so
+// the row loop is compiled per slot count with no branch inside. Cost: T1 + the transposes (~4 VALU
+// per byte of 64 shards) + 64 x outputs x syndrome slots per lane pair.
 //
 // Layout of the work as k_fft3232 (fft_core.h): one lane pair per 32 byte columns of a segment,
 // blockIdx.y = a segment of the launch's list with its own plan, shard_len % 1024 == 0.
+#include <utility>
+
 #include "fft_core.h"
 #include "fftdec_plan.h"
 #include "kernels.h"
+
+#ifndef CEC_FD_NMAX
+#define CEC_FD_NMAX 16  // row loops compiled for 1..CEC_FD_NMAX syndrome slots
+#endif
+// occupancy experiments: -DCEC_FD_WAVES=n asks the compiler for n waves per SIMD
+#ifdef CEC_FD_WAVES
+#define CEC_FD_ATTR __attribute__((amdgpu_waves_per_eu(CEC_FD_WAVES, CEC_FD_WAVES)))
+#else
+#define CEC_FD_ATTR
+#endif
 
 namespace cec {
 
@@ -80,9 +96,8 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
   const auto rA = rsrc(baseA), rB = rsrc(baseB);
   const uint32_t ss = (uint32_t)L.shard_stride;
   const uint32_t lcol = (uint32_t)col + l * ss;  // this lane's byte offset of position 0 / 1
-  const uint32_t presA = P[FftDecLayout::kPresA], R = P[FftDecLayout::kR];
-  const uint32_t nout = P[FftDecLayout::kNout], rslots = P[FftDecLayout::kRslots];
-  const uint32_t pslots = P[FftDecLayout::kPslots];
+  const uint32_t presA = P[FftDecLayout::kPresA];
+  const uint32_t nout = P[FftDecLayout::kNout];
 
   uint32_t X[16][8];
   // coset A, erased shards zeroed (out-of-range loads: no memory traffic), then bit-sliced
@@ -91,68 +106,117 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
   });
   sfor<16>([&](auto J) CEC_FFT_AI { tr8(X[J]); });
   ifft32<BA>(X, em);
-  fft32<BB>(X, em, om);  // q on coset B
+  fft32<BB, true>(X, em, om);  // q on coset B
   // X is complete here: the phases below start from it (keeps the compiler from interleaving the
   // transform's tail with them, which costs registers)
   sfor<16>([&](auto J) CEC_FFT_AI { fence(X[J]); });
-  // syndromes s = p ^ q at the R rows. A slot's load address waits on the slot four before it
-  // (four slots of loads in flight beyond X) and the first ones on the transform's end, so no
-  // load is hoisted above the transform or speculated out of its slot's branch.
-  sfor<16>([&](auto J) CEC_FFT_AI {
-    if ((R >> (2 * J)) & 3) {
-      uint32_t voff = (R >> (2 * J + l)) & 1 ? lcol : kOff;
-      if constexpr (J < 4)
-        asm volatile("" : "+v"(voff) : "v"(X[15][7]), "v"(X[14][7]));
-      else
-        asm volatile("" : "+v"(voff) : "v"(X[J - 4][7]));
-      uint32_t Y[8];
-      bld32(rB, voff, 2 * J * ss, Y);
-      tr8(Y);
-      sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] ^= Y[Q]; });
+  // R slots to the front: step i swaps register slots i and j_i (the plan's swap list)
+  const uint32_t nrs = P[FftDecLayout::kNrs];
+  sfor<15>([&](auto I) CEC_FFT_AI {
+    if (I < nrs) {
+      const uint32_t jm = P[FftDecLayout::kSwap + I];  // 1 << j_i
+      sfor<15 - I>([&](auto D) CEC_FFT_AI {
+        constexpr int J = I + 1 + D;
+        // bit tests, not ji == J: an equality chain becomes a switch whose cases LLVM merges into
+        // one swap with X indexed at run time (X then lives in scratch)
+        if ((jm >> J) & 1) {
+          asm volatile("");
+          sfor<8>([&](auto Q) CEC_FFT_AI { std::swap(X[I][Q], X[J][Q]); });
+        }
+      });
     }
   });
   const uint32_t keep = l ? 0xF0F0F0F0u : 0x0F0F0F0Fu;
   const uint32_t rot = l ? 28u : 4u;
-  sfor<16>([&](auto J) CEC_FFT_AI {
-    if ((pslots >> J) & 1) {
-      asm volatile("");  // a branch, not a select over every slot
-      pack_slot(X[J], keep, rot);
-    }
-  });
-  cplan_t mp = P + FftDecLayout::kMasks;
-  for (uint32_t o = 0; o < nout; ++o) {
-    const uint32_t od = P[FftDecLayout::kOuts + o];
-    const uint32_t t = od & 31;
-    uint32_t acc[8];
-    sfor<8>([&](auto Q) CEC_FFT_AI { acc[Q] = 0; });
-    if (od & 32) {  // an erased shard of B: its q, then the syndrome rows
-      const uint32_t nib = (t & 1) ? 0xF0F0F0F0u : 0x0F0F0F0Fu;
-      sfor<16>([&](auto J) CEC_FFT_AI {
-        if ((t >> 1) == J) sfor<8>([&](auto Q) CEC_FFT_AI { acc[Q] = X[J][Q] & nib; });
-      });
-    }
-    sfor<16>([&](auto J) CEC_FFT_AI {
-      if ((rslots >> J) & 1) {
-        sfor<8>([&](auto Q) CEC_FFT_AI {
-          sfor<8>([&](auto Pp) CEC_FFT_AI {
-            acc[Q] = FFT_BOP3(acc[Q], X[J][Pp], mp[Q * 8 + Pp], kXand);
-          });
-        });
-        mp += 64;
+  const uint32_t npk = P[FftDecLayout::kNpk];
+  auto outputs = [&](auto N) CEC_FFT_AI {
+    constexpr int NR = decltype(N)::value;
+    // syndromes s = p ^ q in register slots [0, NR): the R rows of B (an erased or unused position
+    // of a slot loads zeros). Slot i's load address waits on slot i - 3 (three slots of loads in
+    // flight beyond X), the first ones on the transform's end.
+    sfor<NR>([&](auto I) CEC_FFT_AI {
+      const uint32_t rs = P[FftDecLayout::kRsl + I];  // j_i | R bits of the slot << 8
+      uint32_t voff = (rs >> (8 + l)) & 1 ? lcol : kOff;
+      if constexpr (I < 3)
+        asm volatile("" : "+v"(voff) : "v"(X[15][7]), "v"(X[14][7]));
+      else
+        asm volatile("" : "+v"(voff) : "v"(X[I - 3][7]));
+      uint32_t Y[8];
+      bld32(rB, voff, 2 * (rs & 15) * ss, Y);
+      tr8(Y);
+      sfor<8>([&](auto Q) CEC_FFT_AI { X[I][Q] ^= Y[Q]; });
+    });
+    // nibble-pack the R slots and the slots holding an erased B output's q, one slot after the
+    // other (interleaved, the packs of 16 slots hold twice the registers)
+    sfor<NR>([&](auto I) CEC_FFT_AI {
+      uint32_t r = rot;
+      if constexpr (I > 0) asm volatile("" : "+v"(r) : "v"(X[I - 1][7]));
+      pack_slot(X[I], keep, r);
+    });
+    sfor<16 - NR>([&](auto D) CEC_FFT_AI {
+      constexpr int J = NR + D;
+      if ((npk >> J) & 1) {
+        asm volatile("");  // a branch, not a select over every slot
+        pack_slot(X[J], keep, rot);
       }
     });
-    // both positions' contributions to the lane's 16 columns, in the low nibbles; back to bytes
-    uint32_t w[8];
-    sfor<8>([&](auto Q) CEC_FFT_AI { w[Q] = FFT_BOP3(acc[Q], acc[Q] >> 4, 0x0F0F0F0Fu, kAndX); });
-    tr8(w);
-    uint8_t* dst = ((od & 32) ? baseB : baseA) + col + (uint64_t)t * ss + l * 512;
-    __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4*>(dst));
-  }
+    for (uint32_t o = 0; o < nout; ++o) {
+      const uint32_t od = P[FftDecLayout::kOuts + o];
+      const uint32_t t = od & 31, qm = od >> 16;  // qm = 1 << (slot of q)
+      const cplan_t mk = P + FftDecLayout::kMasks + o * (8 * NR);
+      uint32_t acc[8] = {};
+      // a step's masks are loaded once the step two before it is done (one step of prefetch): at
+      // 16 slots all 128 masks of a row up front would not fit the SGPRs
+      uint32_t dep1 = 0, dep2 = 0;
+      if constexpr (NR > 0) sfor<8>([&](auto B) CEC_FFT_AI {
+        constexpr int b = 7 - B;
+        cplan_t mb = mk + b * NR;
+        if constexpr (B >= 2) asm volatile("" : "+s"(mb) : "v"(dep2));
+        if constexpr (b == 7) {
+          sfor<8>([&](auto Q) CEC_FFT_AI { acc[Q] = X[0][Q] & mb[0]; });
+        } else {  // acc = 2 acc (planes: 0 <- 7, q <- q - 1, 2..4 also ^= 7; poly 0x11D)
+          const uint32_t a7 = acc[7];
+          sfor<7>([&](auto Q) CEC_FFT_AI { acc[7 - Q] = acc[6 - Q]; });
+          acc[0] = a7;
+          acc[2] ^= a7;
+          acc[3] ^= a7;
+          acc[4] ^= a7;
+          sfor<8>([&](auto Q) CEC_FFT_AI { acc[Q] = FFT_BOP3(acc[Q], X[0][Q], mb[0], kXand); });
+        }
+        sfor<NR - 1>([&](auto I) CEC_FFT_AI {
+          sfor<8>([&](auto Q) CEC_FFT_AI {
+            acc[Q] = FFT_BOP3(acc[Q], X[I + 1][Q], mb[I + 1], kXand);
+          });
+        });
+        dep2 = dep1;
+        dep1 = acc[7];
+      });
+      if (od & 32) {  // an erased shard of B: add its q
+        const uint32_t nib = (t & 1) ? 0xF0F0F0F0u : 0x0F0F0F0Fu;
+        sfor<16>([&](auto J) CEC_FFT_AI {
+          if ((qm >> J) & 1) sfor<8>([&](auto Q) CEC_FFT_AI { acc[Q] = FFT_BOP3(acc[Q], X[J][Q], nib, kXand); });
+        });
+      }
+      // both positions' contributions to the lane's 16 columns, in the low nibbles; back to bytes
+      uint32_t w[8];
+      sfor<8>([&](auto Q) CEC_FFT_AI { w[Q] = FFT_BOP3(acc[Q], acc[Q] >> 4, 0x0F0F0F0Fu, kAndX); });
+      tr8(w);
+      uint8_t* dst = ((od & 32) ? baseB : baseA) + col + (uint64_t)t * ss + l * 512;
+      __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4*>(dst));
+    }
+  };
+  // one row loop per slot count (0..16), selected by a bit test of the one-hot count (an equality
+  // chain becomes a switch, and LLVM then sinks the variants' common tails into one block whose
+  // registers are the union of all of them)
+  const uint32_t nrs1 = P[FftDecLayout::kNrs1];
+  sfor<CEC_FD_NMAX + 1>([&](auto N) CEC_FFT_AI {
+    if ((nrs1 >> N) & 1) outputs(std::integral_constant<int, N>{});
+  });
 }
 
 // plans: per listed segment (y) its plan, or `plan1` for every segment
 template <unsigned SIDE>
-__global__ __launch_bounds__(256) void k_fftdec_m(Layout L, const uint32_t* __restrict__ plan1,
+__global__ __launch_bounds__(256) CEC_FD_ATTR void k_fftdec_m(Layout L, const uint32_t* __restrict__ plan1,
                                                   const uint32_t* const* __restrict__ plans,
                                                   const uint32_t* __restrict__ seg_list,
                                                   uint32_t seg0) {

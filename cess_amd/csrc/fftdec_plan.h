@@ -11,9 +11,12 @@
 //        of the coset A. At d = |D| present points R of B the syndromes s = p_R ^ q_R = h(R) give
 //        u = inv(L[R][D]) s (any d points of B work: the code is MDS);
 //   out  erased c in D: u_c; erased e in B: q_e ^ h(e) = q_e ^ L[e][D] inv(L[R][D]) s.
-// Mode M (matvec) applies those rows to the syndromes as bit-plane masks in the kernel: cost
+// Mode M (matvec) applies those rows to the syndromes in the kernel, in bit-plane form: cost
 // (outputs) x (slots holding R), so the plan takes A = the coset with fewer erasures and packs R
-// into as few lane-pair slots (positions 2j, 2j + 1) as the present shards allow.
+// into as few lane-pair slots (positions 2j, 2j + 1) as the present shards allow. A row is applied
+// by Horner over the coefficient bits: out = sum_b 2^b T_b, T_b = XOR of the syndromes whose
+// coefficient has bit b, so a (row, slot) pair costs one mask per bit (8 words) instead of one per
+// entry of its 8 x 8 bit matrix (64): the plan stays in the scalar cache at 32 outputs.
 #pragma once
 #include <stdint.h>
 
@@ -36,9 +39,18 @@ struct FftDecLayout {
   static constexpr int kNout = 5;    // outputs written
   static constexpr int kRslots = 6;  // bit j: slot j (positions 2j, 2j + 1 of B) holds R rows
   static constexpr int kPslots = 7;  // bit j: slot j is packed (R or an erased B output)
-  static constexpr int kOuts = 8;    // [32]: output o = t | (on B) << 5
-  static constexpr int kMasks = 64;  // [nout][popcount(rslots)][8 q][8 p]
-  static size_t words(int nout, int nrslots) { return kMasks + (size_t)nout * nrslots * 64; }
+  static constexpr int kNrs = 8;     // popcount(kRslots)
+  static constexpr int kNpk = 9;
+  static constexpr int kNrs1 = 10;   // 1 << nrs     // bit r: register slot r is packed after the swaps
+  static constexpr int kSwap = 16;   // [16]: 1 << j_i, j_i the i-th R slot ascending (the kernel
+                                     // swaps register slots i and j_i for i < nrs: R slots land
+                                     // in [0, nrs))
+  static constexpr int kRsl = 32;    // [16]: j_i | (R bits of slot j_i: even, odd) << 8
+  static constexpr int kOuts = 48;   // [32]: output o = t | (on B) << 5 | (1 << the register slot
+                                     // of its q after the swaps) << 16
+  static constexpr int kMasks = 80;  // [nout][8 bits b][nrs]: bit b of the row's coefficients of
+                                     // the slot's even (low nibbles) and odd (high) position
+  static size_t words(int nout, int nrslots) { return kMasks + (size_t)nout * nrslots * 8; }
 };
 
 struct FftDecPlan {
@@ -138,13 +150,35 @@ inline bool fftdec_plan_m(const uint8_t* present, bool data_only, FftDecPlan* ou
   w[FftDecLayout::kNout] = (uint32_t)p.nout;
   w[FftDecLayout::kRslots] = rslots;
   w[FftDecLayout::kPslots] = pslots;
+  w[FftDecLayout::kNrs] = (uint32_t)nrs;
+  w[FftDecLayout::kNrs1] = 1u << nrs;
+  // the kernel's slot swaps: step i exchanges register slots i and j_i (j_i >= i, and no earlier
+  // step touched slot j_i), so R slot j_i ends in slot i; where every other slot ends (an erased
+  // B output's q) follows from the same swaps
+  int jr[16], at[16];  // jr: R slots ascending; at[j]: register slot holding original slot j
+  for (int j = 0, i = 0; j < 16; ++j)
+    if (rslots >> j & 1) jr[i++] = j;
+  int reg[16];  // reg[r]: original slot in register slot r
+  for (int j = 0; j < 16; ++j) reg[j] = j;
+  for (int i = 0; i < nrs; ++i) {
+    w[FftDecLayout::kSwap + i] = 1u << jr[i];
+    std::swap(reg[i], reg[jr[i]]);
+  }
+  uint32_t npk = 0;
+  for (int r = 0; r < 16; ++r) {
+    at[reg[r]] = r;
+    if (pslots >> reg[r] & 1) npk |= 1u << r;
+  }
+  w[FftDecLayout::kNpk] = npk;
+  for (int i = 0; i < nrs; ++i)
+    w[FftDecLayout::kRsl + i] = (uint32_t)jr[i] | (R >> (2 * jr[i]) & 3u) << 8;
   // syndrome index of each R position (column of the rows below)
   int ridx[32];
   for (int i = 0, t = 0; t < 32; ++t) ridx[t] = (R >> t & 1) ? i++ : -1;
   for (int o = 0; o < p.nout; ++o) {
     const uint32_t od = outs[o];
-    w[FftDecLayout::kOuts + o] = od;
     const unsigned t = od & 31;
+    w[FftDecLayout::kOuts + o] = od | (1u << at[t >> 1]) << 16;
     uint8_t row[32] = {};  // coefficients over the syndromes
     if (!(od & 32)) {      // an erased point of A: row of inv(L[R][D])
       const int di = (int)(std::find(Dl.begin(), Dl.end(), baseA ^ t) - Dl.begin());
@@ -157,18 +191,13 @@ inline bool fftdec_plan_m(const uint8_t* present, bool data_only, FftDecPlan* ou
         for (int r = 0; r < d; ++r) row[r] ^= gf_mul(le, linv.v[c][r]);
       }
     }
-    uint32_t* mk = w + FftDecLayout::kMasks + (size_t)o * nrs * 64;
-    for (int j = 0; j < 16; ++j) {
-      if (!(rslots >> j & 1)) continue;
-      const int lo = ridx[2 * j], hi = ridx[2 * j + 1];
-      const BitMatrix ml = gf_bitmatrix(lo >= 0 ? row[lo] : 0);
-      const BitMatrix mh = gf_bitmatrix(hi >= 0 ? row[hi] : 0);
-      for (int q = 0; q < 8; ++q)
-        for (int pp = 0; pp < 8; ++pp)
-          mk[q * 8 + pp] = ((ml.row[q] >> pp & 1) ? 0x0F0F0F0Fu : 0u) |
-                           ((mh.row[q] >> pp & 1) ? 0xF0F0F0F0u : 0u);
-      mk += 64;
-    }
+    uint32_t* mk = w + FftDecLayout::kMasks + (size_t)o * nrs * 8;
+    for (int b = 0; b < 8; ++b)
+      for (int i = 0; i < nrs; ++i) {
+        const int lo = ridx[2 * jr[i]], hi = ridx[2 * jr[i] + 1];
+        const bool bl = lo >= 0 && (row[lo] >> b & 1), bh = hi >= 0 && (row[hi] >> b & 1);
+        mk[b * nrs + i] = (bl ? 0x0F0F0F0Fu : 0u) | (bh ? 0xF0F0F0F0u : 0u);
+      }
   }
   *out = std::move(p);
   return true;

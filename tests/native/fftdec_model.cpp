@@ -2,7 +2,8 @@
 // the library builds (cess_amd/csrc/fftdec_plan.h): per byte column, T1 (IFFT over coset A with
 // its erased shards zeroed, FFT onto coset B), the syndromes at the plan's R rows, and every output
 // from the plan's bit-plane masks exactly as the kernel applies them (low / high nibble = the
-// slot's even / odd position). Compared with the codeword of the product's own encode matrix for
+// slot's even / odd position), including the register-slot swaps that bring the R slots to the
+// front and the Horner pass over each row's coefficient bits. Compared with the codeword of the product's own encode matrix for
 // random erasure patterns of 1..32 shards, both sides, with and without data_only.
 // Build: g++ -std=c++20 -O1 -fconstexpr-ops-limit=2000000000 fftdec_model.cpp
 #include <cstdio>
@@ -36,17 +37,8 @@ static void fft(uint8_t* v, unsigned beta) {
       }
   }
 }
-// x -> the byte the kernel's masks produce for one nibble half (0: low, 1: high)
-static uint8_t apply_masks(const uint32_t* mk, uint8_t x, int half) {
-  const uint32_t sel = half ? 0xF0F0F0F0u : 0x0F0F0F0Fu;
-  uint8_t r = 0;
-  for (int q = 0; q < 8; ++q) {
-    int bit = 0;
-    for (int p = 0; p < 8; ++p) bit ^= ((mk[q * 8 + p] & sel) == sel) & (x >> p & 1);
-    r |= (uint8_t)(bit << q);
-  }
-  return r;
-}
+// bit-sliced x -> 2x (poly 0x11D) on one byte
+static uint8_t xt(uint8_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1D : 0)); }
 
 int main() {
   using Big = Mat<64, 64>;
@@ -100,17 +92,55 @@ int main() {
       uint8_t s[32] = {};
       for (int t = 0; t < 32; ++t)
         if (R >> t & 1) s[t] = (uint8_t)(cw[baseB ^ t] ^ v[t]);
-      const int nrs = __builtin_popcount(rslots);
+      const int nrs = (int)w[FftDecLayout::kNrs];
+      if (nrs != __builtin_popcount(rslots) || w[FftDecLayout::kNrs1] != 1u << nrs) ++fails;
+      // register slots after the kernel's swaps: slot r holds the pair (even, odd) of positions
+      // of original slot reg[r] (syndromes where R, q where an erased B output, else unused)
+      uint8_t sv[16][2], qv[16][2];
+      for (int j = 0; j < 16; ++j)
+        for (int h = 0; h < 2; ++h) {
+          sv[j][h] = s[2 * j + h];
+          qv[j][h] = v[2 * j + h];
+        }
+      for (int i = 0; i < nrs; ++i) {
+        const uint32_t jm = w[FftDecLayout::kSwap + i];
+        if (__builtin_popcount(jm) != 1) ++fails;
+        const int ji = __builtin_ctz(jm);
+        // the syndrome loads of register slot i: shard pair j_i, its R positions
+        const uint32_t rs = w[FftDecLayout::kRsl + i];
+        if ((int)(rs & 15) != ji || (rs >> 8 & 3) != (R >> (2 * ji) & 3)) ++fails;
+        if (ji < i || !(rslots >> ji & 1)) ++fails;
+        for (int h = 0; h < 2; ++h) {
+          std::swap(sv[i][h], sv[ji][h]);
+          std::swap(qv[i][h], qv[ji][h]);
+        }
+      }
+      // packed register slots after the swaps: the R slots and those holding an erased B output
+      {
+        int reg[16];
+        for (int j = 0; j < 16; ++j) reg[j] = j;
+        for (int i = 0; i < nrs; ++i) std::swap(reg[i], reg[__builtin_ctz(w[FftDecLayout::kSwap + i])]);
+        uint32_t want = 0;
+        for (int r = 0; r < 16; ++r)
+          if ((R | w[FftDecLayout::kEB]) >> (2 * reg[r]) & 3) want |= 1u << r;
+        if (want != w[FftDecLayout::kNpk]) ++fails;
+      }
       for (int o = 0; o < p.nout; ++o) {
         const uint32_t od = w[FftDecLayout::kOuts + o];
-        const unsigned t = od & 31;
-        uint8_t acc = (od & 32) ? v[t] : 0;
-        const uint32_t* mk = w + FftDecLayout::kMasks + (size_t)o * nrs * 64;
-        for (int j = 0; j < 16; ++j) {
-          if (!(rslots >> j & 1)) continue;
-          acc ^= apply_masks(mk, s[2 * j], 0) ^ apply_masks(mk, s[2 * j + 1], 1);
-          mk += 64;
+        const unsigned t = od & 31, qm = od >> 16;
+        if (__builtin_popcount(qm) != 1 && (od & 32)) ++fails;
+        const unsigned qs = qm ? __builtin_ctz(qm) : 0;
+        const uint32_t* mk = w + FftDecLayout::kMasks + (size_t)o * nrs * 8;
+        uint8_t acc = 0;
+        for (int b = 7; b >= 0; --b) {
+          acc = xt(acc);
+          for (int i = 0; i < nrs; ++i) {
+            const uint32_t m = mk[b * nrs + i];
+            if (m & 0x0F0F0F0Fu) acc ^= sv[i][0];
+            if (m & 0xF0F0F0F0u) acc ^= sv[i][1];
+          }
         }
+        if (od & 32) acc ^= qv[qs][t & 1];
         const unsigned pos = ((od & 32) ? baseB : baseA) ^ t;
         ++cases;
         if (acc != cw[pos] || present[pos] || (data_only && pos >= 32)) {

@@ -690,6 +690,7 @@ def test_fftdec_matches_oracle(torch, cess, corc, ne, ln):
     want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
     present = _wide_patterns(rng, nseg, ne)
     enc = cess.New(k, m)
+    enc.set_option(8, 1)  # every FFT-domain-eligible rebuild on the decoder (no cost model)
     for fmin in (2, 0):  # the FFT-domain decoder from two outputs, then never
         enc.set_option(7, fmin)
         d_data = to_dev(torch, data * present[:, :k, None])
@@ -707,6 +708,36 @@ def test_fftdec_matches_oracle(torch, cess, corc, ne, ln):
         assert np.array_equal(d_data.cpu().numpy(), data), ("data_only", fmin)
         assert np.array_equal(d_par.cpu().numpy(), want * one[None, k:, None]), ("data_only p", fmin)
     enc.set_option(7, 5)
+    enc.set_option(8, 0)
+
+
+@pytest.mark.parametrize("ne", [8, 32])
+def test_fftdec_dispatch_by_cost(torch, cess, corc, ne):
+    """CEC_OPT_FFTDEC_MODE 0 (the default) sends a random RS(32,32) pattern to the FFT-domain
+    decoder only where its cost model beats k_rthx (eight erasures: the decoder; 32 with 16
+    syndrome slots: the matrix kernel), counted by CEC_STAT_FFTDEC_SEGMENTS; bit-exact either way."""
+    k = m = 32
+    nseg, ln = 6, 4096
+    rng = np.random.default_rng(500 + ne)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = np.ones((nseg, 64), np.uint8)
+    for s in range(nseg):
+        present[s, rng.choice(32, size=ne // 2, replace=False)] = 0
+        if ne == 32:  # every even parity shard: the 16 syndrome rows sit in 16 slots
+            present[s, 32::2] = 0
+        else:
+            present[s, 32 + rng.choice(32, size=ne - ne // 2, replace=False)] = 0
+    enc = cess.New(k, m)
+    before = enc.stat(4)
+    d_data = to_dev(torch, data * present[:, :k, None])
+    d_par = to_dev(torch, want * present[:, k:, None])
+    enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_data.cpu().numpy(), data)
+    assert np.array_equal(d_par.cpu().numpy(), want)
+    on_fd = enc.stat(4) - before
+    assert on_fd == (nseg if ne == 8 else 0), on_fd
 
 
 @pytest.mark.parametrize("ne,ln", [(1, 4096 + 3), (2, (1 << 16) + 16), (3, 4096 + 3), (4, 999)])

@@ -16,11 +16,25 @@ for step in "$@"; do
         --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/b_gpus2.json 2> gpurun_out/b_gpus2.err \
         || exit 1 ;;
     c6)
-      for e in 5 8 16 32; do
+      for e in ${FD_E:-5 8 16 32}; do
         for f in 0 5; do
           timeout -k 10 120 python -u bench.py --config 6 --erasures $e --fftdec-min $f --steps 50 \
             --warmup 5 --no-cpu-baseline >> gpurun_out/c6_ab.jsonl 2>> gpurun_out/c6_ab.err || exit 1
         done
+      done ;;
+    fdtests)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 \
+        --timeout-method thread -m gpu -k "fftdec or decode_cache or all_parity or reconstruct or dispatch" \
+        > gpurun_out/t_fd.log 2>&1 || exit 1 ;;
+    fdab)  # k_fftdec_m on each library of FD_LIBS (CESS_EC_LIB), k_rthx beside
+      for e in ${FD_E:-5 8 16 32}; do
+        for lib in ${FD_LIBS:-cess_amd/libcessec.so}; do
+          CESS_EC_LIB=$PWD/$lib timeout -k 10 120 python -u bench.py --config 6 --erasures $e \
+            --fftdec-mode 1 --steps 50 --warmup 5 --no-cpu-baseline >> gpurun_out/fd_ab.jsonl \
+            2>> gpurun_out/fd_ab.err || exit 1
+        done
+        timeout -k 10 120 python -u bench.py --config 6 --erasures $e --fftdec-min ${FD_RTHX:-0} --steps 50 \
+          --warmup 5 --no-cpu-baseline >> gpurun_out/fd_ab.jsonl 2>> gpurun_out/fd_ab.err || exit 1
       done ;;
   esac
 done
