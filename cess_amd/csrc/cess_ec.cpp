@@ -364,6 +364,7 @@ struct PsPlan {
   size_t mixed_off = 0, mixed_count = 0;  // tagged list (segment | erased << 30), count 0: none
   struct FdLaunch {
     int side;
+    bool big;           // cec::fftdec_big of the plans' syndrome slot count
     size_t off, count;  // segments list + per-segment FFT-domain plans (pointer array)
   };
   std::vector<FdLaunch> fd;
@@ -652,7 +653,8 @@ int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* s
   if (!c->force_generic && p.single < 0 && is_reencode(c, p))
     return do_encode(c, L, seg_list, nseg, st);
   if (use_fftdec(c, p) &&
-      cec::launch_fftdec(L, p.fd_side, p.fd, nullptr, seg_list, nseg, st)) {
+      cec::launch_fftdec(L, p.fd_side, cec::fftdec_big(p.fd_nrs), p.fd, nullptr, seg_list,
+                         nseg, st)) {
     c->fd_segments += nseg;
     return check_launch();
   }
@@ -711,7 +713,7 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
     groups[it->second].second.push_back((uint32_t)s);
   }
   bool all_ct = !c->force_generic;
-  std::vector<std::pair<ProgPtr, const std::vector<uint32_t>*>> progs, reencode, fdg[2];
+  std::vector<std::pair<ProgPtr, const std::vector<uint32_t>*>> progs, reencode, fdg[4];
   // new patterns' program uploads stay in flight until the one synchronisation below (one per
   // plan, not per pattern: 64 new RS(32,32) patterns cost ~1 ms of waits otherwise); every return
   // path waits for them before their host images go
@@ -738,7 +740,7 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
       continue;
     }
     if (fdok && use_fftdec(c, *p)) {  // RS(32,32) wide rebuilds: the FFT-domain decoder
-      fdg[p->fd_side].push_back({p, &g.second});
+      fdg[p->fd_side * 2 + (cec::fftdec_big(p->fd_nrs) ? 1 : 0)].push_back({p, &g.second});
       continue;
     }
     progs.push_back({p, &g.second});
@@ -753,10 +755,10 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
   // the run-time launches index the segment list and the chunk-pointer array with one offset:
   // keep them aligned past the re-encode lists
   hp.resize(hl.size(), nullptr);
-  for (int side = 0; side < 2; ++side) {
-    if (fdg[side].empty()) continue;
-    PsPlan::FdLaunch f{side, hl.size(), 0};
-    for (auto& pr : fdg[side])
+  for (int cls = 0; cls < 4; ++cls) {  // side x size class: one launch each
+    if (fdg[cls].empty()) continue;
+    PsPlan::FdLaunch f{cls >> 1, (cls & 1) != 0, hl.size(), 0};
+    for (auto& pr : fdg[cls])
       for (uint32_t sg : *pr.second) {
         hl.push_back(sg);
         hp.push_back(pr.first->fd);
@@ -848,8 +850,8 @@ int launch_ps_plan(cec_codec* c, const PsPlan& p, const Layout& L, hipStream_t s
   }
   const uint32_t* const* ptrs = static_cast<const uint32_t* const*>(p.ptrs);
   for (const auto& f : p.fd) {
-    if (!cec::launch_fftdec(L, f.side, nullptr, ptrs + f.off, p.list + f.off, (uint32_t)f.count,
-                            st))
+    if (!cec::launch_fftdec(L, f.side, f.big, nullptr, ptrs + f.off, p.list + f.off,
+                            (uint32_t)f.count, st))
       return set_err(CEC_EINVAL, "FFT-domain decode plan on a layout it does not fit");
     c->fd_segments += f.count;
     int rc = check_launch();

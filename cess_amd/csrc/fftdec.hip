@@ -27,9 +27,6 @@
 #include "fftdec_plan.h"
 #include "kernels.h"
 
-#ifndef CEC_FD_NMAX
-#define CEC_FD_NMAX 16  // row loops compiled for 1..CEC_FD_NMAX syndrome slots
-#endif
 // occupancy experiments: -DCEC_FD_WAVES=n asks the compiler for n waves per SIMD
 #ifdef CEC_FD_WAVES
 #define CEC_FD_ATTR __attribute__((amdgpu_waves_per_eu(CEC_FD_WAVES, CEC_FD_WAVES)))
@@ -74,18 +71,28 @@ __device__ __forceinline__ void fence(uint32_t (&x)[8]) {
 // Lane pair slot J (positions 2J, 2J + 1) -> nibble-packed: both lanes hold both positions for
 // their half of the columns (lane 0: columns of dwords 0-3 = the low nibble of every plane byte,
 // lane 1: dwords 4-7 = the high nibble), the even position in the low nibble, the odd in the high.
-// Lane 0 sends its high nibbles down, lane 1 its low nibbles up: a rotate by 4 / 28 (the wrapped
-// bits land in the half the receiver keeps from its own register).
+// Each lane reads its partner's plane (DPP straight from the register, no wait states) and rotates
+// it (rot: 28 on lane 0, the partner's low nibbles go up; 4 on lane 1, its high nibbles go down)
+// into the half it does not keep.
 __device__ __forceinline__ void pack_slot(uint32_t (&x)[8], uint32_t keep, uint32_t rot) {
   sfor<8>([&](auto Q) CEC_FFT_AI {
-    const uint32_t send = __builtin_amdgcn_alignbit(x[Q], x[Q], rot);
-    x[Q] = FFT_BOP3(keep, x[Q], partner(send), kSel);
+    const uint32_t y = __builtin_amdgcn_alignbit(partner(x[Q]), partner(x[Q]), rot);
+    x[Q] = FFT_BOP3(keep, x[Q], y, kSel);
   });
 }
 
-template <unsigned SIDE>
+// The first LR syndrome slots' rows are fetched at the start into LDS (buffer loads to LDS, 2 x
+// 1 KiB per slot and wave), so they land while the transform runs instead of being waited for after
+// it. Two kernels by syndrome slot count (the plan's nrs): up to kSmallNr slots in at most 168
+// VGPRs with LR = 4 (32 KiB per workgroup: three waves per SIMD), more slots at two waves per SIMD
+// with LR = 8 (64 KiB).
+constexpr int kSmallNr = 4;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef const __attribute__((address_space(3))) u32x4 lds_u32x4;
+
+template <unsigned SIDE, int NLO, int NHI, int LR>
 __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64_t col,
-                                           cplan_t P) {
+                                           cplan_t P, lds_u32* lw) {
   constexpr unsigned BA = SIDE ? 32u : 0u, BB = SIDE ? 0u : 32u;
   const uint32_t l = threadIdx.x & 1;
   const uint32_t em = l ? 0u : 0xFFFFFFFFu, om = ~em;
@@ -104,6 +111,18 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
   sfor<16>([&](auto J) CEC_FFT_AI {
     bld32(rA, (presA >> (2 * J + l)) & 1 ? lcol : kOff, 2 * J * ss, X[J]);
   });
+  // the syndrome rows of the first LR R slots into this wave's LDS area (lane k's 16 bytes of a
+  // piece land at 16 k: each lane reads back only what it loaded)
+  const uint32_t nrs = P[FftDecLayout::kNrs];
+  const uint32_t npre = nrs < (uint32_t)LR ? nrs : (uint32_t)LR;
+  for (uint32_t i = 0; i < npre; ++i) {
+    const uint32_t rs = P[FftDecLayout::kRsl + i];
+    const uint32_t voff = (rs >> (8 + l)) & 1 ? lcol : kOff;
+    const uint32_t soff = 2 * (rs & 15) * ss;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_u32*)(lw + i * 512), 16, voff, soff, 0, 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_u32*)(lw + i * 512 + 256), 16, voff + 512,
+                                             soff, 0, 2);
+  }
   sfor<16>([&](auto J) CEC_FFT_AI { tr8(X[J]); });
   ifft32<BA>(X, em);
   fft32<BB, true>(X, em, om);  // q on coset B
@@ -111,7 +130,6 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
   // transform's tail with them, which costs registers)
   sfor<16>([&](auto J) CEC_FFT_AI { fence(X[J]); });
   // R slots to the front: step i swaps register slots i and j_i (the plan's swap list)
-  const uint32_t nrs = P[FftDecLayout::kNrs];
   sfor<15>([&](auto I) CEC_FFT_AI {
     if (I < nrs) {
       const uint32_t jm = P[FftDecLayout::kSwap + I];  // 1 << j_i
@@ -127,31 +145,43 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
     }
   });
   const uint32_t keep = l ? 0xF0F0F0F0u : 0x0F0F0F0Fu;
-  const uint32_t rot = l ? 28u : 4u;
+  const uint32_t rot = l ? 4u : 28u;  // pack_slot rotates the partner's plane: by the partner's amount
   const uint32_t npk = P[FftDecLayout::kNpk];
   auto outputs = [&](auto N) CEC_FFT_AI {
     constexpr int NR = decltype(N)::value;
     // syndromes s = p ^ q in register slots [0, NR): the R rows of B (an erased or unused position
-    // of a slot loads zeros). Slot i's load address waits on slot i - 3 (three slots of loads in
-    // flight beyond X), the first ones on the transform's end.
+    // of a slot loads zeros), from LDS for the first LR slots; past them slot i's load address
+    // waits on slot i - 3 (three slots of loads in flight beyond X).
+    if constexpr (NR > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS rows
+    const uint32_t lane = threadIdx.x & 63;
     sfor<NR>([&](auto I) CEC_FFT_AI {
-      const uint32_t rs = P[FftDecLayout::kRsl + I];  // j_i | R bits of the slot << 8
-      uint32_t voff = (rs >> (8 + l)) & 1 ? lcol : kOff;
-      if constexpr (I < 3)
-        asm volatile("" : "+v"(voff) : "v"(X[15][7]), "v"(X[14][7]));
-      else
-        asm volatile("" : "+v"(voff) : "v"(X[I - 3][7]));
       uint32_t Y[8];
-      bld32(rB, voff, 2 * (rs & 15) * ss, Y);
+      if constexpr (I < LR) {
+        // a lane whose position is not an R row loaded out of range: the LDS DMA then writes
+        // nothing, so its bytes there are stale and are masked to zero here
+        const uint32_t rs = P[FftDecLayout::kRsl + I];
+        const uint32_t keepm = 0u - ((rs >> (8 + l)) & 1);
+        const u32x4 a = *reinterpret_cast<lds_u32x4*>(lw + I * 512 + lane * 4);
+        const u32x4 b = *reinterpret_cast<lds_u32x4*>(lw + I * 512 + 256 + lane * 4);
+        Y[0] = a.x & keepm; Y[1] = a.y & keepm; Y[2] = a.z & keepm; Y[3] = a.w & keepm;
+        Y[4] = b.x & keepm; Y[5] = b.y & keepm; Y[6] = b.z & keepm; Y[7] = b.w & keepm;
+      } else {
+        const uint32_t rs = P[FftDecLayout::kRsl + I];  // j_i | R bits of the slot << 8
+        uint32_t voff = (rs >> (8 + l)) & 1 ? lcol : kOff;
+        asm volatile("" : "+v"(voff) : "v"(X[I - 3][7]));
+        bld32(rB, voff, 2 * (rs & 15) * ss, Y);
+      }
       tr8(Y);
       sfor<8>([&](auto Q) CEC_FFT_AI { X[I][Q] ^= Y[Q]; });
     });
     // nibble-pack the R slots and the slots holding an erased B output's q, one slot after the
     // other (interleaved, the packs of 16 slots hold twice the registers)
     sfor<NR>([&](auto I) CEC_FFT_AI {
-      uint32_t r = rot;
-      if constexpr (I > 0) asm volatile("" : "+v"(r) : "v"(X[I - 1][7]));
-      pack_slot(X[I], keep, r);
+      if constexpr (I > 0)
+        asm volatile("" : "+v"(X[I][0]), "+v"(X[I][1]), "+v"(X[I][2]), "+v"(X[I][3]),
+                     "+v"(X[I][4]), "+v"(X[I][5]), "+v"(X[I][6]), "+v"(X[I][7])
+                     : "v"(X[I - 1][7]));
+      pack_slot(X[I], keep, rot);
     });
     sfor<16 - NR>([&](auto D) CEC_FFT_AI {
       constexpr int J = NR + D;
@@ -205,31 +235,38 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
       __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4*>(dst));
     }
   };
-  // one row loop per slot count (0..16), selected by a bit test of the one-hot count (an equality
+  // one row loop per slot count (NLO..NHI), selected by a bit test of the one-hot count (an equality
   // chain becomes a switch, and LLVM then sinks the variants' common tails into one block whose
   // registers are the union of all of them)
   const uint32_t nrs1 = P[FftDecLayout::kNrs1];
-  sfor<CEC_FD_NMAX + 1>([&](auto N) CEC_FFT_AI {
+  sfor<NHI + 1 - NLO>([&](auto N0) CEC_FFT_AI {
+    constexpr int N = NLO + N0;
     if ((nrs1 >> N) & 1) outputs(std::integral_constant<int, N>{});
   });
 }
 
-// plans: per listed segment (y) its plan, or `plan1` for every segment
-template <unsigned SIDE>
+// plans: per listed segment (y) its plan, or `plan1` for every segment. BIG: plans with more than
+// kSmallNr syndrome slots (the host sorts them, fftdec_big).
+template <unsigned SIDE, bool BIG>
 __global__ __launch_bounds__(256) CEC_FD_ATTR void k_fftdec_m(Layout L, const uint32_t* __restrict__ plan1,
                                                   const uint32_t* const* __restrict__ plans,
                                                   const uint32_t* __restrict__ seg_list,
                                                   uint32_t seg0) {
+  constexpr int NLO = BIG ? kSmallNr + 1 : 0, NHI = BIG ? 16 : kSmallNr, LR = BIG ? 8 : kSmallNr;
   const uint32_t y = seg0 + blockIdx.y;
   const uint32_t seg = seg_list ? seg_list[y] : y;
   const uint32_t* P = plans ? plans[y] : plan1;
   const uint64_t gp = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 1;  // lane pair
   const uint64_t col = (gp >> 5) * 1024 + (gp & 31) * 16;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4 * LR * 512];
   if (col >= L.len) return;  // whole waves leave together
-  dec_m_cols<SIDE>(L, seg, col, (cplan_t)P);
+  dec_m_cols<SIDE, NLO, NHI, LR>(L, seg, col, (cplan_t)P,
+                                 (lds_u32*)(lds + (threadIdx.x >> 6) * (LR * 512)));
 }
 
 }  // namespace
+
+bool fftdec_big(int nrs) { return nrs > kSmallNr; }
 
 bool fftdec_layout_ok(const Layout& L) {
   const uintptr_t bits = (uintptr_t)L.data | (uintptr_t)L.parity | L.shard_stride |
@@ -238,19 +275,17 @@ bool fftdec_layout_ok(const Layout& L) {
          L.shard_stride < (uint64_t(1) << 26);  // 32-bit buffer offsets over a coset
 }
 
-bool launch_fftdec(const Layout& L, int side, const uint32_t* plan1,
+bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
                    const uint32_t* const* plans, const uint32_t* seg_list, uint32_t nseg,
                    hipStream_t st) {
   if (!fftdec_layout_ok(L) || (side != 0 && side != 1)) return false;
   const uint64_t gx = (L.len / 32 * 2 + 255) / 256;
+  auto kern = side ? (big ? k_fftdec_m<1, true> : k_fftdec_m<1, false>)
+                   : (big ? k_fftdec_m<0, true> : k_fftdec_m<0, false>);
   for (uint32_t s0 = 0; s0 < nseg; s0 += 65535) {
     const uint32_t ny = nseg - s0 < 65535 ? nseg - s0 : 65535;
-    if (side)
-      hipLaunchKernelGGL(k_fftdec_m<1>, dim3((unsigned)gx, ny), dim3(256), 0, st, L, plan1, plans,
-                         seg_list, s0);
-    else
-      hipLaunchKernelGGL(k_fftdec_m<0>, dim3((unsigned)gx, ny), dim3(256), 0, st, L, plan1, plans,
-                         seg_list, s0);
+    hipLaunchKernelGGL(kern, dim3((unsigned)gx, ny), dim3(256), 0, st, L, plan1, plans, seg_list,
+                       s0);
   }
   return true;
 }

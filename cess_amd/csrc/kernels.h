@@ -81,10 +81,13 @@ bool launch_fft_rs3232_verify(const Layout& L, uint8_t* ok, uint32_t nseg, hipSt
 
 // RS(32,32) erasure decode on the additive FFT (fftdec.hip) with plans of fftdec_plan.h: every
 // segment uses `plan1`, or listed segment y uses plans[y] (all of the launch's plans take the same
-// side). False (nothing launched) when the layout does not fit (fftdec_layout_ok).
+// side and the same size class, fftdec_big of their syndrome slot count). False (nothing launched)
+// when the layout does not fit (fftdec_layout_ok).
 bool fftdec_layout_ok(const Layout& L);
-bool launch_fftdec(const Layout& L, int side, const uint32_t* plan1, const uint32_t* const* plans,
-                   const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
+bool fftdec_big(int nrs);
+bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
+                   const uint32_t* const* plans, const uint32_t* seg_list, uint32_t nseg,
+                   hipStream_t st);
 
 // Whether a compile-time single-erasure decode kernel exists for (k, m, missing).
 bool has_decode_ct(int k, int m, int missing);
