@@ -368,6 +368,79 @@ def launch_ranks(n: int, argv) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def kernel_label(config: int, fd_frac, erasures: int, generic: bool, rt_mode: int, k: int) -> str:
+    """The dominant kernel of a bench line. Config 6: fd_frac = share of the timed rebuilds the
+    library sent to the FFT-domain decoder (CEC_STAT_FFTDEC_SEGMENTS)."""
+    if config == 6:
+        name = ("k_fftdec_m" if fd_frac == 1 else
+                "k_rthx<8>" if fd_frac == 0 and erasures > 4 else
+                "k_rtb" if fd_frac == 0 else
+                f"k_fftdec_m ({fd_frac:.0%} of segments) + k_rthx<8> (by pattern cost)")
+    else:
+        name = {2: "k_ct<EncCT<2, 1>>",
+                3: "k_ct_dec1_mixed21 (Dec1CT<2, 1, e> / EncCT<2, 1> per segment)",
+                4: "k_ct<EncCT<2, 1>>", 5: "k_fft3232<true, true>", 7: "k_rtb<1>",
+                8: "k_rtb<4>"}[config]
+    if generic:
+        name = "k_rthx" if k <= 32 else "k_rt"
+    if rt_mode and (generic or config in (6, 7, 8)):
+        name = {1: "k_rt", 2: "k_rth", 3: "k_rtb"}[rt_mode]
+    return name
+
+
+def wide_code_legs(dev, local, stream, nseg=64, reps=10) -> dict:
+    """RS(32,32) legs timed with HIP events on `stream` (64 segments of 16 MiB, 2 GiB per batch):
+    encode, restoral of one random lost fragment per segment, rebuilds of 8 and 32 random
+    erasures per segment (per-segment patterns; the library picks k_fftdec_m or k_rthx by its
+    cost model), verify. Algorithmic bytes as the bench line's: (k + outputs) x F per segment
+    (encode and verify: (k + m) x F). The batch is checked with the fused verify afterwards."""
+    import torch
+
+    import cess_amd
+    k, m, F = 32, 32, 512 * 1024
+    enc = cess_amd.New(k, m, device=local)
+    d_data = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
+    d_par = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
+    cess_amd.fill_synthetic(d_data, k * F, nseg, 0, 0xCE550005, stream=stream)
+    rng = np.random.default_rng(0xCE55)
+
+    def timed_ms(fn):
+        for _ in range(2):
+            fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            fn()
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        return a.elapsed_time(b) / reps
+
+    legs = {}
+
+    def leg(name, fn, outs):
+        ms = timed_ms(fn)
+        legs[name] = {"ms": round(ms, 4),
+                      "GBps": round(nseg * (k + outs) * F / (ms * 1e-3) / GB, 1)}
+
+    leg("encode", lambda: enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream), m)
+    for ne, name in ((1, "restoral_1_lost"), (8, "rebuild_8_lost"), (32, "rebuild_32_lost")):
+        pres = np.ones((nseg, k + m), np.uint8)
+        for s_ in range(nseg):
+            pres[s_, rng.choice(k + m, size=ne, replace=False)] = 0
+        fd0 = enc.stat(4)
+        leg(name, lambda: enc.ReconstructBatch(d_data, d_par, nseg, F, pres, stream=stream), ne)
+        legs[name]["fftdec_segment_share"] = round(
+            (enc.stat(4) - fd0) / (nseg * (reps + 2)), 3)
+    d_ok = torch.empty(nseg, dtype=torch.uint8, device=dev)
+    leg("verify", lambda: enc.VerifyBatch(d_data, d_par, nseg, F, d_ok=d_ok, stream=stream), m)
+    torch.cuda.synchronize(dev)
+    legs["codeword_consistent_after_rebuilds"] = bool(d_ok.cpu().numpy().all())
+    legs["workload"] = f"RS(32,32), {nseg} segments of 16 MiB (F = 512 KiB) per launch"
+    enc.close()
+    del d_data, d_par
+    return legs
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -715,17 +788,8 @@ def main() -> None:
         fd_frac = (fd_seg1 - fd_seg0) / max(1, nseg * (args.steps + args.warmup))
         fd_frac = round(min(1.0, fd_frac), 4)
     tag = f"c{args.config}"
-    kernel_name = {2: "k_ct<EncCT<2, 1>>", 3: "k_ct_dec1_mixed21 (Dec1CT<2, 1, e> / EncCT<2, 1> per segment)",
-                   4: "k_ct<EncCT<2, 1>>", 5: "k_fft3232<true, true>",
-                   6: ("k_fftdec_m" if fd_frac == 1 else
-                       "k_rthx<8>" if fd_frac == 0 and (args.erasures or m) > 4 else
-                       "k_rtb" if fd_frac == 0 else
-                       f"k_fftdec_m ({fd_frac:.0%} of segments) + k_rthx<8> (by pattern cost)"),
-                   7: "k_rtb<1>", 8: "k_rtb<4>"}[args.config]
-    if args.generic:
-        kernel_name = "k_rthx" if k <= 32 else "k_rt"
-    if args.rt_mode and (args.generic or args.config in (6, 7, 8)):
-        kernel_name = {1: "k_rt", 2: "k_rth", 3: "k_rtb"}[args.rt_mode]
+    kernel_name = kernel_label(args.config, fd_frac, args.erasures or m, args.generic,
+                               args.rt_mode, k)
     traffic = load_traffic(tag, bytes_step_gpu, kernel_name)
     out = {
         "metric": METRIC,
@@ -826,6 +890,9 @@ def main() -> None:
         out.setdefault("extra", {}).update(
             {"reconstruct_GBps_per_gpu": round(bytes_step_gpu / (dms * 1e-3) / GB, 2),
              "reconstruct_ms": round(dms, 4)})
+        # the wide code (BASELINE config 5's RS(32,32), 16 MiB segments: F = 512 KiB) in the same
+        # run, so the driver's own line carries its encode, restoral and multi-erasure rebuild rates
+        out["extra"]["wide_code"] = wide_code_legs(dev, local, stream)
         # the measured-copy ceiling beside the spec peak: a device-to-device copy
         # of the same 1 GiB data batch (HIP's blit kernel), read + write bytes per copy
         src = d_data.view(-1)

@@ -637,10 +637,13 @@ bool is_reencode(const cec_codec* c, const Program& p) {
 
 // The FFT-domain decoder costs T1 plus (outputs x syndrome slots) Horner rows; k_rthx costs
 // about the same per output at every pattern. Fitted to RS(32,32) rebuilds of 64 segments of
-// 512 KiB, random patterns (bench.py --config 6 --erasures e, profiles/r03/fd_dispatch.jsonl, r03 first-pass rows):
-// k_fftdec_m ~ 0.315 ms + 3.76 us per (output, slot), k_rthx ~ 0.235 ms + 33.9 us per output, so
-// the decoder wins where 84 + outputs x slots < 62.5 + 9 outputs.
-bool fftdec_cheaper(int nout, int nrs) { return 2 * (84 + nout * nrs) < 2 * 62 + 1 + 18 * nout; }
+// 512 KiB, random patterns (bench.py --config 6 --erasures e; profiles/r03/fd_lds_split.jsonl):
+// k_fftdec_m ~ 0.296 ms + 3.3 us per (output, slot) at up to four slots (three waves per SIMD),
+// ~3.8 us past four (two waves); k_rthx ~ 0.235 ms + 33.9 us per output.
+bool fftdec_cheaper(int nout, int nrs) {
+  const long pairs = (long)nout * nrs;
+  return cec::fftdec_big(nrs) ? 10 * pairs + 160 < 89L * nout : 10 * pairs + 186 < 103L * nout;
+}
 
 bool use_fftdec(const cec_codec* c, const Program& p) {
   if (c->force_generic || !p.fd || c->fftdec_min <= 0 || p.nout < c->fftdec_min) return false;

@@ -56,3 +56,16 @@ def test_too_few_gpus_exits_nonzero():
     assert r.returncode == 2, (r.stdout, r.stderr)
     assert "--gpus 64" in r.stderr
     assert r.stdout.strip() == ""
+
+
+def test_kernel_label_every_config():
+    """bench.py's line names its dominant kernel for every config (config 6 from the share of
+    segments the FFT-domain decoder took), with no GPU."""
+    import bench
+    for cfg in (2, 3, 4, 5, 7, 8):
+        assert bench.kernel_label(cfg, None, 1, False, 0, 2).startswith("k_")
+    assert bench.kernel_label(6, 1.0, 8, False, 0, 32) == "k_fftdec_m"
+    assert bench.kernel_label(6, 0.0, 32, False, 0, 32) == "k_rthx<8>"
+    assert bench.kernel_label(6, 0.0, 3, False, 0, 32) == "k_rtb"
+    assert "50%" in bench.kernel_label(6, 0.5, 16, False, 0, 32)
+    assert bench.kernel_label(2, None, 1, True, 0, 2) == "k_rthx"
