@@ -381,7 +381,7 @@ struct cec_codec {
   KernelOpts opts;
   bool force_generic = false;
   // RS(32,32) patterns with at least this many outputs take the FFT-domain decoder (0: never)
-  int fftdec_min = 5;
+  int fftdec_min = 4;
   int fftdec_mode = 0;  // 0: by the cost model (fftdec_cheaper), 1: every such rebuild
   uint64_t fd_segments = 0;  // segments rebuilt by the FFT-domain decoder (CEC_STAT_FFTDEC_SEGMENTS)
   DevPool pool;  // declared before every holder of pool blocks: destroyed after them
@@ -639,9 +639,12 @@ bool is_reencode(const cec_codec* c, const Program& p) {
 // about the same per output at every pattern. Fitted to RS(32,32) rebuilds of 64 segments of
 // 512 KiB, random patterns (bench.py --config 6 --erasures e; profiles/r03/fd_lds_split.jsonl):
 // k_fftdec_m ~ 0.296 ms + 3.3 us per (output, slot) at up to four slots (three waves per SIMD),
-// ~3.8 us past four (two waves); k_rthx ~ 0.235 ms + 33.9 us per output.
+// ~3.8 us past four (two waves); k_rthx ~ 0.235 ms + 33.9 us per output; up to four outputs the
+// alternative is k_rtb, ~0.13 ms + 57 us per output (5.9 / 4.9 / 3.9 / 3.4 TB/s
+// at one to four outputs).
 bool fftdec_cheaper(int nout, int nrs) {
   const long pairs = (long)nout * nrs;
+  if (nout <= 4) return 33 * pairs + 1660 < 570L * nout;
   return cec::fftdec_big(nrs) ? 10 * pairs + 160 < 89L * nout : 10 * pairs + 186 < 103L * nout;
 }
 

@@ -393,7 +393,7 @@ int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t s
 #define CEC_OPT_DECODE_CACHE 6  /* capacity (>= 1) of the decode-program LRU cache, one entry
                                    per erasure pattern (default 4096) */
 #define CEC_OPT_FFTDEC_MIN 7    /* RS(32,32): rebuilds of at least this many shards per segment
-                                   may run the FFT-domain erasure decoder (0 = never; default 5) */
+                                   may run the FFT-domain erasure decoder (0 = never; default 4) */
 #define CEC_OPT_FFTDEC_MODE 8   /* RS(32,32), rebuilds past CEC_OPT_FFTDEC_MIN: 0 = the FFT-domain
                                    decoder where its cost model beats the run-time matrix kernel
                                    (default), 1 = always the FFT-domain decoder */

@@ -707,7 +707,7 @@ def test_fftdec_matches_oracle(torch, cess, corc, ne, ln):
         torch.cuda.synchronize()
         assert np.array_equal(d_data.cpu().numpy(), data), ("data_only", fmin)
         assert np.array_equal(d_par.cpu().numpy(), want * one[None, k:, None]), ("data_only p", fmin)
-    enc.set_option(7, 5)
+    enc.set_option(7, 4)
     enc.set_option(8, 0)
 
 
@@ -753,6 +753,7 @@ def test_rtb_tuning_shapes_agree(torch, cess, corc, ne, ln):
         present[s, rng.choice(k + m, size=ne, replace=False)] = 0
     enc = cess.New(k, m, tuning=True)
     enc.set_option(4, 3)
+    enc.set_option(7, 0)  # the bit-plane kernel, never the FFT-domain decoder
     for v in [-1] + list(range(40, 50)):
         enc.set_option(2, v)
         d_data = to_dev(torch, data * present[:, :k, None])
