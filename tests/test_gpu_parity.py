@@ -460,6 +460,40 @@ def test_fft_more_segments_than_grid_y(torch, cess, corc):
     assert ok.sum() == nseg - 1 and not ok[nseg - 3]
 
 
+def test_fftdec_more_segments_than_grid_y(torch, cess):
+    """The FFT-domain decoder over 70,000 RS(32,32) segments of 1 KiB fragments: one pattern for
+    the whole batch, then per-segment patterns cycling over both sides and both size classes
+    (launches split at grid.y chunks, plans indexed per listed segment); every segment equals the
+    encoded original."""
+    k, m, ln, nseg = 32, 32, 1024, 70000
+    gen = torch.Generator(device="cuda").manual_seed(6)
+    d_data = torch.randint(0, 256, (nseg, k, ln), dtype=torch.uint8, device="cuda", generator=gen)
+    d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
+    enc = cess.New(k, m)
+    enc.EncodeBatch(d_data, d_par, nseg, ln)
+    ref_d, ref_p = d_data.clone(), d_par.clone()
+    rng = np.random.default_rng(70)
+    pats = []
+    for ne, lo, hi in ((8, 0, 64), (6, 0, 32), (6, 32, 64), (16, 0, 64), (12, 0, 64)):
+        p = np.ones(64, np.uint8)
+        p[lo + rng.choice(hi - lo, size=ne, replace=False)] = 0
+        pats.append(p)
+    enc.set_option(8, 1)  # every pattern on the decoder
+    before = enc.stat(4)
+    try:
+        for per_seg in (False, True):
+            present = np.stack([pats[s % len(pats)] for s in range(nseg)]) if per_seg else pats[0]
+            pm = torch.from_numpy(present if per_seg else present[None].repeat(nseg, 0)).cuda()
+            d_data.mul_(pm[:, :k, None])
+            d_par.mul_(pm[:, k:, None])
+            enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+            torch.cuda.synchronize()
+            assert torch.equal(d_data, ref_d) and torch.equal(d_par, ref_p), per_seg
+        assert enc.stat(4) - before == 2 * nseg
+    finally:
+        enc.set_option(8, 0)
+
+
 def test_encode_file_sharded_single_rank(tmp_path, orc):
     from cess_amd.segments import encode_file_sharded
     rng = np.random.default_rng(21)
