@@ -103,6 +103,7 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
   const auto rA = rsrc(baseA), rB = rsrc(baseB);
   const uint32_t ss = (uint32_t)L.shard_stride;
   const uint32_t lcol = (uint32_t)col + l * ss;  // this lane's byte offset of position 0 / 1
+  const uint32_t vst = (uint32_t)col + l * 512;   // its 16 bytes of an output row (packed form)
   const uint32_t presA = P[FftDecLayout::kPresA];
   const uint32_t nout = P[FftDecLayout::kNout];
 
@@ -231,8 +232,12 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
       uint32_t w[8];
       sfor<8>([&](auto Q) CEC_FFT_AI { w[Q] = FFT_BOP3(acc[Q], acc[Q] >> 4, 0x0F0F0F0Fu, kAndX); });
       tr8(w);
-      uint8_t* dst = ((od & 32) ? baseB : baseA) + col + (uint64_t)t * ss + l * 512;
-      __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4*>(dst));
+      // a buffer store: the shard offset is scalar, the lane's column offset the same every row
+      const u32x4 v = {w[0], w[1], w[2], w[3]};
+      if (od & 32)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rB, vst, t * ss, 2);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(v, rA, vst, t * ss, 2);
     }
   };
   // one row loop per slot count (NLO..NHI), selected by a bit test of the one-hot count (an equality
