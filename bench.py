@@ -368,14 +368,19 @@ def launch_ranks(n: int, argv) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def kernel_label(config: int, fd_frac, erasures: int, generic: bool, rt_mode: int, k: int) -> str:
+def kernel_label(config: int, fd_frac, erasures: int, generic: bool, rt_mode: int, k: int,
+                 fdd_frac=0) -> str:
     """The dominant kernel of a bench line. Config 6: fd_frac = share of the timed rebuilds the
-    library sent to the FFT-domain decoder (CEC_STAT_FFTDEC_SEGMENTS)."""
+    library sent to the FFT-domain decoders (CEC_STAT_FFTDEC_SEGMENTS), fdd_frac the share of them
+    on the formal-derivative one (CEC_STAT_FFTDEC_D_SEGMENTS)."""
     if config == 6:
-        name = ("k_fftdec_m" if fd_frac == 1 else
+        fdm = (fd_frac or 0) - (fdd_frac or 0)
+        name = ("k_fftdec_d" if fdd_frac == 1 else
+                "k_fftdec_m" if fd_frac == 1 and not fdd_frac else
                 "k_rthx<8>" if fd_frac == 0 and erasures > 4 else
                 "k_rtb" if fd_frac == 0 else
-                f"k_fftdec_m ({fd_frac:.0%} of segments) + k_rthx<8> (by pattern cost)")
+                f"k_fftdec_m ({fdm:.0%} of segments) + k_fftdec_d ({fdd_frac or 0:.0%}) + "
+                f"k_rthx<8> (by pattern cost)")
     else:
         name = {2: "k_ct<EncCT<2, 1>>",
                 3: "k_ct_dec1_mixed21 (Dec1CT<2, 1, e> / EncCT<2, 1> per segment)",
@@ -427,10 +432,12 @@ def wide_code_legs(dev, local, stream, nseg=64, reps=10) -> dict:
         pres = np.ones((nseg, k + m), np.uint8)
         for s_ in range(nseg):
             pres[s_, rng.choice(k + m, size=ne, replace=False)] = 0
-        fd0 = enc.stat(4)
+        fd0, fdd0 = enc.stat(4), enc.stat(5)
         leg(name, lambda: enc.ReconstructBatch(d_data, d_par, nseg, F, pres, stream=stream), ne)
         legs[name]["fftdec_segment_share"] = round(
             (enc.stat(4) - fd0) / (nseg * (reps + 2)), 3)
+        legs[name]["fftdec_d_segment_share"] = round(
+            (enc.stat(5) - fdd0) / (nseg * (reps + 2)), 3)
     d_ok = torch.empty(nseg, dtype=torch.uint8, device=dev)
     leg("verify", lambda: enc.VerifyBatch(d_data, d_par, nseg, F, d_ok=d_ok, stream=stream), m)
     torch.cuda.synchronize(dev)
@@ -473,9 +480,10 @@ def main() -> None:
     ap.add_argument("--fftdec-min", type=int, default=-1,
                     help="RS(32,32) rebuilds of at least this many shards run the FFT-domain "
                          "decoder (CEC_OPT_FFTDEC_MIN; 0 = never; -1 = library default)")
-    ap.add_argument("--fftdec-mode", type=int, default=0, choices=[0, 1],
-                    help="RS(32,32) rebuilds: 0 = FFT-domain decoder where its cost model beats "
-                         "k_rthx (library default), 1 = always (CEC_OPT_FFTDEC_MODE)")
+    ap.add_argument("--fftdec-mode", type=int, default=0, choices=[0, 1, 2],
+                    help="RS(32,32) rebuilds: 0 = the cost model's pick of the FFT-domain decoders "
+                         "and k_rthx (library default), 1 = always the syndrome-row decoder, "
+                         "2 = always the formal-derivative decoder (CEC_OPT_FFTDEC_MODE)")
     ap.add_argument("--erasures", type=int, default=0,
                     help="config 6: random erasures per segment (default m)")
     ap.add_argument("--lose-parity", action="store_true",
@@ -679,7 +687,8 @@ def main() -> None:
                               "GBps": round(nseg * per_seg / med / 1e6, 1)}), flush=True)
         return
 
-    fd_seg0 = enc.stat(4)  # segments the FFT-domain decoder rebuilt before this run
+    fd_seg0 = enc.stat(4)  # segments the FFT-domain decoders rebuilt before this run
+    fdd_seg0 = enc.stat(5)  # of those, the formal-derivative decoder
     for _ in range(args.warmup):
         step()
     drain()  # the timed region starts with an empty hash window and ends with it drained
@@ -711,6 +720,7 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     fd_seg1 = enc.stat(4)
+    fdd_seg1 = enc.stat(5)
 
     launch_ms = (float(np.mean([a.elapsed_time(b) for a, b in ev])) if per_step
                  else ev[0][0].elapsed_time(ev[0][1]) / args.steps)
@@ -783,13 +793,14 @@ def main() -> None:
                 "basis": "whole step (hash ticks share the chip with the encode); peak at 2.4 GHz"}
 
     # share of the timed rebuilds the library sent to the FFT-domain decoder (CEC_STAT 4)
-    fd_frac = None
+    fd_frac = fdd_frac = None
     if args.config == 6:
         fd_frac = (fd_seg1 - fd_seg0) / max(1, nseg * (args.steps + args.warmup))
         fd_frac = round(min(1.0, fd_frac), 4)
+        fdd_frac = round(min(1.0, (fdd_seg1 - fdd_seg0) / max(1, nseg * (args.steps + args.warmup))), 4)
     tag = f"c{args.config}"
     kernel_name = kernel_label(args.config, fd_frac, args.erasures or m, args.generic,
-                               args.rt_mode, k)
+                               args.rt_mode, k, fdd_frac)
     traffic = load_traffic(tag, bytes_step_gpu, kernel_name)
     out = {
         "metric": METRIC,

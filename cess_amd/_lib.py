@@ -148,6 +148,7 @@ CEC_STAT_DECODE_CACHED = 1
 CEC_STAT_RETIRED_PENDING = 2
 CEC_STAT_POOL_BYTES = 3
 CEC_STAT_FFTDEC_SEGMENTS = 4
+CEC_STAT_FFTDEC_D_SEGMENTS = 5
 CEC_HQOPT_TICK = 1
 CEC_DIST_ID_BYTES = 128
 CEC_DIST_SURVIVOR = 0

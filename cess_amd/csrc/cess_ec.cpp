@@ -186,6 +186,9 @@ struct Program {
   size_t fd_bytes = 0;
   int fd_side = 0;
   int fd_nrs = 0;  // syndrome slots of the plan (its row cost: outputs x slots)
+  // and as a formal-derivative plan (fftdec_plan_d: cost independent of the erasure count)
+  uint32_t* fdd = nullptr;
+  size_t fdd_bytes = 0;
   uint8_t in_idx[cec::kMaxShards] = {};   // survivors read (host copy)
   uint8_t out_idx[cec::kMaxShards] = {};  // shards written (host copy)
 };
@@ -243,11 +246,12 @@ using HostImages = PinnedArena;
 int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int nin,
                   const uint8_t* out_idx, int nout, const BigMat& coef, ProgPtr* out,
                   bool partial = false, HostImages* keep = nullptr,
-                  const cec::FftDecPlan* fdp = nullptr) {
+                  const cec::FftDecPlan* fdp = nullptr, const cec::FftDecPlan* fddp = nullptr) {
   DevPool* pp = &pool;
   std::shared_ptr<Program> prog(new Program, [pp](Program* p) {
     for (auto& c : p->chunks) pp->retire(c.dev, c.bytes);
     pp->retire(p->fd, p->fd_bytes);
+    pp->retire(p->fdd, p->fdd_bytes);
     delete p;
   });
   prog->nout = nout;
@@ -314,24 +318,34 @@ int build_program(DevPool& pool, hipStream_t upload, const uint8_t* in_idx, int 
     prog->chunks.push_back(c);
     HIP_TRY(hipMemcpyAsync(c.dev, h, c.bytes, hipMemcpyHostToDevice, upload));
   }
-  if (fdp) {  // the FFT-domain decode plan of the same pattern
-    const size_t bytes = fdp->w.size() * sizeof(uint32_t);
+  // the FFT-domain decode plans of the same pattern
+  auto upload_plan = [&](const cec::FftDecPlan& fp, uint32_t** dev, size_t* dbytes) -> int {
+    const size_t bytes = fp.w.size() * sizeof(uint32_t);
     uint32_t* h = keep ? keep->take(bytes) : nullptr;
     if (!h) {
-      hosts.emplace_back(fdp->w);
+      hosts.emplace_back(fp.w);
       h = hosts.back().data();
       staged = false;
     } else {
-      std::memcpy(h, fdp->w.data(), bytes);
+      std::memcpy(h, fp.w.data(), bytes);
     }
     void* d = nullptr;
     int rc = pool.alloc(bytes, &d);
     if (rc) return rc;
-    prog->fd = static_cast<uint32_t*>(d);
-    prog->fd_bytes = bytes;
+    *dev = static_cast<uint32_t*>(d);
+    *dbytes = bytes;
+    HIP_TRY(hipMemcpyAsync(*dev, h, bytes, hipMemcpyHostToDevice, upload));
+    return CEC_OK;
+  };
+  if (fdp) {
+    int rc = upload_plan(*fdp, &prog->fd, &prog->fd_bytes);
+    if (rc) return rc;
     prog->fd_side = fdp->side;
     prog->fd_nrs = fdp->nrslots;
-    HIP_TRY(hipMemcpyAsync(prog->fd, h, bytes, hipMemcpyHostToDevice, upload));
+  }
+  if (fddp) {
+    int rc = upload_plan(*fddp, &prog->fdd, &prog->fdd_bytes);
+    if (rc) return rc;
   }
   // the block may be a reused one whose readers have completed; the upload must land before
   // any caller-stream launch that reads it, and pageable images die here (arena images live
@@ -363,7 +377,7 @@ struct PsPlan {
   std::vector<PsLaunch> rt;
   size_t mixed_off = 0, mixed_count = 0;  // tagged list (segment | erased << 30), count 0: none
   struct FdLaunch {
-    int side;
+    int side;           // 0, 1: syndrome-row decoder of that side; 2: formal derivative
     bool big;           // cec::fftdec_big of the plans' syndrome slot count
     size_t off, count;  // segments list + per-segment FFT-domain plans (pointer array)
   };
@@ -382,8 +396,9 @@ struct cec_codec {
   bool force_generic = false;
   // RS(32,32) patterns with at least this many outputs take the FFT-domain decoder (0: never)
   int fftdec_min = 4;
-  int fftdec_mode = 0;  // 0: by the cost model (fftdec_cheaper), 1: every such rebuild
-  uint64_t fd_segments = 0;  // segments rebuilt by the FFT-domain decoder (CEC_STAT_FFTDEC_SEGMENTS)
+  int fftdec_mode = 0;  // 0: by the cost model (fftdec_choice), 1: syndrome rows, 2: derivative
+  uint64_t fd_segments = 0;  // segments rebuilt by the FFT-domain decoders (CEC_STAT_FFTDEC_SEGMENTS)
+  uint64_t fdd_segments = 0;  // of those, by the formal-derivative one (CEC_STAT_FFTDEC_D_SEGMENTS)
   DevPool pool;  // declared before every holder of pool blocks: destroyed after them
   ProgPtr encode;
   // decode programs by erasure pattern (n presence flags + data_only), least recently used last
@@ -549,11 +564,13 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* ou
   if (plan->nout > 0) {
     // RS(32,32) rebuilds of several shards: also the FFT-domain plan (picked at launch by the
     // codec's CEC_OPT_FFTDEC_MIN and the layout)
-    cec::FftDecPlan fdp;
-    const bool fd = c->k == 32 && c->m == 32 && plan->nout >= 2 &&
-                    cec::fftdec_plan_m(flags, data_only, &fdp);
+    cec::FftDecPlan fdp, fddp;
+    const bool wide = c->k == 32 && c->m == 32 && plan->nout >= 2;
+    const bool fd = wide && cec::fftdec_plan_m(flags, data_only, &fdp);
+    const bool fdd = wide && cec::fftdec_plan_d(flags, data_only, &fddp);
     int rc = build_program(c->pool, c->stream, plan->in_idx, c->k, plan->out_idx, plan->nout,
-                           plan->coef, &prog, false, keep, fd ? &fdp : nullptr);
+                           plan->coef, &prog, false, keep, fd ? &fdp : nullptr,
+                           fdd ? &fddp : nullptr);
     if (rc) return rc;
   } else {
     prog = std::make_shared<const Program>();
@@ -642,15 +659,24 @@ bool is_reencode(const cec_codec* c, const Program& p) {
 // ~3.8 us past four (two waves); k_rthx ~ 0.235 ms + 33.9 us per output; up to four outputs the
 // alternative is k_rtb, ~0.13 ms + 57 us per output (5.9 / 4.9 / 3.9 / 3.4 TB/s
 // at one to four outputs).
-bool fftdec_cheaper(int nout, int nrs) {
-  const long pairs = (long)nout * nrs;
-  if (nout <= 4) return 33 * pairs + 1660 < 570L * nout;
-  return cec::fftdec_big(nrs) ? 10 * pairs + 160 < 89L * nout : 10 * pairs + 186 < 103L * nout;
+// The formal-derivative decoder k_fftdec_d costs about the same at every pattern: ~kFddCost us.
+constexpr double kFddCost = 700.0;
+enum FdKind { kFdNone = 0, kFdM = 1, kFdD = 2 };
+int fftdec_choice(int nout, int nrs, bool has_m, bool has_d) {
+  const double alt = nout <= 4 ? 130.0 + 57.0 * nout : 235.0 + 33.9 * nout;
+  const double m = has_m ? 296.0 + (cec::fftdec_big(nrs) ? 3.8 : 3.3) * nout * nrs : 1e30;
+  const double d = has_d ? kFddCost : 1e30;
+  if (m < alt && m <= d) return kFdM;
+  if (d < alt) return kFdD;
+  return kFdNone;
 }
 
-bool use_fftdec(const cec_codec* c, const Program& p) {
-  if (c->force_generic || !p.fd || c->fftdec_min <= 0 || p.nout < c->fftdec_min) return false;
-  return c->fftdec_mode == 1 || fftdec_cheaper(p.nout, p.fd_nrs);
+int use_fftdec(const cec_codec* c, const Program& p) {
+  if (c->force_generic || (!p.fd && !p.fdd) || c->fftdec_min <= 0 || p.nout < c->fftdec_min)
+    return kFdNone;
+  if (c->fftdec_mode == 1) return p.fd ? kFdM : kFdNone;
+  if (c->fftdec_mode == 2) return p.fdd ? kFdD : kFdNone;
+  return fftdec_choice(p.nout, p.fd_nrs, p.fd != nullptr, p.fdd != nullptr);
 }
 
 int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* seg_list,
@@ -658,10 +684,12 @@ int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* s
   if (p.nout == 0 || nseg == 0 || L.len == 0) return CEC_OK;
   if (!c->force_generic && p.single < 0 && is_reencode(c, p))
     return do_encode(c, L, seg_list, nseg, st);
-  if (use_fftdec(c, p) &&
-      cec::launch_fftdec(L, p.fd_side, cec::fftdec_big(p.fd_nrs), p.fd, nullptr, seg_list,
-                         nseg, st)) {
+  const int fk = use_fftdec(c, p);
+  if ((fk == kFdM && cec::launch_fftdec(L, p.fd_side, cec::fftdec_big(p.fd_nrs), p.fd, nullptr,
+                                        seg_list, nseg, st)) ||
+      (fk == kFdD && cec::launch_fftdec_d(L, p.fdd, nullptr, seg_list, nseg, st))) {
     c->fd_segments += nseg;
+    if (fk == kFdD) c->fdd_segments += nseg;
     return check_launch();
   }
   if (c->force_generic || p.single < 0 ||
@@ -719,7 +747,7 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
     groups[it->second].second.push_back((uint32_t)s);
   }
   bool all_ct = !c->force_generic;
-  std::vector<std::pair<ProgPtr, const std::vector<uint32_t>*>> progs, reencode, fdg[4];
+  std::vector<std::pair<ProgPtr, const std::vector<uint32_t>*>> progs, reencode, fdg[5];
   // new patterns' program uploads stay in flight until the one synchronisation below (one per
   // plan, not per pattern: 64 new RS(32,32) patterns cost ~1 ms of waits otherwise); every return
   // path waits for them before their host images go
@@ -745,8 +773,13 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
       reencode.push_back({p, &g.second});  // the encode kernels, whatever the other groups take
       continue;
     }
-    if (fdok && use_fftdec(c, *p)) {  // RS(32,32) wide rebuilds: the FFT-domain decoder
+    const int fk = fdok ? use_fftdec(c, *p) : kFdNone;
+    if (fk == kFdM) {  // RS(32,32) wide rebuilds: the FFT-domain decoders
       fdg[p->fd_side * 2 + (cec::fftdec_big(p->fd_nrs) ? 1 : 0)].push_back({p, &g.second});
+      continue;
+    }
+    if (fk == kFdD) {
+      fdg[4].push_back({p, &g.second});
       continue;
     }
     progs.push_back({p, &g.second});
@@ -761,13 +794,13 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
   // the run-time launches index the segment list and the chunk-pointer array with one offset:
   // keep them aligned past the re-encode lists
   hp.resize(hl.size(), nullptr);
-  for (int cls = 0; cls < 4; ++cls) {  // side x size class: one launch each
+  for (int cls = 0; cls < 5; ++cls) {  // side x size class, and the derivative: one launch each
     if (fdg[cls].empty()) continue;
-    PsPlan::FdLaunch f{cls >> 1, (cls & 1) != 0, hl.size(), 0};
+    PsPlan::FdLaunch f{cls == 4 ? 2 : cls >> 1, (cls & 1) != 0, hl.size(), 0};
     for (auto& pr : fdg[cls])
       for (uint32_t sg : *pr.second) {
         hl.push_back(sg);
-        hp.push_back(pr.first->fd);
+        hp.push_back(cls == 4 ? pr.first->fdd : pr.first->fd);
         ++f.count;
       }
     plan->fd.push_back(f);
@@ -856,10 +889,14 @@ int launch_ps_plan(cec_codec* c, const PsPlan& p, const Layout& L, hipStream_t s
   }
   const uint32_t* const* ptrs = static_cast<const uint32_t* const*>(p.ptrs);
   for (const auto& f : p.fd) {
-    if (!cec::launch_fftdec(L, f.side, f.big, nullptr, ptrs + f.off, p.list + f.off,
-                            (uint32_t)f.count, st))
+    const bool ok = f.side == 2 ? cec::launch_fftdec_d(L, nullptr, ptrs + f.off, p.list + f.off,
+                                                       (uint32_t)f.count, st)
+                                : cec::launch_fftdec(L, f.side, f.big, nullptr, ptrs + f.off,
+                                                     p.list + f.off, (uint32_t)f.count, st);
+    if (!ok)
       return set_err(CEC_EINVAL, "FFT-domain decode plan on a layout it does not fit");
     c->fd_segments += f.count;
+    if (f.side == 2) c->fdd_segments += f.count;
     int rc = check_launch();
     if (rc) return rc;
   }
@@ -996,7 +1033,8 @@ int cec_set_option(cec_codec* c, int option, int value) {
       c->fftdec_min = value;
       return CEC_OK;
     case CEC_OPT_FFTDEC_MODE:
-      if (value < 0 || value > 1) return set_err(CEC_EINVAL, "fftdec mode is 0 (auto) or 1 (always)");
+      if (value < 0 || value > 2)
+        return set_err(CEC_EINVAL, "fftdec mode is 0 (auto), 1 (syndrome rows) or 2 (derivative)");
       c->fftdec_mode = value;
       return CEC_OK;
     case CEC_OPT_DECODE_CACHE:
@@ -1015,6 +1053,7 @@ int cec_get_stat(const cec_codec* c, int stat, uint64_t* value) {
     case CEC_STAT_RETIRED_PENDING: *value = c->pool.pending(); return CEC_OK;
     case CEC_STAT_POOL_BYTES: *value = c->pool.held(); return CEC_OK;
     case CEC_STAT_FFTDEC_SEGMENTS: *value = c->fd_segments; return CEC_OK;
+    case CEC_STAT_FFTDEC_D_SEGMENTS: *value = c->fdd_segments; return CEC_OK;
   }
   return set_err(CEC_EINVAL, "unknown stat");
 }

@@ -1,0 +1,314 @@
+// RS(32,32) erasure decode by the formal derivative (k_fftdec_d), gfx950: the rebuild whose cost
+// does not grow with the number of lost fragments. A miner exit marks every fragment the miner held
+// (c-pallets/file-bank/src/functions.rs:543-562), so a wide-coded segment can lose up to 32 of its
+// 64 fragments at once; the syndrome decoder (fftdec.hip) pays per (output, syndrome slot) and the
+// run-time matrix kernels per (output, input), while this one pays two 64-point transforms.
+//
+// Algorithm (plan: fftdec_plan_d in fftdec_plan.h). Points are shard indices 0..63, the GF(2)-span
+// of {1, 2, .., 32}; lam(x) = prod_{e erased} (x ^ e):
+//   X_t  = lam(t) c_t          (present shards; erased ones read as zeros)
+//   g    = IFFT_64(X)          (Lin-Chung-Han, novel polynomial basis, coset 0)
+//   g'   = D(g)                (formal derivative: D(Xhat_i) = sum_{bit j of i} c_j Xhat_{i - 2^j},
+//                               c_j = W_j'(0) / W_j(2^j), compile-time)
+//   c_e  = FFT_64(g')(e) / lam'(e)
+//
+// Layout: a quad of lanes (l = lane & 3) owns 32 byte columns of a segment; lane l holds positions
+// t = 4j + l, j = 0..15, as 8 bit planes each (128 VGPRs), so each skew of layers 1..5 depends only
+// on j (lane-uniform, compile-time). Layer 0's skew What_0(t & ~1) = t & ~1 has the lane's bit 1 in
+// it: the uniform part 4j plus 2 on lanes 2 and 3 (one masked doubling). Layers 0 and 1 pair lanes
+// through DPP quad_perm, layers 2..5 registers of one lane. A lane's 32 bytes of a shard are two
+// 16-byte pieces 256 bytes apart: each load or store of a wave's 16 lanes with the same l covers 256
+// contiguous bytes of one shard. The run-time multiplications by lam(t) and 1 / lam'(e) differ per
+// lane (position): Horner over the coefficient bits with each bit's mask made by one v_bfe_i32.
+#include <utility>
+
+#include "fft_core.h"
+#include "fftdec_plan.h"
+#include "kernels.h"
+
+#ifdef CEC_FDD_WAVES
+#define CEC_FDD_ATTR __attribute__((amdgpu_waves_per_eu(CEC_FDD_WAVES, CEC_FDD_WAVES)))
+#else
+#define CEC_FDD_ATTR
+#endif
+
+namespace cec {
+
+using namespace fftc;
+
+namespace {
+
+typedef const __attribute__((address_space(4))) uint32_t* cplan_t;
+
+// Loads and stores that a lane may skip go through a raw buffer resource: an out-of-range offset
+// reads zeros / drops the write without touching memory. Offsets are 32-bit: a coset's 32 shards
+// must span < 2 GiB (fftdec_layout_ok).
+constexpr uint32_t kOff = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, 0x7FFFFFFF,
+                                           0x00020000);
+}
+constexpr uint32_t kPiece = 256;  // distance of a lane's two 16-byte pieces
+__device__ __forceinline__ void bld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff,
+                                    uint32_t (&w)[8]) {
+  const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 2);  // nt
+  const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(r, voff + kPiece, soff, 2);
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff,
+                                    const uint32_t (&w)[8]) {
+  const u32x4 a = {w[0], w[1], w[2], w[3]}, b = {w[4], w[5], w[6], w[7]};
+  __builtin_amdgcn_raw_buffer_store_b128(a, r, voff, soff, 2);
+  __builtin_amdgcn_raw_buffer_store_b128(b, r, voff + kPiece, soff, 2);
+}
+
+// every plane of a slot materialised here (an empty asm that reads and writes them): phases and
+// slots start from complete registers, so the scheduler cannot interleave them into more live values
+__device__ __forceinline__ void fence(uint32_t (&x)[8]) {
+  asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
+               "+v"(x[6]), "+v"(x[7]));
+}
+__device__ __forceinline__ void fence_all(uint32_t (&X)[16][8]) {
+  sfor<16>([&](auto J) CEC_FFT_AI { fence(X[J]); });
+}
+// slot J's work starts once slot J - 1's last plane is written
+template <int J>
+__device__ __forceinline__ void after_prev(uint32_t (&X)[16][8]) {
+  if constexpr (J > 0) asm volatile("" : "+v"(X[J][0]) : "v"(X[J - 1][7]));
+}
+
+// quad partners: lane l reads lane l ^ 1 / l ^ 2
+__device__ __forceinline__ uint32_t qp1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);  // [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t qp2(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);  // [2,3,0,1]
+}
+
+struct Skews64 {
+  static constexpr LchSkews<6> s = lch_skews<6>(0);
+};
+
+// c_j = W_j'(0) / W_j(2^j): W_j is linearised, so its derivative is the constant prod of the
+// nonzero points of span(1, .., 2^(j-1))
+constexpr uint8_t lch_dconst(int j) {
+  uint8_t p = 1;
+  for (int a = 1; a < (1 << j); ++a) p = gf_mul(p, (uint8_t)a);
+  return gf_mul(p, gf_inv(lch_w(j, (uint8_t)(1u << j))));
+}
+template <int J>
+struct DConst {
+  static constexpr unsigned v = lch_dconst(J);
+};
+static_assert(lch_dconst(0) == 1, "c_0 = 1: the b = 0 term of the derivative is a plain XOR");
+
+// What_0 is linear: the skew of layer 0 on lanes 2, 3 is the uniform one ^ What_0(2) = ^ 2
+static_assert(lch_what(0, 2) == 2, "layer-0 skew delta of the quad's upper pair");
+
+// x ^= m & 2z (planes: 2z = z << 1 with 0x11D's taps 2, 3, 4 fed by plane 7)
+__device__ __forceinline__ void xtime_acc_masked(uint32_t (&x)[8], const uint32_t (&z)[8],
+                                                 uint32_t m) {
+  x[0] = FFT_BOP3(x[0], z[7], m, kXand);
+  x[1] = FFT_BOP3(x[1], z[0], m, kXand);
+  x[2] = FFT_BOP3(x[2], z[1] ^ z[7], m, kXand);
+  x[3] = FFT_BOP3(x[3], z[2] ^ z[7], m, kXand);
+  x[4] = FFT_BOP3(x[4], z[3] ^ z[7], m, kXand);
+  x[5] = FFT_BOP3(x[5], z[4], m, kXand);
+  x[6] = FFT_BOP3(x[6], z[5], m, kXand);
+  x[7] = FFT_BOP3(x[7], z[6], m, kXand);
+}
+
+// x = c * x for a per-lane constant c (bits 0..7 of cv): Horner over c's bits, each bit's mask
+// (0 or ~0) from one v_bfe_i32
+__device__ __forceinline__ void mul_rt(uint32_t (&x)[8], uint32_t cv) {
+  uint32_t z[8], acc[8];
+  sfor<8>([&](auto Q) CEC_FFT_AI { z[Q] = x[Q]; });
+  {
+    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)cv, 7, 1);
+    sfor<8>([&](auto Q) CEC_FFT_AI { acc[Q] = z[Q] & m; });
+  }
+  sfor<7>([&](auto B) CEC_FFT_AI {
+    constexpr int b = 6 - B;
+    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)cv, b, 1);
+    const uint32_t a7 = acc[7];
+    sfor<7>([&](auto Q) CEC_FFT_AI { acc[7 - Q] = acc[6 - Q]; });
+    acc[0] = a7;
+    acc[2] ^= a7;
+    acc[3] ^= a7;
+    acc[4] ^= a7;
+    sfor<8>([&](auto Q) CEC_FFT_AI { acc[Q] = FFT_BOP3(acc[Q], z[Q], m, kXand); });
+  });
+  sfor<8>([&](auto Q) CEC_FFT_AI { x[Q] = acc[Q]; });
+}
+
+// IFFT_64 (values -> coefficients), layer i: b ^= a; a ^= s*b. e1 / e2: lanes with bit 0 / bit 1
+// of l clear (the lower position of a layer-0 / layer-1 pair); hi = ~e2.
+__device__ __forceinline__ void ifft64(uint32_t (&X)[16][8], uint32_t e1, uint32_t e2,
+                                       uint32_t hi) {
+  using S = Skews64;
+  // layer 0 (lanes l, l ^ 1). Z = a ^ b on both lanes; lower -> a ^ s*Z, upper -> Z
+  sfor<16>([&](auto J) CEC_FFT_AI {
+    constexpr unsigned s = S::s.s[0][2 * J];
+    static_assert(S::s.s[0][2 * J + 1] == (s ^ 2u), "layer-0 skew is linear in t");
+    after_prev<J>(X);
+    uint32_t Z[8];
+    sfor<8>([&](auto Q) CEC_FFT_AI { Z[Q] = X[J][Q] ^ qp1(X[J][Q]); });
+    if constexpr (s == 0) {
+      sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] ^= Z[Q]; });
+    } else {
+      mul_acc<s, true>(X[J], Z, Z);  // X ^ Z ^ s*Z
+    }
+    xtime_acc_masked(X[J], Z, hi);  // lanes 2, 3: the skew's extra 2
+    sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] = FFT_BOP3(Z[Q], e1, X[J][Q], kXand); });
+  });
+  // layer 1 (lanes l, l ^ 2): skew What_1(4j), uniform
+  sfor<16>([&](auto J) CEC_FFT_AI {
+    constexpr unsigned s = S::s.s[1][J];
+    after_prev<J>(X);
+    uint32_t Z[8];
+    sfor<8>([&](auto Q) CEC_FFT_AI { Z[Q] = X[J][Q] ^ qp2(X[J][Q]); });
+    if constexpr (s == 0) {
+      sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] = FFT_BOP3(e2, X[J][Q], Z[Q], kSel); });
+    } else {
+      mul_acc<s, true>(X[J], Z, Z);
+      sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] = FFT_BOP3(Z[Q], e2, X[J][Q], kXand); });
+    }
+  });
+  // layers 2..5 (in-lane: registers j and j + 2^(i-2)); block of position 4j: j >> (i - 1)
+  sfor<4>([&](auto I2) CEC_FFT_AI {
+    constexpr int i = I2 + 2, hj = 1 << (i - 2);
+    sfor<16>([&](auto J) CEC_FFT_AI {
+      if constexpr (!(J & hj)) {
+        constexpr unsigned s = S::s.s[i][J >> (i - 1)];
+        sfor<8>([&](auto Q) CEC_FFT_AI { X[J + hj][Q] = x2(X[J + hj][Q], X[J][Q]); });
+        if constexpr (s != 0) mul_acc<s, false>(X[J], X[J + hj], X[J]);
+      }
+    });
+  });
+}
+
+// FFT_64 (coefficients -> values), layer i: a ^= s*b; b ^= a (i = 5 .. 0).
+__device__ __forceinline__ void fft64(uint32_t (&X)[16][8], uint32_t e1, uint32_t e2,
+                                      uint32_t hi) {
+  using S = Skews64;
+  sfor<4>([&](auto I2) CEC_FFT_AI {
+    constexpr int i = 5 - I2, hj = 1 << (i - 2);
+    sfor<16>([&](auto J) CEC_FFT_AI {
+      if constexpr (!(J & hj)) {
+        constexpr unsigned s = S::s.s[i][J >> (i - 1)];
+        if constexpr (s != 0) mul_acc<s, false>(X[J], X[J + hj], X[J]);
+        sfor<8>([&](auto Q) CEC_FFT_AI { X[J + hj][Q] = x2(X[J + hj][Q], X[J][Q]); });
+      }
+    });
+  });
+  // layer 1 (lanes l, l ^ 2). P = b on both lanes: lower -> a ^ s*P, upper -> b ^ a ^ s*P
+  sfor<16>([&](auto J) CEC_FFT_AI {
+    constexpr unsigned s = S::s.s[1][J];
+    after_prev<J>(X);
+    uint32_t P[8];
+    sfor<8>([&](auto Q) CEC_FFT_AI {
+      const uint32_t y = qp2(X[J][Q]);
+      P[Q] = FFT_BOP3(e2, y, X[J][Q], kSel);
+      X[J][Q] = FFT_BOP3(X[J][Q], ~e2, y, kXand);
+    });
+    if constexpr (s != 0) mul_acc<s, false>(X[J], P, P);
+  });
+  // layer 0 (lanes l, l ^ 1), skew uniform part plus 2 on lanes 2, 3
+  sfor<16>([&](auto J) CEC_FFT_AI {
+    constexpr unsigned s = S::s.s[0][2 * J];
+    after_prev<J>(X);
+    uint32_t P[8];
+    sfor<8>([&](auto Q) CEC_FFT_AI {
+      const uint32_t y = qp1(X[J][Q]);
+      P[Q] = FFT_BOP3(e1, y, X[J][Q], kSel);
+      X[J][Q] = FFT_BOP3(X[J][Q], ~e1, y, kXand);
+    });
+    if constexpr (s != 0) mul_acc<s, false>(X[J], P, P);
+    xtime_acc_masked(X[J], P, hi);
+  });
+}
+
+// g'[t] = XOR over the bits b not set in t of c_b g[t + 2^b], in place in ascending j (every
+// term reads a higher register, or this register of another lane, before it is overwritten)
+__device__ __forceinline__ void derivative(uint32_t (&X)[16][8], uint32_t e1, uint32_t e2) {
+  sfor<16>([&](auto J) CEC_FFT_AI {
+    after_prev<J>(X);
+    uint32_t acc[8], z[8];
+    sfor<8>([&](auto Q) CEC_FFT_AI {
+      acc[Q] = qp1(X[J][Q]) & e1;  // b = 0: c_0 = 1, partner t + 1 on lanes with bit 0 clear
+      z[Q] = qp2(X[J][Q]) & e2;    // b = 1: t + 2 on lanes with bit 1 clear
+    });
+    mul_acc<DConst<1>::v, false>(acc, z, z);
+    sfor<4>([&](auto B) CEC_FFT_AI {  // b = B + 2: register j + 2^B
+      if constexpr (!((J >> B) & 1)) mul_acc<DConst<B + 2>::v, false>(acc, X[J + (1 << B)], acc);
+    });
+    sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] = acc[Q]; });
+  });
+}
+
+__global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const uint32_t* __restrict__ plan1,
+                                                  const uint32_t* const* __restrict__ plans,
+                                                  const uint32_t* __restrict__ seg_list,
+                                                  uint32_t seg0) {
+  const uint32_t y = seg0 + blockIdx.y;
+  const uint32_t seg = seg_list ? seg_list[y] : y;
+  const cplan_t P = (cplan_t)(plans ? plans[y] : plan1);
+  const uint64_t gq = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 2;  // quad
+  const uint64_t col = (gq >> 4) * 512 + (gq & 15) * 16;
+  if (col >= L.len) return;  // whole waves leave together (len % 512 == 0)
+  const uint32_t l = threadIdx.x & 3;
+  const uint32_t e1 = (l & 1) ? 0u : 0xFFFFFFFFu, e2 = (l & 2) ? 0u : 0xFFFFFFFFu, hi = ~e2;
+  const uint32_t ss = (uint32_t)L.shard_stride;
+  const auto rD = rsrc(L.data + seg * L.data_seg_stride);
+  const auto rP = rsrc(L.parity + seg * L.par_seg_stride);
+  const uint32_t lcol = (uint32_t)col + l * ss;  // this lane's byte offset of position 4j + l
+  const uint32_t sh = 8 * l;
+
+  uint32_t X[16][8];
+  // present shards, each times lam(t) (an erased shard loads as zeros: lam(t) = 0 there)
+  sfor<16>([&](auto J) CEC_FFT_AI {
+    const uint32_t lw = P[FftDecDLayout::kLam + J];
+    const uint32_t voff = ((lw >> sh) & 0xFF) ? lcol : kOff;
+    bld(J < 8 ? rD : rP, voff, (uint32_t)(4 * (J & 7)) * ss, X[J]);
+  });
+  sfor<16>([&](auto J) CEC_FFT_AI {
+    after_prev<J>(X);
+    tr8(X[J]);
+    mul_rt(X[J], P[FftDecDLayout::kLam + J] >> sh);
+  });
+  fence_all(X);
+  ifft64(X, e1, e2, hi);
+  fence_all(X);
+  derivative(X, e1, e2);
+  fence_all(X);
+  fft64(X, e1, e2, hi);
+  fence_all(X);
+  // outputs: times 1 / lam'(e), back to bytes, stored by the lanes whose position is an output
+  sfor<16>([&](auto J) CEC_FFT_AI {
+    const uint32_t dw = P[FftDecDLayout::kDinv + J];
+    after_prev<J>(X);
+    if (dw) {
+      mul_rt(X[J], dw >> sh);
+      tr8(X[J]);
+      const uint32_t voff = ((dw >> sh) & 0xFF) ? lcol : kOff;
+      bst(J < 8 ? rD : rP, voff, (uint32_t)(4 * (J & 7)) * ss, X[J]);
+    }
+  });
+}
+
+}  // namespace
+
+bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* const* plans,
+                     const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+  if (!fftdec_layout_ok(L)) return false;
+  const uint64_t gx = (L.len / 512 * 64 + 255) / 256;
+  for (uint32_t s0 = 0; s0 < nseg; s0 += 65535) {
+    const uint32_t ny = nseg - s0 < 65535 ? nseg - s0 : 65535;
+    hipLaunchKernelGGL(k_fftdec_d, dim3((unsigned)gx, ny), dim3(256), 0, st, L, plan1, plans,
+                       seg_list, s0);
+  }
+  return true;
+}
+
+}  // namespace cec

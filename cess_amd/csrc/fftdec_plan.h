@@ -203,4 +203,55 @@ inline bool fftdec_plan_m(const uint8_t* present, bool data_only, FftDecPlan* ou
   return true;
 }
 
+// ---- mode D: the formal-derivative decoder (k_fftdec_d, fftdec_d.hip) ---------------------------
+// Lin-Chung-Han erasure decoding over the whole 64-point space (points = shard indices): with E the
+// erased set and the error locator lam(x) = prod_{e in E} (x ^ e), g = lam * f has degree < 64 and
+// its values lam(t) c_t at every point are known (zero on E). So
+//   g   = IFFT_64(lam(t) c_t)               (novel-basis coefficients of g)
+//   g'  = formal derivative of g            (compile-time constants, fftdec_d.hip)
+//   c_e = FFT_64(g')(e) / lam'(e)           (lam(e) = 0, so g'(e) = lam'(e) f(e))
+// Its cost does not depend on how many shards are lost: two 64-point transforms, the derivative,
+// and per position one run-time multiplication in (lam(t)) and one out (1 / lam'(e)).
+// Plan words (uint32), per register slot j of the kernel (positions 4j + l, l = 0..3 the lane of
+// a quad), byte l of the word belongs to position 4j + l.
+struct FftDecDLayout {
+  static constexpr int kFlags = 0;  // bits 8..15: mode (1 = D)
+  static constexpr int kNout = 1;
+  static constexpr int kLam = 16;   // [16]: lam(t) of present t, 0 for an erased one
+  static constexpr int kDinv = 32;  // [16]: 1 / lam'(t) of an output t, 0 elsewhere
+  static constexpr int kWords = 48;
+};
+
+// Build the mode-D plan for RS(32,32) pattern `present` (64 flags). False when more than 32 shards
+// are erased or there is nothing to write.
+inline bool fftdec_plan_d(const uint8_t* present, bool data_only, FftDecPlan* out) {
+  int ne = 0, nout = 0;
+  uint8_t erased[64];
+  for (int t = 0; t < 64; ++t)
+    if (!present[t]) erased[ne++] = (uint8_t)t;
+  if (ne == 0 || ne > 32) return false;
+  FftDecPlan p;
+  p.side = 0;
+  p.w.assign(FftDecDLayout::kWords, 0u);
+  uint32_t* w = p.w.data();
+  w[FftDecDLayout::kFlags] = 1u << 8;
+  for (int t = 0; t < 64; ++t) {
+    uint8_t lam = 1;  // lam(t), or lam'(t) = prod_{e != t} (t ^ e) at an erased t
+    for (int i = 0; i < ne; ++i)
+      if (erased[i] != t) lam = gf_mul(lam, (uint8_t)(t ^ erased[i]));
+    const int sh = 8 * (t & 3);
+    if (present[t]) {
+      w[FftDecDLayout::kLam + (t >> 2)] |= (uint32_t)lam << sh;
+    } else if (!(data_only && t >= 32)) {
+      w[FftDecDLayout::kDinv + (t >> 2)] |= (uint32_t)gf_inv(lam) << sh;
+      ++nout;
+    }
+  }
+  if (!nout) return false;
+  w[FftDecDLayout::kNout] = (uint32_t)nout;
+  p.nout = nout;
+  *out = std::move(p);
+  return true;
+}
+
 }  // namespace cec

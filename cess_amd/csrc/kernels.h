@@ -88,6 +88,9 @@ bool fftdec_big(int nrs);
 bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
                    const uint32_t* const* plans, const uint32_t* seg_list, uint32_t nseg,
                    hipStream_t st);
+// The formal-derivative decoder (fftdec_d.hip, plans of fftdec_plan_d): same arguments, any side.
+bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* const* plans,
+                     const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
 
 // Whether a compile-time single-erasure decode kernel exists for (k, m, missing).
 bool has_decode_ct(int k, int m, int missing);

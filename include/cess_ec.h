@@ -394,9 +394,10 @@ int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t s
                                    per erasure pattern (default 4096) */
 #define CEC_OPT_FFTDEC_MIN 7    /* RS(32,32): rebuilds of at least this many shards per segment
                                    may run the FFT-domain erasure decoder (0 = never; default 4) */
-#define CEC_OPT_FFTDEC_MODE 8   /* RS(32,32), rebuilds past CEC_OPT_FFTDEC_MIN: 0 = the FFT-domain
-                                   decoder where its cost model beats the run-time matrix kernel
-                                   (default), 1 = always the FFT-domain decoder */
+#define CEC_OPT_FFTDEC_MODE 8   /* RS(32,32), rebuilds past CEC_OPT_FFTDEC_MIN: 0 = the cheapest
+                                   of the FFT-domain decoders (syndrome rows, formal derivative) and
+                                   the run-time matrix kernel by the cost model (default), 1 = always
+                                   the syndrome-row decoder, 2 = always the formal-derivative one */
 int cec_set_option(cec_codec* codec, int option, int value);
 /* Counters (tests / monitoring). */
 #define CEC_STAT_DECODE_CACHED 1   /* erasure patterns in the decode cache */
@@ -405,8 +406,9 @@ int cec_set_option(cec_codec* codec, int option, int value);
 #define CEC_STAT_POOL_BYTES 3      /* HBM held by the codec's block pool (programs, plans, small
                                       scratch); batch-sized scratch is stream-ordered and is not
                                       held after the call's launches complete */
-#define CEC_STAT_FFTDEC_SEGMENTS 4 /* segments rebuilt by the RS(32,32) FFT-domain decoder so far
+#define CEC_STAT_FFTDEC_SEGMENTS 4 /* segments rebuilt by the RS(32,32) FFT-domain decoders so far
                                       (the rest of a rebuild ran the run-time matrix kernels) */
+#define CEC_STAT_FFTDEC_D_SEGMENTS 5 /* of those, segments rebuilt by the formal-derivative decoder */
 int cec_get_stat(const cec_codec* codec, int stat, uint64_t* value);
 
 #ifdef __cplusplus

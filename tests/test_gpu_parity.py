@@ -461,7 +461,7 @@ def test_fft_more_segments_than_grid_y(torch, cess, corc):
 
 
 def test_fftdec_more_segments_than_grid_y(torch, cess):
-    """The FFT-domain decoder over 70,000 RS(32,32) segments of 1 KiB fragments: one pattern for
+    """The FFT-domain decoders over 70,000 RS(32,32) segments of 1 KiB fragments: one pattern for
     the whole batch, then per-segment patterns cycling over both sides and both size classes
     (launches split at grid.y chunks, plans indexed per listed segment); every segment equals the
     encoded original."""
@@ -478,18 +478,18 @@ def test_fftdec_more_segments_than_grid_y(torch, cess):
         p = np.ones(64, np.uint8)
         p[lo + rng.choice(hi - lo, size=ne, replace=False)] = 0
         pats.append(p)
-    enc.set_option(8, 1)  # every pattern on the decoder
     before = enc.stat(4)
     try:
-        for per_seg in (False, True):
+        for mode, per_seg in ((1, False), (1, True), (2, False), (2, True)):
+            enc.set_option(8, mode)  # every pattern on that decoder (syndrome rows / derivative)
             present = np.stack([pats[s % len(pats)] for s in range(nseg)]) if per_seg else pats[0]
             pm = torch.from_numpy(present if per_seg else present[None].repeat(nseg, 0)).cuda()
             d_data.mul_(pm[:, :k, None])
             d_par.mul_(pm[:, k:, None])
             enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
             torch.cuda.synchronize()
-            assert torch.equal(d_data, ref_d) and torch.equal(d_par, ref_p), per_seg
-        assert enc.stat(4) - before == 2 * nseg
+            assert torch.equal(d_data, ref_d) and torch.equal(d_par, ref_p), (mode, per_seg)
+        assert enc.stat(4) - before == 4 * nseg
     finally:
         enc.set_option(8, 0)
 
@@ -710,13 +710,15 @@ def _wide_patterns(rng, nseg, ne):
     return present
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("ne", [2, 3, 5, 8, 13, 16, 24, 31, 32])
 @pytest.mark.parametrize("ln", [1024, 8192, 3 * 1024 + 512 * 2])
-def test_fftdec_matches_oracle(torch, cess, corc, ne, ln):
-    """RS(32,32) rebuilds on the FFT-domain erasure decoder (fftdec.hip: T1 transform, syndromes,
-    bit-plane run-time rows) are bit-exact with the C oracle's codeword: per-segment patterns on
-    both sides (data / parity / mixed erasures), one pattern for the whole batch, data_only, and
-    the same bytes as the run-time matrix kernels (CEC_OPT_FFTDEC_MIN = 0)."""
+def test_fftdec_matches_oracle(torch, cess, corc, ne, ln, mode):
+    """RS(32,32) rebuilds on the FFT-domain erasure decoders (mode 1, fftdec.hip: T1 transform,
+    syndromes, bit-plane run-time rows; mode 2, fftdec_d.hip: the formal-derivative decoder over
+    64-point transforms) are bit-exact with the C oracle's codeword: per-segment patterns on both
+    sides (data / parity / mixed erasures), one pattern for the whole batch, data_only, and the
+    same bytes as the run-time matrix kernels (CEC_OPT_FFTDEC_MIN = 0)."""
     k = m = 32
     nseg = 8
     rng = np.random.default_rng(ne * 7 + ln)
@@ -724,7 +726,8 @@ def test_fftdec_matches_oracle(torch, cess, corc, ne, ln):
     want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
     present = _wide_patterns(rng, nseg, ne)
     enc = cess.New(k, m)
-    enc.set_option(8, 1)  # every FFT-domain-eligible rebuild on the decoder (no cost model)
+    enc.set_option(8, mode)  # every FFT-domain-eligible rebuild on that decoder (no cost model)
+    before = enc.stat(4)
     for fmin in (2, 0):  # the FFT-domain decoder from two outputs, then never
         enc.set_option(7, fmin)
         d_data = to_dev(torch, data * present[:, :k, None])
@@ -741,15 +744,18 @@ def test_fftdec_matches_oracle(torch, cess, corc, ne, ln):
         torch.cuda.synchronize()
         assert np.array_equal(d_data.cpu().numpy(), data), ("data_only", fmin)
         assert np.array_equal(d_par.cpu().numpy(), want * one[None, k:, None]), ("data_only p", fmin)
+        if fmin:  # the per-segment call ran on the decoder (data_only may leave < 2 outputs)
+            assert enc.stat(4) - before >= nseg, mode
     enc.set_option(7, 4)
     enc.set_option(8, 0)
 
 
 @pytest.mark.parametrize("ne", [8, 32])
 def test_fftdec_dispatch_by_cost(torch, cess, corc, ne):
-    """CEC_OPT_FFTDEC_MODE 0 (the default) sends a random RS(32,32) pattern to the FFT-domain
-    decoder only where its cost model beats k_rthx (eight erasures: the decoder; 32 with 16
-    syndrome slots: the matrix kernel), counted by CEC_STAT_FFTDEC_SEGMENTS; bit-exact either way."""
+    """CEC_OPT_FFTDEC_MODE 0 (the default) sends a random RS(32,32) pattern to the cheapest of the
+    FFT-domain decoders and k_rthx by the cost model (eight erasures: the syndrome-row decoder; 32
+    with 16 syndrome slots: the formal-derivative decoder, no longer the matrix kernel), counted by
+    CEC_STAT_FFTDEC_SEGMENTS; bit-exact either way."""
     k = m = 32
     nseg, ln = 6, 4096
     rng = np.random.default_rng(500 + ne)
@@ -771,7 +777,7 @@ def test_fftdec_dispatch_by_cost(torch, cess, corc, ne):
     assert np.array_equal(d_data.cpu().numpy(), data)
     assert np.array_equal(d_par.cpu().numpy(), want)
     on_fd = enc.stat(4) - before
-    assert on_fd == (nseg if ne == 8 else 0), on_fd
+    assert on_fd == nseg, on_fd
 
 
 @pytest.mark.parametrize("ne,ln", [(1, 4096 + 3), (2, (1 << 16) + 16), (3, 4096 + 3), (4, 999)])
