@@ -90,13 +90,6 @@ struct Skews64 {
   static constexpr LchSkews<6> s = lch_skews<6>(0);
 };
 
-// c_j = W_j'(0) / W_j(2^j): W_j is linearised, so its derivative is the constant prod of the
-// nonzero points of span(1, .., 2^(j-1))
-constexpr uint8_t lch_dconst(int j) {
-  uint8_t p = 1;
-  for (int a = 1; a < (1 << j); ++a) p = gf_mul(p, (uint8_t)a);
-  return gf_mul(p, gf_inv(lch_w(j, (uint8_t)(1u << j))));
-}
 template <int J>
 struct DConst {
   static constexpr unsigned v = lch_dconst(J);

@@ -260,6 +260,14 @@ constexpr LchSkews<K> lch_skews(uint8_t beta) {
       r.s[i][b] = lch_what(i, (uint8_t)((b << (i + 1)) ^ beta));
   return r;
 }
+// Formal derivative in the novel basis: D(Xhat_i) = sum_{bit j of i} c_j Xhat_{i - 2^j} with
+// c_j = What_j' = W_j'(0) / W_j(v_j). W_j is linearised, so its derivative is the constant
+// prod of the nonzero points of span(v_0..v_{j-1}).
+constexpr uint8_t lch_dconst(int j) {
+  uint8_t p = 1;
+  for (int a = 1; a < (1 << j); ++a) p = gf_mul(p, (uint8_t)a);
+  return gf_mul(p, gf_inv(lch_w(j, (uint8_t)(1u << j))));
+}
 // GF(2) matrix of x -> c*x on bit planes: row q = mask of input bits p whose product c * 2^p has
 // bit q (plane q of c*x = XOR of planes p in row q).
 struct BitMatrix {

@@ -5,6 +5,9 @@
 // slot's even / odd position), including the register-slot swaps that bring the R slots to the
 // front and the Horner pass over each row's coefficient bits. Compared with the codeword of the product's own encode matrix for
 // random erasure patterns of 1..32 shards, both sides, with and without data_only.
+// The formal-derivative decoder's plans (fftdec_plan_d, kernel cess_amd/csrc/fftdec_d.hip) run
+// through the same patterns: lam(t) c_t from the plan's bytes, the 64-point IFFT, the derivative
+// with gf256.h's constants, the 64-point FFT, times the plan's 1 / lam'(e) at every output.
 // Build: g++ -std=c++20 -O1 -fconstexpr-ops-limit=2000000000 fftdec_model.cpp
 #include <cstdio>
 #include <cstdlib>
@@ -37,6 +40,58 @@ static void fft(uint8_t* v, unsigned beta) {
       }
   }
 }
+static void ifft64(uint8_t* v) {
+  const LchSkews<6> S = lch_skews<6>(0);
+  for (int i = 0; i < 6; ++i) {
+    const int h = 1 << i;
+    for (int b0 = 0; b0 < 64; b0 += 2 * h)
+      for (int t = b0; t < b0 + h; ++t) {
+        v[t + h] ^= v[t];
+        v[t] ^= gf_mul(S.s[i][b0 >> (i + 1)], v[t + h]);
+      }
+  }
+}
+static void fft64(uint8_t* v) {
+  const LchSkews<6> S = lch_skews<6>(0);
+  for (int i = 5; i >= 0; --i) {
+    const int h = 1 << i;
+    for (int b0 = 0; b0 < 64; b0 += 2 * h)
+      for (int t = b0; t < b0 + h; ++t) {
+        v[t] ^= gf_mul(S.s[i][b0 >> (i + 1)], v[t + h]);
+        v[t + h] ^= v[t];
+      }
+  }
+}
+// mode D on one byte column: the fails it finds
+static int check_d(const uint8_t* present, bool data_only, const uint8_t* cw, int* cases) {
+  FftDecPlan p;
+  int want = 0, fails = 0;
+  for (int i = 0; i < 64; ++i) want += !present[i] && (!data_only || i < 32);
+  if (!fftdec_plan_d(present, data_only, &p)) return want ? 1 : 0;
+  const uint32_t* w = p.w.data();
+  if ((int)w[FftDecDLayout::kNout] != want || (w[FftDecDLayout::kFlags] >> 8 & 255) != 1) ++fails;
+  auto byte = [&](int base, int t) { return (uint8_t)(w[base + (t >> 2)] >> (8 * (t & 3))); };
+  uint8_t v[64], d[64] = {};
+  for (int t = 0; t < 64; ++t) {
+    const uint8_t lam = byte(FftDecDLayout::kLam, t);
+    if ((lam != 0) != (present[t] != 0)) ++fails;
+    v[t] = gf_mul(lam, cw[t]);
+  }
+  ifft64(v);
+  for (int i = 0; i < 64; ++i)
+    for (int j = 0; j < 6; ++j)
+      if (i >> j & 1) d[i - (1 << j)] ^= gf_mul(lch_dconst(j), v[i]);
+  fft64(d);
+  for (int t = 0; t < 64; ++t) {
+    const uint8_t di = byte(FftDecDLayout::kDinv, t);
+    const bool out = !present[t] && (!data_only || t < 32);
+    if ((di != 0) != out) ++fails;
+    if (!out) continue;
+    ++*cases;
+    if (gf_mul(d[t], di) != cw[t]) ++fails;
+  }
+  return fails;
+}
 // bit-sliced x -> 2x (poly 0x11D) on one byte
 static uint8_t xt(uint8_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1D : 0)); }
 
@@ -47,7 +102,7 @@ int main() {
   static BigW work;
   if (!gf_encode_matrix(32, 32, E, top, topinv, work)) return 2;
   std::mt19937_64 rng(12345);
-  int fails = 0, cases = 0;
+  int fails = 0, cases = 0, dfails = 0, dcases = 0;
   for (int trial = 0; trial < 600; ++trial) {
     const int e = trial < 64 ? 1 + trial % 32 : 1 + (int)(rng() % 32);
     uint8_t present[64];
@@ -63,6 +118,18 @@ int main() {
     if (trial % 7 == 3)  // a structured pattern: the first e shards of one coset
       for (int i = 0; i < 64; ++i) present[i] = !(i >= (trial & 32) && i < (trial & 32) + e);
     const bool data_only = trial % 3 == 1;
+    for (int col = 0; col < 4; ++col) {  // mode D
+      uint8_t cw[64];
+      for (int c = 0; c < 32; ++c) cw[c] = (uint8_t)rng();
+      for (int r = 32; r < 64; ++r) {
+        uint8_t a = 0;
+        for (int c = 0; c < 32; ++c) a ^= gf_mul(E.v[r][c], cw[c]);
+        cw[r] = a;
+      }
+      const int f = check_d(present, data_only, cw, &dcases);
+      if (f && dfails < 10) std::printf("mode D mismatch trial %d e %d\n", trial, e);
+      dfails += f;
+    }
     FftDecPlan p;
     bool any_out = false;
     for (int i = 0; i < 64; ++i) any_out |= !present[i] && (!data_only || i < 32);
@@ -164,6 +231,7 @@ int main() {
       ++fails;
     }
   }
-  std::printf("fftdec model: %d outputs checked, %d failures\n", cases, fails);
-  return fails ? 1 : 0;
+  std::printf("fftdec model: %d outputs checked, %d failures; mode D: %d outputs, %d failures\n",
+              cases, fails, dcases, dfails);
+  return fails || dfails ? 1 : 0;
 }

@@ -155,15 +155,16 @@ def test_fftdec_plans_model(tmp_path):
     """The RS(32,32) FFT-domain decoder's plans (cess_amd/csrc/fftdec_plan.h) run through a CPU
     model of the kernel (T1 transform, syndromes, the bit-plane masks exactly as the kernel
     applies them) rebuild every erased shard of random patterns of 1..32 erasures, both sides,
-    with and without data_only, equal to the product's encode matrix
-    (tests/native/fftdec_model.cpp)."""
+    with and without data_only, equal to the product's encode matrix; the formal-derivative
+    decoder's plans (fftdec_plan_d) through the byte-level 64-point IFFT / derivative / FFT on the
+    same patterns (tests/native/fftdec_model.cpp)."""
     exe = str(tmp_path / "fftdec_model")
     subprocess.run(["g++", "-std=c++20", "-O1", "-fconstexpr-ops-limit=2000000000",
                     os.path.join(ROOT, "tests", "native", "fftdec_model.cpp"), "-o", exe],
                    check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-3000:]
-    assert "0 failures" in r.stdout
+    assert "0 failures; mode D:" in r.stdout and r.stdout.strip().endswith(" 0 failures")
 
 
 @pytest.mark.parametrize("k,flen", [(2, 4096), (2, 1000), (3, 64), (1, 77)])
@@ -295,7 +296,7 @@ def test_product_kernel_occupancy():
     3 waves per SIMD (<= 168 VGPRs), the one-wave hash tick at 4 (<= 128), the bit-plane restoral
     kernel k_rtb<1..2> at 6 or more (<= 80), the fused RS(32,32) verify and the FFT-domain
     erasure decoder for more than four syndrome slots at 2 (<= 224, <= 256), the decoder for up to
-    four at 3 (<= 168), none with scratch."""
+    four at 3 (<= 168), the formal-derivative decoder at 2 (<= 256), none with scratch."""
     import os
     import sys
     from cess_amd import _lib
@@ -305,7 +306,8 @@ def test_product_kernel_occupancy():
     res = sha_slots.kernel_resources(_lib.LIB_PATH)
     budget = {"k_fft3232I": 168, "k_sha256_tick1": 128, "k_ct_dec1_mixed21": 64,
               "k_rtbILi1E": 80, "k_rtbILi2E": 80, "k_fft3232_verify": 224,
-              "k_fftdec_m": 256, "k_fftdec_mILj0ELb0E": 168, "k_fftdec_mILj1ELb0E": 168}
+              "k_fftdec_m": 256, "k_fftdec_mILj0ELb0E": 168, "k_fftdec_mILj1ELb0E": 168,
+              "k_fftdec_d": 256}
     for pat, cap in budget.items():
         ks = {n: r for n, r in res.items() if pat in n}
         assert ks, pat
