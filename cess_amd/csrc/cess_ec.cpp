@@ -659,14 +659,19 @@ bool is_reencode(const cec_codec* c, const Program& p) {
 // ~3.8 us past four (two waves); k_rthx ~ 0.235 ms + 33.9 us per output; up to four outputs the
 // alternative is k_rtb, ~0.13 ms + 57 us per output (5.9 / 4.9 / 3.9 / 3.4 TB/s
 // at one to four outputs).
-// The formal-derivative decoder k_fftdec_d costs about the same at every pattern: ~kFddCost us.
-constexpr double kFddCost = 700.0;
+// The formal-derivative decoder k_fftdec_d costs nearly the same at every pattern: 0.69 ms at 8
+// outputs, 0.82 at 32 (the last FFT layers, the division and the stores only for slots holding
+// an output; profiles/r03/fdd_libs_ab1.jsonl).
+double fdd_cost(int nout) { return 647.0 + 5.4 * nout; }
 enum FdKind { kFdNone = 0, kFdM = 1, kFdD = 2 };
 int fftdec_choice(int nout, int nrs, bool has_m, bool has_d) {
   const double alt = nout <= 4 ? 130.0 + 57.0 * nout : 235.0 + 33.9 * nout;
   const double m = has_m ? 296.0 + (cec::fftdec_big(nrs) ? 3.8 : 3.3) * nout * nrs : 1e30;
-  const double d = has_d ? kFddCost : 1e30;
-  if (m < alt && m <= d) return kFdM;
+  const double d = has_d ? fdd_cost(nout) : 1e30;
+  // the syndrome-row decoder only with a 15 % margin over the derivative: a batch split between
+  // the two runs two smaller launches (24 random erasures: 0.854 ms split 34/66 by the bare
+  // costs, 0.797 all on the derivative)
+  if (m < alt && m < 0.85 * d) return kFdM;
   if (d < alt) return kFdD;
   return kFdNone;
 }

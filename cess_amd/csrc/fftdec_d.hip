@@ -26,11 +26,13 @@
 #include "fftdec_plan.h"
 #include "kernels.h"
 
-#ifdef CEC_FDD_WAVES
-#define CEC_FDD_ATTR __attribute__((amdgpu_waves_per_eu(CEC_FDD_WAVES, CEC_FDD_WAVES)))
-#else
-#define CEC_FDD_ATTR
+// Three waves per SIMD (<= 168 VGPRs, no scratch): measured 0.82 ms against 0.91 at the
+// compiler's own two for 32 random erasures of 64 x 512 KiB segments (profiles/r03/fdd_libs_ab1.jsonl).
+// -DCEC_FDD_WAVES=n for occupancy experiments.
+#ifndef CEC_FDD_WAVES
+#define CEC_FDD_WAVES 3
 #endif
+#define CEC_FDD_ATTR __attribute__((amdgpu_waves_per_eu(CEC_FDD_WAVES, CEC_FDD_WAVES)))
 
 namespace cec {
 
@@ -79,11 +81,21 @@ __device__ __forceinline__ void after_prev(uint32_t (&X)[16][8]) {
 }
 
 // quad partners: lane l reads lane l ^ 1 / l ^ 2
+// (DPP moves issue at half rate; -DCEC_FDD_SWZ moves them through the LDS crossbar instead:
+// ds_swizzle in quad-permute mode, no VALU issue slot)
 __device__ __forceinline__ uint32_t qp1(uint32_t v) {
+#ifdef CEC_FDD_SWZ
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x80B1);
+#else
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);  // [1,0,3,2]
+#endif
 }
 __device__ __forceinline__ uint32_t qp2(uint32_t v) {
+#ifdef CEC_FDD_SWZ
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x804E);
+#else
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);  // [2,3,0,1]
+#endif
 }
 
 struct Skews64 {
@@ -99,17 +111,20 @@ static_assert(lch_dconst(0) == 1, "c_0 = 1: the b = 0 term of the derivative is 
 // What_0 is linear: the skew of layer 0 on lanes 2, 3 is the uniform one ^ What_0(2) = ^ 2
 static_assert(lch_what(0, 2) == 2, "layer-0 skew delta of the quad's upper pair");
 
-// x ^= m & 2z (planes: 2z = z << 1 with 0x11D's taps 2, 3, 4 fed by plane 7)
+constexpr int kXandN = 0xB4;  // a ^ (b & ~c)
+
+// x ^= ~m & 2z (planes: 2z = z << 1 with 0x11D's taps 2, 3, 4 fed by plane 7); m = e2, so the
+// doubling lands on lanes 2 and 3
 __device__ __forceinline__ void xtime_acc_masked(uint32_t (&x)[8], const uint32_t (&z)[8],
                                                  uint32_t m) {
-  x[0] = FFT_BOP3(x[0], z[7], m, kXand);
-  x[1] = FFT_BOP3(x[1], z[0], m, kXand);
-  x[2] = FFT_BOP3(x[2], z[1] ^ z[7], m, kXand);
-  x[3] = FFT_BOP3(x[3], z[2] ^ z[7], m, kXand);
-  x[4] = FFT_BOP3(x[4], z[3] ^ z[7], m, kXand);
-  x[5] = FFT_BOP3(x[5], z[4], m, kXand);
-  x[6] = FFT_BOP3(x[6], z[5], m, kXand);
-  x[7] = FFT_BOP3(x[7], z[6], m, kXand);
+  x[0] = FFT_BOP3(x[0], z[7], m, kXandN);
+  x[1] = FFT_BOP3(x[1], z[0], m, kXandN);
+  x[2] = FFT_BOP3(x[2], z[1] ^ z[7], m, kXandN);
+  x[3] = FFT_BOP3(x[3], z[2] ^ z[7], m, kXandN);
+  x[4] = FFT_BOP3(x[4], z[3] ^ z[7], m, kXandN);
+  x[5] = FFT_BOP3(x[5], z[4], m, kXandN);
+  x[6] = FFT_BOP3(x[6], z[5], m, kXandN);
+  x[7] = FFT_BOP3(x[7], z[6], m, kXandN);
 }
 
 // x = c * x for a per-lane constant c (bits 0..7 of cv): Horner over c's bits, each bit's mask
@@ -135,10 +150,32 @@ __device__ __forceinline__ void mul_rt(uint32_t (&x)[8], uint32_t cv) {
   sfor<8>([&](auto Q) CEC_FFT_AI { x[Q] = acc[Q]; });
 }
 
+// The same with the 8 masks read from LDS (the plan's expanded masks of this lane and slot:
+// two 16-byte LDS reads instead of eight half-rate v_bfe_i32)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef const __attribute__((address_space(3))) u32x4 lds_u32x4;
+__device__ __forceinline__ void mul_rt_lds(uint32_t (&x)[8], const lds_u32* mk) {
+  const u32x4 lo = *reinterpret_cast<lds_u32x4*>(mk), hi = *reinterpret_cast<lds_u32x4*>(mk + 4);
+  const uint32_t m[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  uint32_t z[8], acc[8];
+  sfor<8>([&](auto Q) CEC_FFT_AI { z[Q] = x[Q]; });
+  sfor<8>([&](auto Q) CEC_FFT_AI { acc[Q] = z[Q] & m[7]; });
+  sfor<7>([&](auto B) CEC_FFT_AI {
+    constexpr int b = 6 - B;
+    const uint32_t a7 = acc[7];
+    sfor<7>([&](auto Q) CEC_FFT_AI { acc[7 - Q] = acc[6 - Q]; });
+    acc[0] = a7;
+    acc[2] ^= a7;
+    acc[3] ^= a7;
+    acc[4] ^= a7;
+    sfor<8>([&](auto Q) CEC_FFT_AI { acc[Q] = FFT_BOP3(acc[Q], z[Q], m[b], kXand); });
+  });
+  sfor<8>([&](auto Q) CEC_FFT_AI { x[Q] = acc[Q]; });
+}
+
 // IFFT_64 (values -> coefficients), layer i: b ^= a; a ^= s*b. e1 / e2: lanes with bit 0 / bit 1
-// of l clear (the lower position of a layer-0 / layer-1 pair); hi = ~e2.
-__device__ __forceinline__ void ifft64(uint32_t (&X)[16][8], uint32_t e1, uint32_t e2,
-                                       uint32_t hi) {
+// of l clear (the lower position of a layer-0 / layer-1 pair).
+__device__ __forceinline__ void ifft64(uint32_t (&X)[16][8], uint32_t e1, uint32_t e2) {
   using S = Skews64;
   // layer 0 (lanes l, l ^ 1). Z = a ^ b on both lanes; lower -> a ^ s*Z, upper -> Z
   sfor<16>([&](auto J) CEC_FFT_AI {
@@ -152,7 +189,7 @@ __device__ __forceinline__ void ifft64(uint32_t (&X)[16][8], uint32_t e1, uint32
     } else {
       mul_acc<s, true>(X[J], Z, Z);  // X ^ Z ^ s*Z
     }
-    xtime_acc_masked(X[J], Z, hi);  // lanes 2, 3: the skew's extra 2
+    xtime_acc_masked(X[J], Z, e2);  // lanes 2, 3: the skew's extra 2
     sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] = FFT_BOP3(Z[Q], e1, X[J][Q], kXand); });
   });
   // layer 1 (lanes l, l ^ 2): skew What_1(4j), uniform
@@ -181,9 +218,10 @@ __device__ __forceinline__ void ifft64(uint32_t (&X)[16][8], uint32_t e1, uint32
   });
 }
 
-// FFT_64 (coefficients -> values), layer i: a ^= s*b; b ^= a (i = 5 .. 0).
-__device__ __forceinline__ void fft64(uint32_t (&X)[16][8], uint32_t e1, uint32_t e2,
-                                      uint32_t hi) {
+// FFT_64 (coefficients -> values), layer i: a ^= s*b; b ^= a (i = 5 .. 0). Layers 5..2 here;
+// layers 1 and 0 pair the lanes of a quad on one register slot (fft64_tail), so the kernel runs
+// them only for the slots that hold an output.
+__device__ __forceinline__ void fft64_upper(uint32_t (&X)[16][8]) {
   using S = Skews64;
   sfor<4>([&](auto I2) CEC_FFT_AI {
     constexpr int i = 5 - I2, hj = 1 << (i - 2);
@@ -195,31 +233,31 @@ __device__ __forceinline__ void fft64(uint32_t (&X)[16][8], uint32_t e1, uint32_
       }
     });
   });
-  // layer 1 (lanes l, l ^ 2). P = b on both lanes: lower -> a ^ s*P, upper -> b ^ a ^ s*P
-  sfor<16>([&](auto J) CEC_FFT_AI {
+}
+template <int J>
+__device__ __forceinline__ void fft64_tail(uint32_t (&x)[8], uint32_t e1, uint32_t e2) {
+  using S = Skews64;
+  {  // layer 1 (lanes l, l ^ 2). P = b on both lanes: lower -> a ^ s*P, upper -> b ^ a ^ s*P
     constexpr unsigned s = S::s.s[1][J];
-    after_prev<J>(X);
     uint32_t P[8];
     sfor<8>([&](auto Q) CEC_FFT_AI {
-      const uint32_t y = qp2(X[J][Q]);
-      P[Q] = FFT_BOP3(e2, y, X[J][Q], kSel);
-      X[J][Q] = FFT_BOP3(X[J][Q], ~e2, y, kXand);
+      const uint32_t y = qp2(x[Q]);
+      P[Q] = FFT_BOP3(e2, y, x[Q], kSel);
+      x[Q] = FFT_BOP3(x[Q], y, e2, kXandN);
     });
-    if constexpr (s != 0) mul_acc<s, false>(X[J], P, P);
-  });
-  // layer 0 (lanes l, l ^ 1), skew uniform part plus 2 on lanes 2, 3
-  sfor<16>([&](auto J) CEC_FFT_AI {
+    if constexpr (s != 0) mul_acc<s, false>(x, P, P);
+  }
+  {  // layer 0 (lanes l, l ^ 1), skew uniform part plus 2 on lanes 2, 3
     constexpr unsigned s = S::s.s[0][2 * J];
-    after_prev<J>(X);
     uint32_t P[8];
     sfor<8>([&](auto Q) CEC_FFT_AI {
-      const uint32_t y = qp1(X[J][Q]);
-      P[Q] = FFT_BOP3(e1, y, X[J][Q], kSel);
-      X[J][Q] = FFT_BOP3(X[J][Q], ~e1, y, kXand);
+      const uint32_t y = qp1(x[Q]);
+      P[Q] = FFT_BOP3(e1, y, x[Q], kSel);
+      x[Q] = FFT_BOP3(x[Q], y, e1, kXandN);
     });
-    if constexpr (s != 0) mul_acc<s, false>(X[J], P, P);
-    xtime_acc_masked(X[J], P, hi);
-  });
+    if constexpr (s != 0) mul_acc<s, false>(x, P, P);
+    xtime_acc_masked(x, P, e2);
+  }
 }
 
 // g'[t] = XOR over the bits b not set in t of c_b g[t + 2^b], in place in ascending j (every
@@ -240,23 +278,47 @@ __device__ __forceinline__ void derivative(uint32_t (&X)[16][8], uint32_t e1, ui
   });
 }
 
+// A lane's place in its quad and its byte offsets, from an opaque lane id (asm volatile: the
+// kernel derives them again after the transforms instead of keeping them live through them)
+struct LaneCtx {
+  uint32_t l, lcol, sh, e1, e2;
+};
+__device__ __forceinline__ LaneCtx lane_ctx(uint32_t wave_col, uint32_t ss) {
+  uint32_t lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  LaneCtx c;
+  c.l = lane & 3;
+  c.lcol = wave_col + (lane >> 2) * 16 + c.l * ss;  // byte offset of position 4j + l
+  c.sh = 8 * c.l;
+  c.e1 = (c.l & 1) ? 0u : 0xFFFFFFFFu;
+  c.e2 = (c.l & 2) ? 0u : 0xFFFFFFFFu;
+  return c;
+}
+
 __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const uint32_t* __restrict__ plan1,
                                                   const uint32_t* const* __restrict__ plans,
                                                   const uint32_t* __restrict__ seg_list,
                                                   uint32_t seg0) {
   const uint32_t y = seg0 + blockIdx.y;
   const uint32_t seg = seg_list ? seg_list[y] : y;
-  const cplan_t P = (cplan_t)(plans ? plans[y] : plan1);
-  const uint64_t gq = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 2;  // quad
-  const uint64_t col = (gq >> 4) * 512 + (gq & 15) * 16;
-  if (col >= L.len) return;  // whole waves leave together (len % 512 == 0)
-  const uint32_t l = threadIdx.x & 3;
-  const uint32_t e1 = (l & 1) ? 0u : 0xFFFFFFFFu, e2 = (l & 2) ? 0u : 0xFFFFFFFFu, hi = ~e2;
+  const uint32_t* Pg = plans ? plans[y] : plan1;
+  const cplan_t P = (cplan_t)Pg;
+#ifndef CEC_FDD_BFE
+  // the plan's per-lane masks into LDS (4 KiB: 16 bytes per thread), before any wave leaves
+  __shared__ __attribute__((aligned(16))) uint32_t lmask[2 * 16 * 4 * 8];
+  *reinterpret_cast<u32x4*>(lmask + 4 * threadIdx.x) =
+      *reinterpret_cast<const u32x4*>(Pg + FftDecDLayout::kMasks + 4 * threadIdx.x);
+  __syncthreads();
+#endif
+  // a wave owns 512 byte columns: 16 quads of 32 (two 16-byte pieces 256 bytes apart per lane)
+  const uint32_t wave_col =
+      (blockIdx.x * 4 + (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6)) * 512;
+  if (wave_col >= L.len) return;  // whole waves leave together (len % 512 == 0)
   const uint32_t ss = (uint32_t)L.shard_stride;
   const auto rD = rsrc(L.data + seg * L.data_seg_stride);
   const auto rP = rsrc(L.parity + seg * L.par_seg_stride);
-  const uint32_t lcol = (uint32_t)col + l * ss;  // this lane's byte offset of position 4j + l
-  const uint32_t sh = 8 * l;
+  const LaneCtx c0 = lane_ctx(wave_col, ss);
+  const uint32_t l = c0.l, lcol = c0.lcol, sh = c0.sh, e1 = c0.e1, e2 = c0.e2;
 
   uint32_t X[16][8];
   // present shards, each times lam(t) (an erased shard loads as zeros: lam(t) = 0 there)
@@ -268,23 +330,34 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const u
   sfor<16>([&](auto J) CEC_FFT_AI {
     after_prev<J>(X);
     tr8(X[J]);
+#ifdef CEC_FDD_BFE
     mul_rt(X[J], P[FftDecDLayout::kLam + J] >> sh);
+#else
+    mul_rt_lds(X[J], (const lds_u32*)lmask + (J * 4 + l) * 8);
+#endif
   });
   fence_all(X);
-  ifft64(X, e1, e2, hi);
+  ifft64(X, e1, e2);
   fence_all(X);
   derivative(X, e1, e2);
   fence_all(X);
-  fft64(X, e1, e2, hi);
+  fft64_upper(X);
   fence_all(X);
-  // outputs: times 1 / lam'(e), back to bytes, stored by the lanes whose position is an output
+  const LaneCtx c1 = lane_ctx(wave_col, ss);
+  // slots holding an output: the last two FFT layers, times 1 / lam'(e), back to bytes, stored
+  // by the lanes whose position is an output
   sfor<16>([&](auto J) CEC_FFT_AI {
     const uint32_t dw = P[FftDecDLayout::kDinv + J];
     after_prev<J>(X);
     if (dw) {
-      mul_rt(X[J], dw >> sh);
+      fft64_tail<J>(X[J], c1.e1, c1.e2);
+#ifdef CEC_FDD_BFE
+      mul_rt(X[J], dw >> c1.sh);
+#else
+      mul_rt_lds(X[J], (const lds_u32*)lmask + ((16 + J) * 4 + c1.l) * 8);
+#endif
       tr8(X[J]);
-      const uint32_t voff = ((dw >> sh) & 0xFF) ? lcol : kOff;
+      const uint32_t voff = ((dw >> c1.sh) & 0xFF) ? c1.lcol : kOff;
       bst(J < 8 ? rD : rP, voff, (uint32_t)(4 * (J & 7)) * ss, X[J]);
     }
   });

@@ -219,7 +219,10 @@ struct FftDecDLayout {
   static constexpr int kNout = 1;
   static constexpr int kLam = 16;   // [16]: lam(t) of present t, 0 for an erased one
   static constexpr int kDinv = 32;  // [16]: 1 / lam'(t) of an output t, 0 elsewhere
-  static constexpr int kWords = 48;
+  // the same constants as bit masks, one word per (slot j, lane l, bit b): 0 or ~0 = bit b of the
+  // constant of position 4j + l (the kernel's per-lane Horner masks, copied to LDS)
+  static constexpr int kMasks = 48;  // [2][16][4][8]: lam, then 1 / lam'
+  static constexpr int kWords = kMasks + 2 * 16 * 4 * 8;
 };
 
 // Build the mode-D plan for RS(32,32) pattern `present` (64 flags). False when more than 32 shards
@@ -249,6 +252,14 @@ inline bool fftdec_plan_d(const uint8_t* present, bool data_only, FftDecPlan* ou
   }
   if (!nout) return false;
   w[FftDecDLayout::kNout] = (uint32_t)nout;
+  for (int which = 0; which < 2; ++which)
+    for (int t = 0; t < 64; ++t) {
+      const uint8_t c = (uint8_t)(w[(which ? FftDecDLayout::kDinv : FftDecDLayout::kLam) + (t >> 2)] >>
+                                  (8 * (t & 3)));
+      for (int b = 0; b < 8; ++b)
+        w[FftDecDLayout::kMasks + ((which * 16 + (t >> 2)) * 4 + (t & 3)) * 8 + b] =
+            (c >> b & 1) ? 0xFFFFFFFFu : 0u;
+    }
   p.nout = nout;
   *out = std::move(p);
   return true;

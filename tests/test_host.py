@@ -296,7 +296,7 @@ def test_product_kernel_occupancy():
     3 waves per SIMD (<= 168 VGPRs), the one-wave hash tick at 4 (<= 128), the bit-plane restoral
     kernel k_rtb<1..2> at 6 or more (<= 80), the fused RS(32,32) verify and the FFT-domain
     erasure decoder for more than four syndrome slots at 2 (<= 224, <= 256), the decoder for up to
-    four at 3 (<= 168), the formal-derivative decoder at 2 (<= 256), none with scratch."""
+    four at 3 (<= 168), the formal-derivative decoder at 3 (<= 168), none with scratch."""
     import os
     import sys
     from cess_amd import _lib
@@ -307,7 +307,7 @@ def test_product_kernel_occupancy():
     budget = {"k_fft3232I": 168, "k_sha256_tick1": 128, "k_ct_dec1_mixed21": 64,
               "k_rtbILi1E": 80, "k_rtbILi2E": 80, "k_fft3232_verify": 224,
               "k_fftdec_m": 256, "k_fftdec_mILj0ELb0E": 168, "k_fftdec_mILj1ELb0E": 168,
-              "k_fftdec_d": 256}
+              "k_fftdec_d": 168}
     for pat, cap in budget.items():
         ks = {n: r for n, r in res.items() if pat in n}
         assert ks, pat
