@@ -60,7 +60,7 @@ def test_too_few_gpus_exits_nonzero():
 
 def test_kernel_label_every_config():
     """bench.py's line names its dominant kernel for every config (config 6 from the share of
-    segments the FFT-domain decoder took), with no GPU."""
+    segments each FFT-domain decoder took), with no GPU."""
     import bench
     for cfg in (2, 3, 4, 5, 7, 8):
         assert bench.kernel_label(cfg, None, 1, False, 0, 2).startswith("k_")
@@ -68,4 +68,8 @@ def test_kernel_label_every_config():
     assert bench.kernel_label(6, 0.0, 32, False, 0, 32) == "k_rthx<8>"
     assert bench.kernel_label(6, 0.0, 3, False, 0, 32) == "k_rtb"
     assert "50%" in bench.kernel_label(6, 0.5, 16, False, 0, 32)
+    # the formal-derivative decoder's share (CEC_STAT_FFTDEC_D_SEGMENTS)
+    assert bench.kernel_label(6, 1.0, 32, False, 0, 32, 1.0) == "k_fftdec_d"
+    mixed = bench.kernel_label(6, 1.0, 24, False, 0, 32, 0.66)
+    assert "k_fftdec_m (34%" in mixed and "k_fftdec_d (66%)" in mixed
     assert bench.kernel_label(2, None, 1, True, 0, 2) == "k_rthx"

@@ -769,15 +769,16 @@ def test_fftdec_dispatch_by_cost(torch, cess, corc, ne):
         else:
             present[s, 32 + rng.choice(32, size=ne - ne // 2, replace=False)] = 0
     enc = cess.New(k, m)
-    before = enc.stat(4)
+    before, before_d = enc.stat(4), enc.stat(5)
     d_data = to_dev(torch, data * present[:, :k, None])
     d_par = to_dev(torch, want * present[:, k:, None])
     enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
     torch.cuda.synchronize()
     assert np.array_equal(d_data.cpu().numpy(), data)
     assert np.array_equal(d_par.cpu().numpy(), want)
-    on_fd = enc.stat(4) - before
+    on_fd, on_d = enc.stat(4) - before, enc.stat(5) - before_d
     assert on_fd == nseg, on_fd
+    assert on_d == (nseg if ne == 32 else 0), on_d  # 32: the derivative decoder; 8: syndrome rows
 
 
 @pytest.mark.parametrize("ne,ln", [(1, 4096 + 3), (2, (1 << 16) + 16), (3, 4096 + 3), (4, 999)])
