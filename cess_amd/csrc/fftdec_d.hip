@@ -19,7 +19,9 @@
 // through DPP quad_perm, layers 2..5 registers of one lane. A lane's 32 bytes of a shard are two
 // 16-byte pieces 256 bytes apart: each load or store of a wave's 16 lanes with the same l covers 256
 // contiguous bytes of one shard. The run-time multiplications by lam(t) and 1 / lam'(e) differ per
-// lane (position): Horner over the coefficient bits with each bit's mask made by one v_bfe_i32.
+// lane (position): Horner over the coefficient bits, the lane's eight 0 / ~0 bit masks read from
+// LDS (the plan carries them expanded; -DCEC_FDD_BFE makes them with v_bfe_i32 instead, 0.11 ms
+// slower at 32 erasures).
 #include <utility>
 
 #include "fft_core.h"
@@ -82,7 +84,7 @@ __device__ __forceinline__ void after_prev(uint32_t (&X)[16][8]) {
 
 // quad partners: lane l reads lane l ^ 1 / l ^ 2
 // (DPP moves issue at half rate; -DCEC_FDD_SWZ moves them through the LDS crossbar instead:
-// ds_swizzle in quad-permute mode, no VALU issue slot)
+// ds_swizzle in quad-permute mode, no VALU issue slot, but measured slower: 0.94 vs 0.915 ms)
 __device__ __forceinline__ uint32_t qp1(uint32_t v) {
 #ifdef CEC_FDD_SWZ
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x80B1);
