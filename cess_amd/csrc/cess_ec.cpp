@@ -655,7 +655,8 @@ bool is_reencode(const cec_codec* c, const Program& p) {
 // The FFT-domain decoder costs T1 plus (outputs x syndrome slots) Horner rows; k_rthx costs
 // about the same per output at every pattern. Fitted to RS(32,32) rebuilds of 64 segments of
 // 512 KiB, random patterns (bench.py --config 6 --erasures e; profiles/r03/fd_lds_split.jsonl):
-// k_fftdec_m ~ 0.296 ms + 3.3 us per (output, slot) at up to four slots (three waves per SIMD),
+// k_fftdec_m ~ 0.280 ms + 3.3 us per (output, slot) at up to four slots (three waves per SIMD;
+// 0.296 before its last FFT layer ran only on the slots it reads),
 // ~3.8 us past four (two waves); k_rthx ~ 0.235 ms + 33.9 us per output; up to four outputs the
 // alternative is k_rtb, ~0.13 ms + 57 us per output (5.9 / 4.9 / 3.9 / 3.4 TB/s
 // at one to four outputs).
@@ -666,7 +667,7 @@ double fdd_cost(int nout) { return 647.0 + 5.4 * nout; }
 enum FdKind { kFdNone = 0, kFdM = 1, kFdD = 2 };
 int fftdec_choice(int nout, int nrs, bool has_m, bool has_d) {
   const double alt = nout <= 4 ? 130.0 + 57.0 * nout : 235.0 + 33.9 * nout;
-  const double m = has_m ? 296.0 + (cec::fftdec_big(nrs) ? 3.8 : 3.3) * nout * nrs : 1e30;
+  const double m = has_m ? 280.0 + (cec::fftdec_big(nrs) ? 3.8 : 3.3) * nout * nrs : 1e30;
   const double d = has_d ? fdd_cost(nout) : 1e30;
   // the syndrome-row decoder only with a 15 % margin over the derivative: a batch split between
   // the two runs two smaller launches (24 random erasures: 0.854 ms split 34/66 by the bare

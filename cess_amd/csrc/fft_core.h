@@ -176,6 +176,35 @@ __device__ __forceinline__ void ifft32(uint32_t (&X)[16][8], uint32_t em) {
   });
 }
 
+// FFT onto the coset BETA ^ {0..31}, layers 4..1 (in-lane) only: fft32 = this + fft32_l0 on
+// every slot. Callers that need only some slots' values run fft32_l0 for those.
+template <unsigned BETA>
+__device__ __forceinline__ void fft32_upper(uint32_t (&X)[16][8]) {
+  using T = Skews<BETA>;
+  sfor<4>([&](auto I4) CEC_FFT_AI {
+    constexpr int i = 4 - I4, hj = 1 << (i - 1);
+    sfor<16>([&](auto J) CEC_FFT_AI {
+      if constexpr (!(J & hj)) {
+        constexpr unsigned s = T::s.s[i][J >> i];
+        if constexpr (s != 0) mul_acc<s, false>(X[J], X[J + hj], X[J]);
+        sfor<8>([&](auto Q) CEC_FFT_AI { X[J + hj][Q] = x2(X[J + hj][Q], X[J][Q]); });
+      }
+    });
+  });
+}
+// layer 0 of that FFT on register slot J (positions 2J, 2J + 1: across the lane pair)
+template <unsigned BETA, int J>
+__device__ __forceinline__ void fft32_l0(uint32_t (&x)[8], uint32_t em, uint32_t om) {
+  constexpr unsigned s = Skews<BETA>::s.s[0][J];
+  uint32_t P[8];
+  sfor<8>([&](auto Q) CEC_FFT_AI {
+    const uint32_t y = partner(x[Q]);
+    P[Q] = FFT_BOP3(em, y, x[Q], kSel);
+    x[Q] = FFT_BOP3(x[Q], om, y, kXand);
+  });
+  if constexpr (s != 0) mul_acc<s, false>(x, P, P);
+}
+
 // FFT onto the coset BETA ^ {0..31}: coefficients -> values. Layer i: a ^= s*b; b ^= a
 // (i = 4 .. 0). em / om = even / odd-lane masks.
 // SER: each slot's last-layer butterfly starts once the previous slot's is done (for callers that

@@ -126,7 +126,15 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
   }
   sfor<16>([&](auto J) CEC_FFT_AI { tr8(X[J]); });
   ifft32<BA>(X, em);
-  fft32<BB, true>(X, em, om);  // q on coset B
+  // q on coset B; its last layer only on the slots whose q is read (syndrome rows R, erased
+  // outputs of B: the plan's kPslots, numbered before the swaps below)
+  fft32_upper<BB>(X);
+  sfor<16>([&](auto J) CEC_FFT_AI { fence(X[J]); });
+  const uint32_t pslots = P[FftDecLayout::kPslots];
+  sfor<16>([&](auto J) CEC_FFT_AI {
+    if constexpr (J > 0) asm volatile("" : "+v"(X[J][0]) : "v"(X[J - 1][7]));
+    if ((pslots >> J) & 1) fft32_l0<BB, J>(X[J], em, om);
+  });
   // X is complete here: the phases below start from it (keeps the compiler from interleaving the
   // transform's tail with them, which costs registers)
   sfor<16>([&](auto J) CEC_FFT_AI { fence(X[J]); });
