@@ -457,7 +457,10 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps (default 10; config 6: 30, past the clock transient a "
+                         "VALU-heavy decoder rides over its first ~30 launches, "
+                         "profiles/r03/fdd_clock_transient.txt)")
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--variant", type=int, default=-1, help="CT kernel variant (tuning)")
     ap.add_argument("--generic", action="store_true", help="force run-time-coefficient kernel")
@@ -511,6 +514,8 @@ def main() -> None:
                     help="comma list of CT variants: interleaved A/B in one process, prints "
                          "median launch ms per variant and exits")
     args = ap.parse_args()
+    if args.warmup is None:
+        args.warmup = 30 if args.config == 6 else 10
 
     if args.config == 1:  # CPU codec alone (the GPU on the same workload beside it)
         print(json.dumps(config1_cpu(args)), flush=True)
