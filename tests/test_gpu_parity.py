@@ -750,6 +750,29 @@ def test_fftdec_matches_oracle(torch, cess, corc, ne, ln, mode):
     enc.set_option(8, 0)
 
 
+@pytest.mark.parametrize("ln", [1000, 1024 + 512])
+def test_fftdec_d_layout_fallback(torch, cess, corc, ln):
+    """A layout the FFT-domain decoders cannot take (shard_len % 1024 != 0) with the
+    formal-derivative decoder forced (CEC_OPT_FFTDEC_MODE 2): the rebuild runs the run-time matrix
+    kernels instead, bit-exact, and CEC_STAT_FFTDEC_D_SEGMENTS does not move."""
+    k = m = 32
+    nseg = 4
+    rng = np.random.default_rng(ln)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = _wide_patterns(rng, nseg, 32)
+    enc = cess.New(k, m)
+    enc.set_option(8, 2)
+    before = enc.stat(5)
+    d_data = to_dev(torch, data * present[:, :k, None])
+    d_par = to_dev(torch, want * present[:, k:, None])
+    enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_data.cpu().numpy(), data)
+    assert np.array_equal(d_par.cpu().numpy(), want)
+    assert enc.stat(5) == before
+
+
 @pytest.mark.parametrize("ne", [8, 32])
 def test_fftdec_dispatch_by_cost(torch, cess, corc, ne):
     """CEC_OPT_FFTDEC_MODE 0 (the default) sends a random RS(32,32) pattern to the cheapest of the
