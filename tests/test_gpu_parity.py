@@ -750,6 +750,29 @@ def test_fftdec_matches_oracle(torch, cess, corc, ne, ln, mode):
     enc.set_option(8, 0)
 
 
+def test_fftdec_both_decoders_one_call(torch, cess, corc):
+    """One per-segment rebuild whose patterns send half the segments to the syndrome-row decoder
+    (8 erasures) and half to the formal-derivative decoder (32, the cost model's default picks):
+    both launches of the plan write their own segments only, bit-exact with the C oracle."""
+    k = m = 32
+    nseg, ln = 8, 2048
+    rng = np.random.default_rng(808)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = np.ones((nseg, 64), np.uint8)
+    for s in range(nseg):
+        present[s, rng.choice(64, size=8 if s % 2 else 32, replace=False)] = 0
+    enc = cess.New(k, m)
+    b4, b5 = enc.stat(4), enc.stat(5)
+    d_data = to_dev(torch, data * present[:, :k, None])
+    d_par = to_dev(torch, want * present[:, k:, None])
+    enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_data.cpu().numpy(), data)
+    assert np.array_equal(d_par.cpu().numpy(), want)
+    assert enc.stat(4) - b4 == nseg and enc.stat(5) - b5 == nseg // 2
+
+
 @pytest.mark.parametrize("ln", [1000, 1024 + 512])
 def test_fftdec_d_layout_fallback(torch, cess, corc, ln):
     """A layout the FFT-domain decoders cannot take (shard_len % 1024 != 0) with the
