@@ -307,6 +307,9 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const u
   const cplan_t P = (cplan_t)Pg;
 #ifndef CEC_FDD_BFE
   // the plan's per-lane masks into LDS (4 KiB: 16 bytes per thread), before any wave leaves
+  static_assert(FftDecDLayout::kWords - FftDecDLayout::kMasks == 4 * 256 &&
+                    FftDecDLayout::kMasks % 4 == 0,
+                "one 16-byte piece of the mask table per thread of the 256-thread workgroup");
   __shared__ __attribute__((aligned(16))) uint32_t lmask[2 * 16 * 4 * 8];
   *reinterpret_cast<u32x4*>(lmask + 4 * threadIdx.x) =
       *reinterpret_cast<const u32x4*>(Pg + FftDecDLayout::kMasks + 4 * threadIdx.x);
