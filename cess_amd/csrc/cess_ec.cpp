@@ -526,16 +526,20 @@ void scratch_release(cec_codec* c, const Scratch& s, hipStream_t st) {
     c->pool.retire(s.p, s.bytes);
 }
 
+// Cache keys start with a kind tag, so keys of different kinds never compare equal whatever
+// their lengths: 'F' full rebuild, 'P' partial rebuild (decode LRU); 'S' / 'Q' the per-segment
+// plans of cec_reconstruct_batch / cec_reconstruct_partial_batch.
 std::string pattern_key(const uint8_t* present, int n, bool data_only) {
-  std::string key(n + 1, '\0');
-  for (int i = 0; i < n; ++i) key[i] = present[i] ? 1 : 0;
-  key[n] = data_only ? 1 : 0;
+  std::string key(n + 2, '\0');
+  key[0] = 'F';
+  for (int i = 0; i < n; ++i) key[1 + i] = present[i] ? 1 : 0;
+  key[n + 1] = data_only ? 1 : 0;
   return key;
 }
 
 std::string partial_key(const uint8_t* present, const uint8_t* held, int n, bool data_only) {
   std::string key = pattern_key(present, n, data_only);
-  key.push_back(2);  // partial marker: never equal to a full pattern's key
+  key[0] = 'P';
   for (int i = 0; i < n; ++i) key.push_back(held[i] ? 1 : 0);
   return key;
 }
@@ -556,7 +560,7 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* ou
   auto& sc = c->plan_scratch();
   auto* plan = &sc.plan;
   uint8_t flags[cec::kMaxShards];
-  for (int i = 0; i < n; ++i) flags[i] = key[i];
+  for (int i = 0; i < n; ++i) flags[i] = key[1 + i];
   if (cec::gf_decode_plan_sys(c->k, c->m, flags, data_only, *c->E, *plan, sc.a, sc.ainv,
                               sc.work) != 0)
     return set_err(CEC_ETOOFEW, "fewer than k shards present");
@@ -564,10 +568,15 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* ou
   if (plan->nout > 0) {
     // RS(32,32) rebuilds of several shards: also the FFT-domain plan (picked at launch by the
     // codec's CEC_OPT_FFTDEC_MIN and the layout)
+    // They read exactly the program's survivors (the first k present shards): callers stage
+    // only those (the host API below, the multi-GPU gathers), so the plans must not touch any
+    // other shard flagged present.
     cec::FftDecPlan fdp, fddp;
     const bool wide = c->k == 32 && c->m == 32 && plan->nout >= 2;
-    const bool fd = wide && cec::fftdec_plan_m(flags, data_only, &fdp);
-    const bool fdd = wide && cec::fftdec_plan_d(flags, data_only, &fddp);
+    uint8_t read[cec::kMaxShards] = {};
+    for (int j = 0; j < c->k; ++j) read[plan->in_idx[j]] = 1;
+    const bool fd = wide && cec::fftdec_plan_m(read, flags, data_only, &fdp);
+    const bool fdd = wide && cec::fftdec_plan_d(read, flags, data_only, &fddp);
     int rc = build_program(c->pool, c->stream, plan->in_idx, c->k, plan->out_idx, plan->nout,
                            plan->coef, &prog, false, keep, fd ? &fdp : nullptr,
                            fdd ? &fddp : nullptr);
@@ -744,7 +753,7 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
   std::unordered_map<std::string, size_t> gidx;
   std::vector<std::pair<std::string, std::vector<uint32_t>>> groups;
   for (size_t s = 0; s < nseg; ++s) {
-    std::string k = pkey.substr(s * per, per);
+    std::string k = pkey.substr(1 + s * per, per);
     auto it = gidx.find(k);
     if (it == gidx.end()) {
       it = gidx.emplace(k, groups.size()).first;
@@ -1099,8 +1108,9 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
     //  * otherwise: one multi-pattern run-time launch per (chunk index, bucket), each segment's
     //    workgroup row reading its own pattern's chunk, so a batch where every segment has a
     //    different erasure map is still one full-grid launch.
-    std::string pkey(reinterpret_cast<const char*>(present), nseg * n);
-    for (auto& ch : pkey) ch = ch ? 1 : 0;
+    std::string pkey(1, 'S');
+    pkey.reserve(nseg * n + 6);
+    for (size_t i = 0; i < nseg * n; ++i) pkey.push_back(present[i] ? 1 : 0);
     pkey.push_back(data_only ? 1 : 0);
     pkey.push_back(c->force_generic ? 1 : 0);
     const bool fdok = cec::fftdec_layout_ok(L);
@@ -1140,8 +1150,8 @@ int cec_reconstruct_partial_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_pari
   const int n = c->k + c->m;
   Layout L = batch_layout(c, d_data, d_parity, shard_len);
   // per segment: n presence flags then n held flags; the same plan cache as the full rebuild
-  // (the trailing marker keeps the keys apart)
-  std::string pkey;
+  // (the leading kind tag keeps the keys apart)
+  std::string pkey(1, 'Q');
   pkey.reserve(nseg * 2 * n + 3);
   for (size_t s = 0; s < nseg; ++s) {
     for (int i = 0; i < n; ++i) pkey.push_back(present[s * n + i] ? 1 : 0);
@@ -1149,7 +1159,6 @@ int cec_reconstruct_partial_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_pari
   }
   pkey.push_back(data_only ? 1 : 0);
   pkey.push_back(c->force_generic ? 1 : 0);
-  pkey.push_back(2);
   int rc = CEC_OK;
   if (!c->ps || c->ps->key != pkey) {
     std::unique_ptr<PsPlan> plan;

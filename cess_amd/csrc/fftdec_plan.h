@@ -34,11 +34,11 @@ struct FftDecLayout {
                                      // bits 8..15: mode (0 = M)
   static constexpr int kPresA = 1;   // bit t: shard t of coset A is read (present)
   static constexpr int kR = 2;       // bit t: shard t of coset B is a syndrome row (read)
-  static constexpr int kEB = 3;      // bit t: shard t of coset B is erased
-  static constexpr int kDA = 4;      // bit t: shard t of coset A is erased
+  static constexpr int kEB = 3;      // bit t: shard t of coset B is not read
+  static constexpr int kDA = 4;      // bit t: shard t of coset A is not read
   static constexpr int kNout = 5;    // outputs written
   static constexpr int kRslots = 6;  // bit j: slot j (positions 2j, 2j + 1 of B) holds R rows
-  static constexpr int kPslots = 7;  // bit j: slot j is packed (R or an erased B output)
+  static constexpr int kPslots = 7;  // bit j: slot j is packed (R or an output on B)
   static constexpr int kNrs = 8;     // popcount(kRslots)
   static constexpr int kNpk = 9;
   static constexpr int kNrs1 = 10;   // 1 << nrs     // bit r: register slot r is packed after the swaps
@@ -77,23 +77,35 @@ inline uint8_t lagrange(unsigned base, unsigned c, unsigned x) {
 }  // namespace fdp
 
 // Build the mode-M plan for RS(32,32) erasure pattern `present` (64 flags, shards 0..31 data,
-// 32..63 parity); data_only drops parity outputs. Returns false when the pattern has more than
-// 32 erasures (the caller reports ETOOFEW) or nothing to write.
-inline bool fftdec_plan_m(const uint8_t* present, bool data_only, FftDecPlan* out) {
-  uint32_t erd = 0, erp = 0;  // erased data / parity
+// 32..63 parity) that reads only the shards flagged in `read` (a subset of the present ones: the
+// codec's contract is that a rebuild reads the first k present shards, the survivors a caller
+// stages — cess_ec.cpp's host API and the multi-GPU gathers move only those). Every shard not
+// read is an erasure to the algorithm; the outputs are the shards not present (data_only: data
+// shards only). Returns false when more than 32 shards are unread (the caller reports ETOOFEW) or
+// there is nothing to write.
+inline bool fftdec_plan_m(const uint8_t* read, const uint8_t* present, bool data_only,
+                          FftDecPlan* out) {
+  uint32_t erd = 0, erp = 0;  // unread data / parity
+  uint32_t lost_d = 0, lost_p = 0;  // not present (the outputs)
   for (int t = 0; t < 32; ++t) {
-    if (!present[t]) erd |= 1u << t;
-    if (!present[32 + t]) erp |= 1u << t;
+    if (!read[t]) erd |= 1u << t;
+    if (!read[32 + t]) erp |= 1u << t;
+    if (!present[t]) lost_d |= 1u << t;
+    if (!present[32 + t]) lost_p |= 1u << t;
   }
+  if ((lost_d & ~erd) || (lost_p & ~erp)) return false;  // a read shard must be present
   const int nd = fdp::popc(erd), np = fdp::popc(erp);
   if (nd + np > 32 || nd + np == 0) return false;
   // A = the coset with fewer erasures (fewer syndrome rows); data on a tie
   const int side = np < nd ? 1 : 0;
   const unsigned baseA = side ? 32u : 0u, baseB = side ? 0u : 32u;
   const uint32_t DA = side ? erp : erd, EB = side ? erd : erp;
+  // outputs on A (within DA) and on B (within EB)
+  const uint32_t OA = (side ? lost_p : lost_d) & ~(data_only && side == 1 ? ~0u : 0u);
+  const uint32_t OB = (side ? lost_d : lost_p) & ~(data_only && side == 0 ? ~0u : 0u);
   const int d = fdp::popc(DA);
   // R: d present points of B packed into few slots: whole present slots first, then a lone
-  // present position of a slot that is packed anyway (it holds an erased output), then any
+  // read position of a slot that is packed anyway (it holds an output), then any
   uint32_t R = 0;
   int need = d;
   for (int j = 0; j < 16 && need >= 2; ++j)
@@ -104,7 +116,7 @@ inline bool fftdec_plan_m(const uint8_t* present, bool data_only, FftDecPlan* ou
   for (int pass = 0; pass < 2 && need > 0; ++pass)
     for (int t = 0; t < 32 && need > 0; ++t) {
       if ((EB >> t & 1) || (R >> t & 1)) continue;
-      const bool packed = (EB >> (t ^ 1) & 1) || (R >> (t ^ 1) & 1);
+      const bool packed = (OB >> (t ^ 1) & 1) || (R >> (t ^ 1) & 1);
       if (pass == 0 && !packed) continue;
       R |= 1u << t;
       --need;
@@ -113,13 +125,13 @@ inline bool fftdec_plan_m(const uint8_t* present, bool data_only, FftDecPlan* ou
   uint32_t rslots = 0, pslots = 0;
   for (int j = 0; j < 16; ++j) {
     if (R >> (2 * j) & 3) rslots |= 1u << j;
-    if ((R | EB) >> (2 * j) & 3) pslots |= 1u << j;
+    if ((R | OB) >> (2 * j) & 3) pslots |= 1u << j;
   }
-  // outputs: erased data always; erased parity unless data_only
+  // outputs: lost data always; lost parity unless data_only
   std::vector<uint32_t> outs;
   for (int t = 0; t < 32; ++t) {
-    if (DA >> t & 1 && !(data_only && side == 1)) outs.push_back((uint32_t)t);
-    if (EB >> t & 1 && !(data_only && side == 0)) outs.push_back((uint32_t)t | 32u);
+    if (OA >> t & 1) outs.push_back((uint32_t)t);
+    if (OB >> t & 1) outs.push_back((uint32_t)t | 32u);
   }
   if (outs.empty()) return false;
   // u = inv(L[R][D]) s;  h(e) = L[e][D] u
@@ -217,7 +229,7 @@ inline bool fftdec_plan_m(const uint8_t* present, bool data_only, FftDecPlan* ou
 struct FftDecDLayout {
   static constexpr int kFlags = 0;  // bits 8..15: mode (1 = D)
   static constexpr int kNout = 1;
-  static constexpr int kLam = 16;   // [16]: lam(t) of present t, 0 for an erased one
+  static constexpr int kLam = 16;   // [16]: lam(t) of a read t, 0 elsewhere
   static constexpr int kDinv = 32;  // [16]: 1 / lam'(t) of an output t, 0 elsewhere
   // the same constants as bit masks, one word per (slot j, lane l, bit b): 0 or ~0 = bit b of the
   // constant of position 4j + l (the kernel's per-lane Horner masks, copied to LDS)
@@ -225,13 +237,18 @@ struct FftDecDLayout {
   static constexpr int kWords = kMasks + 2 * 16 * 4 * 8;
 };
 
-// Build the mode-D plan for RS(32,32) pattern `present` (64 flags). False when more than 32 shards
-// are erased or there is nothing to write.
-inline bool fftdec_plan_d(const uint8_t* present, bool data_only, FftDecPlan* out) {
+// Build the mode-D plan for RS(32,32) pattern `present` (64 flags) reading only the shards flagged
+// in `read` (present ones; see fftdec_plan_m): the locator's roots are the unread shards, the
+// outputs the shards not present. False when more than 32 shards are unread or there is nothing
+// to write.
+inline bool fftdec_plan_d(const uint8_t* read, const uint8_t* present, bool data_only,
+                          FftDecPlan* out) {
   int ne = 0, nout = 0;
   uint8_t erased[64];
-  for (int t = 0; t < 64; ++t)
-    if (!present[t]) erased[ne++] = (uint8_t)t;
+  for (int t = 0; t < 64; ++t) {
+    if (read[t] && !present[t]) return false;  // a read shard must be present
+    if (!read[t]) erased[ne++] = (uint8_t)t;
+  }
   if (ne == 0 || ne > 32) return false;
   FftDecPlan p;
   p.side = 0;
@@ -243,9 +260,9 @@ inline bool fftdec_plan_d(const uint8_t* present, bool data_only, FftDecPlan* ou
     for (int i = 0; i < ne; ++i)
       if (erased[i] != t) lam = gf_mul(lam, (uint8_t)(t ^ erased[i]));
     const int sh = 8 * (t & 3);
-    if (present[t]) {
+    if (read[t]) {
       w[FftDecDLayout::kLam + (t >> 2)] |= (uint32_t)lam << sh;
-    } else if (!(data_only && t >= 32)) {
+    } else if (!present[t] && !(data_only && t >= 32)) {
       w[FftDecDLayout::kDinv + (t >> 2)] |= (uint32_t)gf_inv(lam) << sh;
       ++nout;
     }

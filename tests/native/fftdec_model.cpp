@@ -63,18 +63,19 @@ static void fft64(uint8_t* v) {
   }
 }
 // mode D on one byte column: the fails it finds
-static int check_d(const uint8_t* present, bool data_only, const uint8_t* cw, int* cases) {
+static int check_d(const uint8_t* read, const uint8_t* present, bool data_only, const uint8_t* cw,
+                   int* cases) {
   FftDecPlan p;
   int want = 0, fails = 0;
   for (int i = 0; i < 64; ++i) want += !present[i] && (!data_only || i < 32);
-  if (!fftdec_plan_d(present, data_only, &p)) return want ? 1 : 0;
+  if (!fftdec_plan_d(read, present, data_only, &p)) return want ? 1 : 0;
   const uint32_t* w = p.w.data();
   if ((int)w[FftDecDLayout::kNout] != want || (w[FftDecDLayout::kFlags] >> 8 & 255) != 1) ++fails;
   auto byte = [&](int base, int t) { return (uint8_t)(w[base + (t >> 2)] >> (8 * (t & 3))); };
   uint8_t v[64], d[64] = {};
   for (int t = 0; t < 64; ++t) {
     const uint8_t lam = byte(FftDecDLayout::kLam, t);
-    if ((lam != 0) != (present[t] != 0)) ++fails;
+    if ((lam != 0) != (read[t] != 0)) ++fails;  // only the read shards are loaded
     v[t] = gf_mul(lam, cw[t]);
   }
   ifft64(v);
@@ -118,6 +119,17 @@ int main() {
     if (trial % 7 == 3)  // a structured pattern: the first e shards of one coset
       for (int i = 0; i < 64; ++i) present[i] = !(i >= (trial & 32) && i < (trial & 32) + e);
     const bool data_only = trial % 3 == 1;
+    // the shards the plans may read: the first 32 present (the codec's survivors, all a caller
+    // stages), or on odd trials any 32 present ones
+    uint8_t read[64] = {};
+    {
+      int idx[64], np = 0;
+      for (int i = 0; i < 64; ++i)
+        if (present[i]) idx[np++] = i;
+      if (trial & 1)
+        for (int i = np - 1; i > 0; --i) std::swap(idx[i], idx[(int)(rng() % (i + 1))]);
+      for (int i = 0; i < 32 && i < np; ++i) read[idx[i]] = 1;
+    }
     for (int col = 0; col < 4; ++col) {  // mode D
       uint8_t cw[64];
       for (int c = 0; c < 32; ++c) cw[c] = (uint8_t)rng();
@@ -126,14 +138,14 @@ int main() {
         for (int c = 0; c < 32; ++c) a ^= gf_mul(E.v[r][c], cw[c]);
         cw[r] = a;
       }
-      const int f = check_d(present, data_only, cw, &dcases);
+      const int f = check_d(read, present, data_only, cw, &dcases);
       if (f && dfails < 10) std::printf("mode D mismatch trial %d e %d\n", trial, e);
       dfails += f;
     }
     FftDecPlan p;
     bool any_out = false;
     for (int i = 0; i < 64; ++i) any_out |= !present[i] && (!data_only || i < 32);
-    if (!fftdec_plan_m(present, data_only, &p)) {
+    if (!fftdec_plan_m(read, present, data_only, &p)) {
       if (any_out) {
         std::printf("plan refused a decodable pattern, trial %d\n", trial);
         ++fails;
@@ -143,6 +155,14 @@ int main() {
     const uint32_t* w = p.w.data();
     const unsigned baseA = p.side ? 32 : 0, baseB = p.side ? 0 : 32;
     const uint32_t R = w[FftDecLayout::kR], rslots = w[FftDecLayout::kRslots];
+    uint32_t outB = 0;  // outputs on coset B
+    for (int o = 0; o < p.nout; ++o)
+      if (w[FftDecLayout::kOuts + o] & 32) outB |= 1u << (w[FftDecLayout::kOuts + o] & 31);
+    for (int t = 0; t < 32; ++t)  // the kernel loads only shards the plan may read
+      if (((w[FftDecLayout::kPresA] >> t & 1) && !read[baseA ^ t]) || ((R >> t & 1) && !read[baseB ^ t])) {
+        std::printf("trial %d: plan reads unread shard\n", trial);
+        ++fails;
+      }
     for (int col = 0; col < 8; ++col) {
       uint8_t cw[64];
       for (int c = 0; c < 32; ++c) cw[c] = (uint8_t)rng();
@@ -189,7 +209,7 @@ int main() {
         for (int i = 0; i < nrs; ++i) std::swap(reg[i], reg[__builtin_ctz(w[FftDecLayout::kSwap + i])]);
         uint32_t want = 0;
         for (int r = 0; r < 16; ++r)
-          if ((R | w[FftDecLayout::kEB]) >> (2 * reg[r]) & 3) want |= 1u << r;
+          if ((R | outB) >> (2 * reg[r]) & 3) want |= 1u << r;
         if (want != w[FftDecLayout::kNpk]) ++fails;
       }
       for (int o = 0; o < p.nout; ++o) {

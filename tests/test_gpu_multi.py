@@ -53,12 +53,17 @@ def _rank(rank, world, port, k, m, nseg, F, q, exchange="survivors"):
     dist.destroy_process_group()
 
 
+# RS(32,32) at 1 MiB fragments loses 1..12 fragments per segment: from four on, the FFT-domain
+# decoders rebuild them from the gathered survivors only (the first k present)
+WIDE = [(32, 32, "survivors"), (32, 32, "partials")]
+
+
 @pytest.mark.parametrize("k,m,exchange", [(2, 1, "survivors"), (4, 2, "survivors"),
-                                          (4, 2, "partials"), (10, 4, "auto")])
+                                          (4, 2, "partials"), (10, 4, "auto")] + WIDE)
 def test_degraded_read_rccl(k, m, exchange):
     import torch
     import torch.multiprocessing as mp
-    world = min(torch.cuda.device_count(), 4)
+    world = min(torch.cuda.device_count(), 8)
     if world < 2:
         pytest.skip("RCCL degraded read needs >= 2 visible GPUs")
     ctx = mp.get_context("spawn")
@@ -103,14 +108,19 @@ def _gloo_rank(rank, world, port, k, m, nseg, F, exchange, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k,m,exchange", [(3, 4, 2, "partials"), (3, 10, 4, "auto"),
-                                                (2, 32, 32, "auto")])
-def test_degraded_read_partials_shared_gpu(world, k, m, exchange):
+@pytest.mark.parametrize("world,k,m,exchange,F", [(3, 4, 2, "partials", (1 << 16) + 32),
+                                                  (3, 10, 4, "auto", (1 << 16) + 32),
+                                                  (2, 32, 32, "auto", (1 << 16) + 32),
+                                                  (2, 32, 32, "survivors", 1 << 16),
+                                                  (3, 32, 32, "auto", 1 << 16)])
+def test_degraded_read_partials_shared_gpu(world, k, m, exchange, F):
+    """F a multiple of 1024 with RS(32,32): segments losing 4..10 fragments rebuild through the
+    FFT-domain decoders from the k gathered survivors (the staging holds nothing else)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    nseg, F = 10, (1 << 16) + 32
+    nseg = 10
     procs = [ctx.Process(target=_gloo_rank, args=(r, world, port, k, m, nseg, F, exchange, q))
              for r in range(world)]
     for p in procs:
@@ -121,7 +131,8 @@ def test_degraded_read_partials_shared_gpu(world, k, m, exchange):
         assert p.exitcode == 0
     assert all(ok for _, ok, _, _ in res), res
     assert sum(nr for _, _, nr, _ in res) == sum(1 + s % m for s in range(nseg))
-    assert all(npart > 0 for *_, npart in res)
+    if exchange != "survivors":
+        assert all(npart > 0 for *_, npart in res)
 
 
 def _codewords(k, m, nseg, F, seed=7):
@@ -142,7 +153,9 @@ def _codewords(k, m, nseg, F, seed=7):
                                                   (10, 4, 12, (1 << 20) + 64, "survivors"),
                                                   (2, 1, 600, 65536, "survivors"),
                                                   (10, 4, 12, (1 << 20) + 64, "partials"),
-                                                  (4, 2, 600, 4096, "partials")])
+                                                  (4, 2, 600, 4096, "partials"),
+                                                  (32, 32, 12, 1 << 16, "survivors"),
+                                                  (32, 32, 12, 1 << 16, "partials")])
 def test_c_dist_degraded_read_world1(k, m, nseg, F, exchange):
     """cec_dist_degraded_read (libcessec's own RCCL group, the C form of degraded_read) at world
     1: plan, agreement all-reduce, local survivor copies, per-segment rebuild and copy-out, every
@@ -202,13 +215,13 @@ def _c_rank(rank, world, uid_path, k, m, nseg, F, q, exchange="survivors"):
 
 
 @pytest.mark.parametrize("k,m,exchange", [(2, 1, "survivors"), (4, 2, "survivors"),
-                                          (4, 2, "partials"), (10, 4, "auto")])
+                                          (4, 2, "partials"), (10, 4, "auto")] + WIDE)
 def test_c_dist_degraded_read_rccl(k, m, exchange, tmp_path):
-    """The C-ABI degraded read across 2..4 GPUs (one process each, the group id handed over
-    through a file as a non-Python host would through its control plane)."""
+    """The C-ABI degraded read across every visible GPU up to 8 (one process each, the group id
+    handed over through a file as a non-Python host would through its control plane)."""
     import torch
     import torch.multiprocessing as mp
-    world = min(torch.cuda.device_count(), 4)
+    world = min(torch.cuda.device_count(), 8)
     if world < 2:
         pytest.skip("RCCL degraded read needs >= 2 visible GPUs")
     ctx = mp.get_context("spawn")

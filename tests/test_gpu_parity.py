@@ -112,6 +112,55 @@ def test_golden_reconstruct_host_api(cess, golden, corc, generic):
                     assert np.array_equal(shards[i], full[i]), (k, m, rec, i)
 
 
+@pytest.mark.parametrize("ne", [4, 8, 16, 24, 32])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_host_api_wide_rebuild_reads_only_survivors(cess, corc, ne, mode):
+    """The host-buffer API stages only the k survivors (the first k present shards) into HBM, so
+    a rebuild must read nothing else: RS(32,32) with shard_len % 1024 == 0 and >= 4 erasures
+    runs the FFT-domain decoders (mode 1 / 2 force one), which must take their plans from those
+    survivors, not from every shard flagged present (the stage holds stale bytes of the previous
+    call there). Every pattern, both data_only settings, bit-exact against the C oracle."""
+    k, m, ln = 32, 32, 4096
+    rng = np.random.default_rng(100 + ne)
+    enc = cess.New(k, m)
+    enc.set_option(8, mode)
+    for trial in range(6):
+        data = [rng.integers(0, 256, ln, dtype=np.uint8) for _ in range(k)]
+        full = data + c_encode(corc, k, m, data)
+        # a previous call leaves other bytes in the stage: garbage where the next one must not read
+        junk = [rng.integers(0, 256, ln, dtype=np.uint8) for _ in range(k + m)]
+        enc.Encode(junk)
+        erased = set(rng.choice(k + m, size=ne, replace=False).tolist())
+        if trial == 0:  # data 0..3 lost plus parity: the advisor's stale-parity pattern
+            erased = set(range(min(ne, 4))) | set(range(k + 4, k + 4 + ne - min(ne, 4)))
+        for data_only in (False, True):
+            shards = [None if i in erased else full[i].copy() for i in range(k + m)]
+            (enc.ReconstructData if data_only else enc.Reconstruct)(shards)
+            for i in range(k + m):
+                if data_only and i >= k and i in erased:
+                    assert shards[i] is None
+                else:
+                    assert np.array_equal(shards[i], full[i]), (ne, mode, trial, data_only, i)
+
+
+def test_repair_fragment_wide_more_than_k_survivors(cess, corc):
+    """repair_fragment with more than k survivors of an RS(32,32) segment that lost many other
+    fragments too (a miner exit): the rebuild must come from the staged survivors only."""
+    from cess_amd.repair import repair_fragment
+    k, m, F = 32, 32, 8192
+    rng = np.random.default_rng(8)
+    data = [rng.integers(0, 256, F, dtype=np.uint8) for _ in range(k)]
+    full = data + c_encode(corc, k, m, data)
+    enc = cess.New(k, m)
+    for lost in (0, 5, 31, 32, 50):
+        others = set(rng.choice([i for i in range(k + m) if i != lost], size=20,
+                                replace=False).tolist())
+        surv = {i: full[i] for i in range(k + m) if i != lost and i not in others}
+        assert len(surv) > k
+        got = repair_fragment(enc, surv, lost)
+        assert np.array_equal(got, full[lost]), lost
+
+
 def test_reconstruct_too_few(cess):
     enc = cess.New(4, 2)
     sh = [np.ones(8, np.uint8)] * 6
