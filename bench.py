@@ -71,16 +71,17 @@ CONFIGS = {
 GPU_BOX_CPU_SHARE = 16  # CPUs the harness gives one GPU's job on the box (its pools obey this)
 
 
-def cpu_threads() -> int:
-    """Threads for the CPU baseline: the host's CPU share for this GPU. The GPU box shows the
-    whole machine's CPUs to nproc / os.cpu_count() but gives one GPU's job a 16-CPU share, and
-    worker pools must stay within it; the CPU rate is therefore quoted at that share, with
-    the per-thread rate beside it."""
+def cpu_threads(gpus: int = 1) -> int:
+    """Threads for the CPU baseline: the host's CPU share for the GPUs in use. The GPU box shows
+    the whole machine's CPUs to nproc / os.cpu_count() but gives each GPU's job a 16-CPU share,
+    and worker pools must stay within it; the CPU rate is therefore quoted at that share (16 per
+    GPU the job holds: the whole node's share on an 8-GPU run), with the per-thread rate
+    beside it."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(GPU_BOX_CPU_SHARE, n))
+    return max(1, min(GPU_BOX_CPU_SHARE * max(1, gpus), n))
 
 
 SIMD_NAMES = {0: "scalar table", 1: "AVX2 split-nibble", 2: "AVX-512BW + GFNI affine"}
@@ -97,8 +98,9 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(k: int, m: int, F: int, target_s: float) -> dict:
-    """Time the C oracle (oracle/rs_oracle.c) on a bounded sample of the same workload."""
+def cpu_baseline(k: int, m: int, F: int, target_s: float, gpus: int = 1) -> dict:
+    """Time the C oracle (oracle/rs_oracle.c) on a bounded sample of the same workload, on the
+    CPU share of the `gpus` GPUs the job holds (the whole node's share for a multi-GPU line)."""
     from oracle.c_oracle import load_c_oracle
     orc = load_c_oracle()
     simd = orc.orc_set_simd(-1)  # the best form the host has
@@ -107,7 +109,7 @@ def cpu_baseline(k: int, m: int, F: int, target_s: float) -> dict:
     data = np.empty(nseg * k * F, np.uint8)
     par = np.empty(nseg * m * F, np.uint8)
     orc.orc_fill_synthetic(data.ctypes.data, k * F, nseg, 0, SEED0 + 2)
-    threads = cpu_threads()
+    threads = cpu_threads(gpus)
     orc.orc_encode_batch(k, m, data.ctypes.data, par.ctypes.data, nseg, F, threads, 1)  # touch
     t1 = orc.orc_encode_batch(k, m, data.ctypes.data, par.ctypes.data, nseg, F, threads, 1)
     reps = max(1, int(target_s / max(t1, 1e-6)))
@@ -121,11 +123,12 @@ def cpu_baseline(k: int, m: int, F: int, target_s: float) -> dict:
         "cores": threads,
         "kind": "port",
         "sample": f"{reps} x {nseg} segments of {k * F // MiB} MiB, RS({k},{m}), "
-                  f"{SIMD_NAMES[simd]} C oracle, {threads} threads (this GPU's CPU share), "
-                  f"{t:.1f} s",
+                  f"{SIMD_NAMES[simd]} C oracle, {threads} threads (the CPU share of the "
+                  f"{gpus} GPU(s) in use: {GPU_BOX_CPU_SHARE} per GPU), {t:.1f} s",
         "value_1thread": round(n1 * per_seg / st / GB, 3),
         "cpu_model": cpu_model(),
         "host_cpus_visible": os.cpu_count(),
+        "gpus_in_use": gpus,
     }
 
 
@@ -230,13 +233,16 @@ def config1_cpu(args) -> dict:
 
 
 def degraded_gather(enc, k: int, m: int, F: int, world: int, rank: int, dev, nseg: int,
-                    exchange: str = "survivors"):
+                    exchange: str = "survivors", transport: str = "torch"):
     """BASELINE config 4's exchange step, set up once: segments 0..nseg*world-1 stored under the
     miner-spread placement (fragment f of segment s on GPU (s + f) mod world,
     c-pallets/file-bank/src/functions.rs:187-283), every segment losing fragment s mod (k+m).
-    Returns (run, verify, plan): run() moves survivors (or, exchange "partials"/"auto", partial
-    rebuilds: SURVEY.md §8e) over the process group (RCCL point to point; RCCL has no XOR
-    reduction) and rebuilds the lost fragments with libcessec."""
+    Returns (run, verify, plan, close): run() moves survivors (or, exchange "partials"/"auto",
+    partial rebuilds: SURVEY.md §8e) between the ranks (RCCL point to point; RCCL has no XOR
+    reduction) and rebuilds the lost fragments with libcessec. transport "torch": the
+    torch.distributed process group (distributed.degraded_read); "cabi": libcessec's own RCCL
+    communicator behind the C ABI (cec_dist_degraded_read, what a Go / Rust host calls), its
+    group id handed to the other ranks over the process group."""
     import torch
     import cess_amd
     from cess_amd import distributed as D
@@ -256,10 +262,21 @@ def degraded_gather(enc, k: int, m: int, F: int, world: int, rank: int, dev, nse
             if (s, f) in store.slots:
                 store.data[store.slots[(s, f)]].copy_(seg_d[0, f] if f < k else seg_p[0, f - k])
     torch.cuda.synchronize(dev)
-    plan = D.plan_gather({s: [s % n] for s in range(total)}, k, m, world, F, exchange=exchange)
+    lost = {s: [s % n] for s in range(total)}
+    plan = D.plan_gather(lost, k, m, world, F, exchange=exchange)
+    group = None
+    if transport == "cabi":
+        import torch.distributed as dist
+        uid = [D.RcclGroup.unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        group = D.RcclGroup(enc, uid[0], world, rank, exchange)
 
-    def run():
-        return D.degraded_read(plan, store, enc, rank)
+        def run():
+            return group.degraded_read(lost, store)
+    else:
+        def run():
+            return D.degraded_read(plan, store, enc, rank)
 
     def verify(out) -> bool:
         ok = True
@@ -268,7 +285,11 @@ def degraded_gather(enc, k: int, m: int, F: int, world: int, rank: int, dev, nse
             enc.EncodeBatch(seg_d, seg_p, 1, F)
             ok &= bool(torch.equal(got, seg_d[0, f] if f < k else seg_p[0, f - k]))
         return ok
-    return run, verify, plan
+
+    def close():
+        if group is not None:
+            group.close()
+    return run, verify, plan, close
 
 
 def cu_split_streams(c: int, dev):
@@ -409,28 +430,36 @@ def wide_code_legs(dev, local, stream, nseg=64, reps=10) -> dict:
     cess_amd.fill_synthetic(d_data, k * F, nseg, 0, 0xCE550005, stream=stream)
     rng = np.random.default_rng(0xCE55)
 
-    # 30 untimed calls first: a VALU-heavy kernel's first ~30 launches ride a clock transient
-    # (k_fftdec_d under rocprof: 0.82 -> 1.12 -> 0.82 ms over launches 1..30,
-    # profiles/r03/fdd_clock_transient.txt)
+    # A VALU-heavy kernel's first ~30 launches ride a clock transient (k_fftdec_d under rocprof:
+    # 0.82 -> 1.12 -> 0.82 ms over launches 1..30, profiles/r03/fdd_clock_transient.txt): each leg
+    # reports the mean of its first `warm` launches (cold: what a short restoral burst sees; one
+    # untimed call before them builds the decode plans) beside the mean of the `reps` after them
     warm = 3 * reps
 
     def timed_ms(fn):
+        fn()  # plans built / cached
+        torch.cuda.synchronize(dev)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
         for _ in range(warm):
             fn()
+        c1.record(stream)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
         for _ in range(reps):
             fn()
         b.record(stream)
         torch.cuda.synchronize(dev)
-        return a.elapsed_time(b) / reps
+        return a.elapsed_time(b) / reps, c0.elapsed_time(c1) / warm
 
     legs = {}
 
     def leg(name, fn, outs):
-        ms = timed_ms(fn)
-        legs[name] = {"ms": round(ms, 4),
-                      "GBps": round(nseg * (k + outs) * F / (ms * 1e-3) / GB, 1)}
+        ms, cold = timed_ms(fn)
+        byt = nseg * (k + outs) * F
+        legs[name] = {"ms": round(ms, 4), "GBps": round(byt / (ms * 1e-3) / GB, 1),
+                      f"cold_ms_first{warm}": round(cold, 4),
+                      "cold_GBps": round(byt / (cold * 1e-3) / GB, 1)}
 
     leg("encode", lambda: enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream), m)
     for ne, name in ((1, "restoral_1_lost"), (8, "rebuild_8_lost"), (32, "rebuild_32_lost")):
@@ -440,9 +469,9 @@ def wide_code_legs(dev, local, stream, nseg=64, reps=10) -> dict:
         fd0, fdd0 = enc.stat(4), enc.stat(5)
         leg(name, lambda: enc.ReconstructBatch(d_data, d_par, nseg, F, pres, stream=stream), ne)
         legs[name]["fftdec_segment_share"] = round(
-            (enc.stat(4) - fd0) / (nseg * (reps + warm)), 3)
+            (enc.stat(4) - fd0) / (nseg * (reps + warm + 1)), 3)
         legs[name]["fftdec_d_segment_share"] = round(
-            (enc.stat(5) - fdd0) / (nseg * (reps + warm)), 3)
+            (enc.stat(5) - fdd0) / (nseg * (reps + warm + 1)), 3)
     d_ok = torch.empty(nseg, dtype=torch.uint8, device=dev)
     leg("verify", lambda: enc.VerifyBatch(d_data, d_par, nseg, F, d_ok=d_ok, stream=stream), m)
     torch.cuda.synchronize(dev)
@@ -451,6 +480,187 @@ def wide_code_legs(dev, local, stream, nseg=64, reps=10) -> dict:
     enc.close()
     del d_data, d_par
     return legs
+
+
+class HashPipeline:
+    """BASELINE config 5's step, windowed over steps: step i encodes into parity buffer i % (W+1)
+    on the launch stream, then (on the hash stream, after the encode) adds the batch's
+    nseg * (k+m) fragment chains to the GPU hash queue and ticks it once: each tick advances every
+    live chain by ceil(blocks per fragment / W) blocks, so a batch's hashes complete W ticks
+    after its encode and W batches hash together (W x nseg x (k+m) chains in flight). The data
+    batch is read-only and shared; parity and hex are (W+1)-buffered: the batch a step overwrites
+    completed one tick earlier, so the encode of step i + 1 waits for tick i - 1 and overlaps
+    tick i."""
+
+    def __init__(self, enc, d_data, d_par, nseg, F, dev, local, stream, sha_stream, W,
+                 tick_pf=0):
+        import torch
+        import cess_amd
+        k, m = enc.DataShards, enc.ParityShards
+        self.enc, self.d_data, self.nseg, self.F = enc, d_data, nseg, F
+        self.k, self.m, self.W, self.NB = k, m, W, W + 1
+        self.stream, self.sha_stream = stream, sha_stream
+        d_hex = torch.empty((nseg, k + m, 64), dtype=torch.uint8, device=dev)
+        self.pipe_par = [d_par] + [torch.empty_like(d_par) for _ in range(self.NB - 1)]
+        self.pipe_hex = [d_hex] + [torch.empty_like(d_hex) for _ in range(self.NB - 1)]
+        chains = W * nseg * (k + m)
+        self.hq = cess_amd.HashQueue(capacity=1 << max(10, (chains - 1).bit_length()),
+                                     device=local, stream=sha_stream)
+        if tick_pf:
+            self.hq.set_option(1, tick_pf)
+        self.tick_blocks = -(-cess_amd.sha256_blocks(F) // W)
+        self.ev_enc = [torch.cuda.Event() for _ in range(self.NB)]
+        self.ev_free = [torch.cuda.Event() for _ in range(self.NB)]
+        self.i = 0
+
+    def step(self):
+        i, NB, W = self.i, self.NB, self.W
+        self.i += 1
+        b = i % NB
+        if i >= NB:
+            self.stream.wait_event(self.ev_free[b])  # batch i - NB's hashes done: b reusable
+        self.enc.EncodeBatch(self.d_data, self.pipe_par[b], self.nseg, self.F, stream=self.stream)
+        self.ev_enc[b].record(self.stream)
+        self.sha_stream.wait_event(self.ev_enc[b])
+        self.hq.add_fragments(self.d_data, self.pipe_par[b], self.nseg, self.k, self.m, self.F,
+                              self.pipe_hex[b])
+        self.hq.tick(self.tick_blocks)
+        # this tick completed batch i - W + 1, whose buffer step i + 2 takes
+        self.ev_free[(i - W + 1) % NB].record(self.sha_stream)
+
+    def drain(self):
+        self.hq.finish()
+        if self.sha_stream is not self.stream:
+            self.stream.wait_stream(self.sha_stream)
+
+
+def config5_leg(dev, local, W: int = 96, warmup: int = 10, sample: int = 48) -> dict:
+    """BASELINE config 5 inside the default line: RS(32,32) encode of 64 x 16 MiB segments plus
+    SHA-256 of all 4,096 fragments per step through the hash-queue pipeline (window W on a second
+    stream), timed over W + 20 steps with the window drained at the end, so every timed batch is
+    fully hashed inside the region. Reports the whole step's rate in fragment bytes (encode and
+    hash of (k+m) x F per segment), the hash ticks against the VALU issue roofline, and a hashlib
+    check of `sample` fragment digests from several pipeline buffers."""
+    import hashlib
+    import torch
+    import cess_amd
+    k, m, F, nseg = CONFIGS[5][0], CONFIGS[5][1], CONFIGS[5][2], CONFIGS[5][3]
+    stream = torch.cuda.Stream(dev)
+    sha_stream = torch.cuda.Stream(dev)
+    enc = cess_amd.New(k, m, device=local)
+    d_data = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
+    d_par = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
+    cess_amd.fill_synthetic(d_data, k * F, nseg, 0, SEED0 + 5, stream=stream)
+    pipe = HashPipeline(enc, d_data, d_par, nseg, F, dev, local, stream, sha_stream, W)
+    for _ in range(warmup):
+        pipe.step()
+    pipe.drain()
+    torch.cuda.synchronize(dev)
+    steps = W + 20
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    a.record(stream)
+    for _ in range(steps):
+        pipe.step()
+    pipe.drain()
+    b.record(stream)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    gpu_ms = a.elapsed_time(b)
+    step_bytes = nseg * (k + m) * F
+    out = {"workload": CONFIGS[5][4], "k": k, "m": m, "fragment_bytes": F, "segments": nseg,
+           "window": W, "steps": steps, "warmup": warmup,
+           "chains_in_flight": W * nseg * (k + m), "tick_blocks": pipe.tick_blocks,
+           "ms_per_step": round(gpu_ms / steps, 4),
+           "step_GBps": round(steps * step_bytes / (gpu_ms * 1e-3) / GB, 1),
+           "step_GBps_host_clock": round(steps * step_bytes / elapsed / GB, 1),
+           "bytes_per_step": step_bytes,
+           "basis": "fragment bytes per step ((k+m) x F per segment: encoded and hashed) / "
+                    "GPU time of the timed steps incl. the final drain (HIP events on the "
+                    "encode stream, which waits for the hash stream at the end)"}
+    slots = load_valu_slots("c5")
+    if slots:
+        blocks = nseg * (k + m) * cess_amd.sha256_blocks(F) * steps
+        ach = blocks * slots["issue_slots_per_block"] / (gpu_ms * 1e-3) / 1e12
+        out["sha_roofline"] = {
+            "bound": "valu", "kernel": "k_sha256_tick1", "achieved": round(ach, 2),
+            "peak": round(VALU_PEAK_TLANE, 2), "unit": "T lane-slots/s",
+            "frac": round(ach / VALU_PEAK_TLANE, 4),
+            "issue_slots_per_block": slots["issue_slots_per_block"],
+            "basis": "whole step (hash ticks share the chip with the encode); peak at 2.4 GHz"}
+    # digests: every batch encodes the same data, so each buffer's hex must be the hashlib digest
+    # of the data fragments and of the parity fragments in that buffer
+    rng = np.random.default_rng(0xC5)
+    ok = True
+    checked = 0
+    for bi in rng.choice(pipe.NB, size=min(pipe.NB, 6), replace=False):
+        hexb = pipe.pipe_hex[int(bi)].cpu().numpy()
+        for s_, f_ in zip(rng.integers(0, nseg, sample // 6), rng.integers(0, k + m, sample // 6)):
+            frag = (d_data[s_, f_] if f_ < k else pipe.pipe_par[int(bi)][s_, f_ - k]).cpu().numpy()
+            ok &= hashlib.sha256(frag.tobytes()).hexdigest().encode() == hexb[s_, f_].tobytes()
+            checked += 1
+    out["digests_checked"] = checked
+    out["digests_match_hashlib"] = bool(ok)
+    enc.close()
+    del pipe, d_data, d_par
+    torch.cuda.empty_cache()
+    return out
+
+
+def line_problems(out: dict) -> list:
+    """What a bench line lacks against the driver's contract and VERDICT's asks (empty = none):
+    the contract keys, `roofline` and `cpu_baseline` at every N (at N > 1 on the CPU share of the
+    GPUs held), and for the default config: at N = 1 the config-5 step with checked digests and
+    the wide-code legs with their cold means; at N > 1 both degraded-read transports (the torch
+    group and libcessec's own RCCL communicator, or the reason it could not form) bit-exact."""
+    bad = []
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                "roofline", "cpu_baseline"):
+        if key not in out:
+            bad.append(f"missing {key}")
+    rl = out.get("roofline") or {}
+    for key in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        if key not in rl:
+            bad.append(f"roofline lacks {key}")
+    cb = out.get("cpu_baseline") or {}
+    for key in ("value", "unit", "cores", "kind", "sample"):
+        if key not in cb:
+            bad.append(f"cpu_baseline lacks {key}")
+    n = out.get("n_gpus", 1)
+    if cb and cb.get("cores", 0) < min(GPU_BOX_CPU_SHARE * cb.get("gpus_in_use", n),
+                                       cb.get("host_cpus_visible") or 1 << 30):
+        bad.append("cpu_baseline below the CPU share of the GPUs in use")
+    if (out.get("config") or {}).get("baseline_config") != 2 or "extra" not in out:
+        return bad
+    ex = out["extra"]
+    if n == 1:
+        c5 = ex.get("config5") or {}
+        if not c5.get("digests_match_hashlib") or not c5.get("step_GBps"):
+            bad.append("extra.config5 missing or its digests unchecked")
+        for name, leg in (ex.get("wide_code") or {}).items():
+            if isinstance(leg, dict) and "ms" in leg and not any(
+                    key.startswith("cold_ms") for key in leg):
+                bad.append(f"wide_code.{name} lacks its cold mean")
+    else:
+        legs = {"degraded_gather": ex.get("degraded_gather"),
+                "degraded_gather_cabi": ex.get("degraded_gather_cabi")}
+        for ename in ("wide_degraded_gather", "wide_degraded_gather_cabi"):
+            w = ex.get(ename) or {}
+            if "skipped" in w:
+                legs[ename] = w
+            for xname in ("survivors", "partials"):
+                if "skipped" not in w:
+                    legs[f"{ename}.{xname}"] = w.get(xname)
+        for name, leg in legs.items():
+            if not leg:
+                bad.append(f"extra.{name} missing")
+            elif "skipped" in leg:
+                if "cabi" not in name:
+                    bad.append(f"extra.{name} skipped")
+            elif leg.get("bit_exact") is not True:
+                bad.append(f"extra.{name} not bit-exact")
+    return bad
 
 
 def main() -> None:
@@ -601,19 +811,7 @@ def main() -> None:
         # the degraded-read gather of 64 segments per rank runs inside every step
         gather = degraded_gather(enc, k, m, F, world, rank, dev, 64, args.exchange)
     if args.config == 5:
-        # Windowed pipeline over steps: step i encodes into parity buffer i % W on the launch
-        # stream, then (on the hash stream, after the encode) adds the batch's 64 * nseg
-        # fragment chains to the GPU hash queue and ticks it once: each tick advances every
-        # live chain by ceil(blocks per fragment / W) blocks, so a batch's hashes complete W
-        # ticks after its encode and W batches hash together (W x nseg x (k+m) chains in
-        # flight). The data batch is read-only and shared; parity and hex are (W+1)-buffered.
         W = max(1, args.window)
-        d_hex = torch.empty((nseg, k + m, 64), dtype=torch.uint8, device=dev)
-        # W + 1 buffers: the batch a step overwrites completed one tick earlier, so the encode
-        # of step i + 1 waits for tick i - 1 and overlaps tick i
-        NB = W + 1
-        pipe_par = [d_par] + [torch.empty_like(d_par) for _ in range(NB - 1)]
-        pipe_hex = [d_hex] + [torch.empty_like(d_hex) for _ in range(NB - 1)]
         # --hash-stream 1: hash queue on its own stream (ticks overlap the next encode);
         # 0: one stream, encode then tick (the tick keeps the whole chip)
         if args.cu_split:
@@ -628,32 +826,15 @@ def main() -> None:
             sha_stream = torch.cuda.Stream(dev, priority=0)
         else:
             sha_stream = torch.cuda.Stream(dev) if args.hash_stream else stream
-        chains = W * nseg * (k + m)
-        hq = cess_amd.HashQueue(capacity=1 << max(10, (chains - 1).bit_length()), device=local,
-                                stream=sha_stream)
-        if args.tick_pf:
-            hq.set_option(1, args.tick_pf)
-        tick_blocks = -(-cess_amd.sha256_blocks(F) // W)
-        ev_enc = [torch.cuda.Event() for _ in range(NB)]
-        ev_free = [torch.cuda.Event() for _ in range(NB)]
-        pipe_i = [0]
+        pipe = HashPipeline(enc, d_data, d_par, nseg, F, dev, local, stream, sha_stream, W,
+                            args.tick_pf)
+        d_hex, tick_blocks = pipe.pipe_hex[0], pipe.tick_blocks
 
     def step():
         if args.config in (3, 6, 7):
             enc.ReconstructBatch(d_data, d_par, nseg, F, present, stream=stream)
         elif args.config == 5:
-            i = pipe_i[0]
-            pipe_i[0] += 1
-            b = i % NB
-            if i >= NB:
-                stream.wait_event(ev_free[b])  # batch i - NB's hashes done: buffer b reusable
-            enc.EncodeBatch(d_data, pipe_par[b], nseg, F, stream=stream)
-            ev_enc[b].record(stream)
-            sha_stream.wait_event(ev_enc[b])
-            hq.add_fragments(d_data, pipe_par[b], nseg, k, m, F, pipe_hex[b])
-            hq.tick(tick_blocks)
-            # this tick completed batch i - W + 1, whose buffer step i + 2 takes
-            ev_free[(i - W + 1) % NB].record(sha_stream)
+            pipe.step()
         elif args.config == 4:
             enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
             gather[0]()
@@ -662,9 +843,7 @@ def main() -> None:
 
     def drain():
         if args.config == 5:
-            hq.finish()
-            if sha_stream is not stream:
-                stream.wait_stream(sha_stream)
+            pipe.drain()
 
     def step_codec():  # the codec kernel alone (config 5's step also hashes)
         if args.config in (3, 6, 7):
@@ -843,7 +1022,7 @@ def main() -> None:
     def gather_leg(run_verify_plan, reps=5, code=(k, F)) -> dict:
         """Time the degraded read (exchange over the process group + rebuild) alone,
         synchronised per rep, max over ranks; verify the rebuilt fragments."""
-        run, verify, plan = run_verify_plan
+        run, verify, plan, close = run_verify_plan
         fb = code[1]
         times = []
         res = None
@@ -864,6 +1043,7 @@ def main() -> None:
         if world > 1:
             dist.all_reduce(v, op=dist.ReduceOp.MAX)
         t, bad = float(v[0]), bool(v[1])
+        close()
         nrebuilt = len(plan.lost)
         kk = code[0]
         return {"segments": nrebuilt, "lost_per_segment": 1,
@@ -881,18 +1061,38 @@ def main() -> None:
     if args.config == 4:
         out["degraded_gather"] = gather_leg(gather)
     elif world > 1 and not args.no_extra and args.config == 2:
-        # config 4's exchange step measured in the default (scaling) run as well
-        out.setdefault("extra", {})["degraded_gather"] = gather_leg(
+        # config 4's exchange step measured in the default (scaling) run as well, through both
+        # transports: the torch.distributed group and libcessec's own RCCL communicator (the C
+        # ABI a Go / Rust host uses), on the same placement and lost list
+        ex_out = out.setdefault("extra", {})
+        ex_out["degraded_gather"] = gather_leg(
             degraded_gather(enc, k, m, F, world, rank, dev, 64))
         # the wide code's single-fragment degraded read, both exchanges: RS(32,32)
         # with 16 MiB segments (F = 512 KiB), 8 fragments per GPU at world 8; 32 segments per GPU
         # keep the survivor leg's grouped point-to-point batch under ~900 transfers per rank
         wk, wm, wF = CONFIGS[5][:3]
         wenc = cess_amd.New(wk, wm, device=local)
-        out["extra"]["wide_degraded_gather"] = {
+        ex_out["wide_degraded_gather"] = {
             ex: gather_leg(degraded_gather(wenc, wk, wm, wF, world, rank, dev, 32, ex),
                            code=(wk, wF))
             for ex in ("survivors", "partials")}
+        if "CESS_DEVICE" in os.environ:
+            # ranks sharing one GPU (the one-GPU rehearsal): RCCL refuses a communicator with
+            # two ranks on one device ("Duplicate GPU detected"), so the C-ABI group cannot form
+            why = ("skipped: the ranks share one GPU (CESS_DEVICE rehearsal) and RCCL refuses "
+                   "two ranks on one device; runs on a multi-GPU node")
+            ex_out["degraded_gather_cabi"] = {"skipped": why}
+            ex_out["wide_degraded_gather_cabi"] = {"skipped": why}
+        else:
+            ex_out["degraded_gather_cabi"] = gather_leg(
+                degraded_gather(enc, k, m, F, world, rank, dev, 64, "survivors", "cabi"))
+            ex_out["wide_degraded_gather_cabi"] = {
+                ex: gather_leg(degraded_gather(wenc, wk, wm, wF, world, rank, dev, 32, ex,
+                                               "cabi"), code=(wk, wF))
+                for ex in ("survivors", "partials")}
+            for leg_ in [ex_out["degraded_gather_cabi"],
+                         *ex_out["wide_degraded_gather_cabi"].values()]:
+                leg_["transport"] = "libcessec cec_dist_degraded_read (own RCCL communicator)"
         wenc.close()
 
     if not args.no_extra and args.config == 2:
@@ -914,6 +1114,8 @@ def main() -> None:
         # the wide code (BASELINE config 5's RS(32,32), 16 MiB segments: F = 512 KiB) in the same
         # run, so the driver's own line carries its encode, restoral and multi-erasure rebuild rates
         out["extra"]["wide_code"] = wide_code_legs(dev, local, stream)
+        # BASELINE config 5 (RS(32,32) encode + SHA-256 of every fragment) as the driver runs it
+        out["extra"]["config5"] = config5_leg(dev, local)
         # the measured-copy ceiling beside the spec peak: a device-to-device copy
         # of the same 1 GiB data batch (HIP's blit kernel), read + write bytes per copy
         src = d_data.view(-1)
@@ -934,8 +1136,12 @@ def main() -> None:
                     "batch through the HIP runtime (torch copy_), read + write bytes / time"}
         del dst
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(k, m, F, args.cpu_seconds)
+    if rank == 0 and not args.no_cpu_baseline:
+        # after the GPU region; at N > 1 on rank 0 alone, on the CPU share of the GPUs the job
+        # holds (16 per GPU: the whole node's at N = 8; ranks sharing one GPU hold one)
+        gpus_held = 1 if "CESS_DEVICE" in os.environ else world
+        out["cpu_baseline"] = cpu_baseline(k, m, F, args.cpu_seconds, gpus_held)
+        out["cpu_baseline"]["node_GBps_gpu"] = out["value"]
         if args.config == 5:
             out["cpu_baseline"]["sha256"] = cpu_sha256(k, m, F, args.cpu_seconds / 2)
 

@@ -117,6 +117,8 @@ SIGNATURES = {
                                                   POINTER(c_size_t)]),
     "cec_audit_random_subject": (c_int, [c_void_p, c_uint32, c_void_p]),
     "cec_audit_random_u64": (c_int, [c_void_p, c_size_t, POINTER(c_uint64)]),
+    "cec_challenge_random_list": (c_int, [c_void_p, c_size_t, c_uint32, c_void_p,
+                                          POINTER(c_size_t)]),
 }
 
 CEC_OK = 0
@@ -136,6 +138,8 @@ CEC_FRAGMENT_COUNT = 3
 CEC_UPLOAD_FILLER_LIMIT = 10
 CEC_FILLER_SIZE = 8 << 20
 CEC_AUDIT_PALLET_ID = b"rewardpt"
+CEC_RANDOMNESS_BYTES = 32
+CEC_CHALLENGE_RANDOM_BYTES = 20
 
 CEC_OPT_FORCE_GENERIC = 1
 CEC_OPT_CT_VARIANT = 2

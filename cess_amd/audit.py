@@ -37,6 +37,27 @@ def challenge_indices(randoms: Sequence[int], chunk_count: int = CHUNK_COUNT,
     return out[:need].tolist(), used.value
 
 
+RANDOM_BYTES = _lib.CEC_CHALLENGE_RANDOM_BYTES
+
+
+def challenge_random_list(randomness: Sequence[bytes], need: int = CHALLENGE_NEED):
+    """NetSnapShot.random_list (c-pallets/audit/src/lib.rs:966-974, generate_challenge_random
+    :1079-1096): randomness[i] = the chain's 32-byte randomness output for the subject
+    (MyPalletId, now + 2 + i) (records.audit_random_subject(now + 2 + i); None as 32 zero bytes).
+    Returns (the `need` distinct 20-byte values in order, outputs consumed)."""
+    buf = b"".join(bytes(r) if r is not None else bytes(32) for r in randomness)
+    if any(r is not None and len(r) != 32 for r in randomness):
+        raise ValueError("each randomness output is 32 bytes (an H256)")
+    src = np.frombuffer(buf, np.uint8).copy() if buf else np.zeros(1, np.uint8)
+    out = np.zeros(max(1, need) * RANDOM_BYTES, np.uint8)
+    used = c_size_t()
+    check(_lib.load().cec_challenge_random_list(src.ctypes.data, len(randomness), need,
+                                                out.ctypes.data, byref(used)),
+          "challenge_random_list")
+    return [out[i * RANDOM_BYTES:(i + 1) * RANDOM_BYTES].tobytes() for i in range(need)], \
+        used.value
+
+
 def audit_chunks(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int,
                  indices: Sequence[int], d_chunks=None, d_hex=None,
                  chunk_count: int = CHUNK_COUNT, stream=None) -> None:

@@ -55,9 +55,13 @@ int set_err(int code, const std::string& msg) {
   } while (0)
 
 // ---- device block pool with stream-ordered retirement -------------------------------------
+// Blocks come from the stream-ordered allocator on the codec's private stream and go back to it
+// with hipFreeAsync: hipMalloc / hipFree would do (hipFree performs an implicit
+// hipDeviceSynchronize), and destroying one codec must not wait for other codecs' work.
 class DevPool {
  public:
   ~DevPool() { drain(); }
+  void set_stream(hipStream_t st) { st_ = st; }
 
   // A block of at least `bytes` (size classes of powers of two from 4 KiB).
   int alloc(size_t bytes, void** out) {
@@ -68,7 +72,9 @@ class DevPool {
       free_[c].pop_back();
       return CEC_OK;
     }
-    HIP_TRY(hipMalloc(out, (size_t)1 << c));
+    // complete before any stream uses it (a rare host wait: freed blocks are reused)
+    HIP_TRY(hipMallocAsync(out, (size_t)1 << c, st_));
+    HIP_TRY(hipStreamSynchronize(st_));
     held_ += (size_t)1 << c;
     return CEC_OK;
   }
@@ -123,7 +129,8 @@ class DevPool {
     done_ = seq_;
     collect();
     for (auto& fl : free_)
-      for (void* p : fl) (void)hipFree(p);
+      for (void* p : fl) (void)hipFreeAsync(p, st_);
+    if (held_) (void)hipStreamSynchronize(st_);
     free_.clear();
     held_ = 0;
     for (hipEvent_t e : evpool_) (void)hipEventDestroy(e);
@@ -151,6 +158,7 @@ class DevPool {
   std::deque<Dead> dead_;  // in retirement order, so tags are non-decreasing
   std::deque<Mark> marks_;
   std::vector<hipEvent_t> evpool_;
+  hipStream_t st_ = nullptr;  // the owner's private stream (allocations and frees)
   uint64_t seq_ = 0;   // marks recorded
   uint64_t done_ = 0;  // every mark <= done_ has completed
   size_t held_ = 0;
@@ -443,7 +451,10 @@ struct cec_codec {
     lru.clear();
     encode.reset();
     pool.drain();
-    if (stage) (void)hipFree(stage);
+    if (stage) {
+      (void)hipFreeAsync(stage, stream);  // the host API's calls synchronise before returning
+      (void)hipStreamSynchronize(stream);
+    }
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -713,12 +724,13 @@ int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* s
   return check_launch();
 }
 
-int ensure(uint8_t** buf, size_t* have, size_t need) {
+// Grow a buffer used only on stream `st` (stream-ordered: no device-wide synchronisation).
+int ensure(uint8_t** buf, size_t* have, size_t need, hipStream_t st) {
   if (*have >= need) return CEC_OK;
-  if (*buf) (void)hipFree(*buf);
+  if (*buf) (void)hipFreeAsync(*buf, st);
   *buf = nullptr;
   *have = 0;
-  HIP_TRY(hipMalloc(buf, need));
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(buf), need, st));
   *have = need;
   return CEC_OK;
 }
@@ -990,6 +1002,7 @@ int cec_create(int k, int m, int device, cec_codec** out) {
       return set_err(CEC_EINVAL, "singular Vandermonde top block");
   }
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  c->pool.set_stream(c->stream);
   {
     auto par = std::make_unique<BigMat>();
     uint8_t in_idx[cec::kMaxShards], out_idx[cec::kMaxShards];
@@ -1250,10 +1263,11 @@ int cec_sha256_hex(const uint8_t* const* d_bufs, size_t n, size_t len, uint8_t* 
   hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
   const uint8_t** dptrs = nullptr;
   uint8_t* dhex = nullptr;
-  HIP_TRY(hipMalloc(&dptrs, n * sizeof(void*)));
-  hipError_t e = hipMalloc(&dhex, n * 64);
+  // stream-ordered (hipFree would synchronise the whole device)
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dptrs), n * sizeof(void*), st));
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&dhex), n * 64, st);
   if (e != hipSuccess) {
-    (void)hipFree(dptrs);
+    (void)hipFreeAsync(dptrs, st);
     return set_err(CEC_ENOMEM, "hex buffer");
   }
   int rc = CEC_OK;
@@ -1265,8 +1279,8 @@ int cec_sha256_hex(const uint8_t* const* d_bufs, size_t n, size_t len, uint8_t* 
     e = hipStreamSynchronize(st);
   } while (0);
   if (e != hipSuccess) rc = set_err(CEC_EHIP, std::string("sha256: ") + hipGetErrorString(e));
-  (void)hipFree(dptrs);
-  (void)hipFree(dhex);
+  (void)hipFreeAsync(dptrs, st);
+  (void)hipFreeAsync(dhex, st);
   return rc;
 }
 
@@ -1382,7 +1396,7 @@ int cec_encode(cec_codec* c, uint8_t* const* shards, size_t shard_len) {
     if (!shards[i]) return set_err(CEC_EINVAL, "null shard");
   HIP_TRY(hipSetDevice(c->device));
   const size_t stride = pad256(shard_len);
-  int rc = ensure(&c->stage, &c->stage_bytes, stride * n);
+  int rc = ensure(&c->stage, &c->stage_bytes, stride * n, c->stream);
   if (rc) return rc;
   Layout L = stage_layout(c, shard_len);
   for (int i = 0; i < c->k; ++i)
@@ -1410,7 +1424,7 @@ int cec_reconstruct(cec_codec* c, uint8_t* const* shards, const uint8_t* present
   for (int i = 0; i < n; ++i)
     if (!shards[i]) return set_err(CEC_EINVAL, "null shard");
   const size_t stride = pad256(shard_len);
-  rc = ensure(&c->stage, &c->stage_bytes, stride * n);
+  rc = ensure(&c->stage, &c->stage_bytes, stride * n, c->stream);
   if (rc) return rc;
   Layout L = stage_layout(c, shard_len);
   // Upload only the survivors the plan reads.
@@ -1439,7 +1453,7 @@ int cec_verify(cec_codec* c, uint8_t* const* shards, size_t shard_len, int* ok) 
     if (!shards[i]) return set_err(CEC_EINVAL, "null shard");
   HIP_TRY(hipSetDevice(c->device));
   const size_t stride = pad256(shard_len);
-  int rc = ensure(&c->stage, &c->stage_bytes, stride * n);
+  int rc = ensure(&c->stage, &c->stage_bytes, stride * n, c->stream);
   if (rc) return rc;
   Layout L = stage_layout(c, shard_len);
   for (int i = 0; i < c->k; ++i)

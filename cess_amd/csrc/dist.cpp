@@ -166,17 +166,23 @@ struct cec_dist {
   size_t pstage_bytes = 0;
   int* d_flag = nullptr;
   bool broken = false;  // the communicator was aborted after a failure inside a transfer group
+  // Device memory is stream-ordered (hipMallocAsync / hipFreeAsync): hipFree performs an implicit
+  // hipDeviceSynchronize, which would stall every other codec on the device. `done` is recorded on
+  // the caller's stream at the end of every degraded read (its last enqueued work); destruction
+  // waits for it alone and frees on the handle's own stream.
+  hipStream_t own = nullptr;
+  hipEvent_t done = nullptr;
+  bool used = false;
 };
 
 namespace {
-// Grow a device buffer (its old contents may still be read by work queued on `st`).
+// Grow a device buffer on `st` (the caller's stream, ordered after the previous call's `done`).
 int grow(uint8_t** buf, size_t* have, size_t need, hipStream_t st) {
   if (need <= *have) return CEC_OK;
-  DI_TRY(hipStreamSynchronize(st));
-  DI_TRY(hipFree(*buf));
+  if (*buf) DI_TRY(hipFreeAsync(*buf, st));
   *buf = nullptr;
   *have = 0;
-  DI_TRY(hipMalloc(buf, need));
+  DI_TRY(hipMallocAsync(reinterpret_cast<void**>(buf), need, st));
   *have = need;
   return CEC_OK;
 }
@@ -211,16 +217,29 @@ int cec_dist_create(cec_codec* codec, const uint8_t* id, int world, int rank, ce
   (void)hipGetDevice(&prev);
   hipError_t he = hipSetDevice(d->device);
   ncclResult_t res = he == hipSuccess ? r.comm_init_rank(&d->comm, world, u, rank) : ncclSuccess;
-  if (he == hipSuccess && res == ncclSuccess) he = hipMalloc(&d->d_flag, sizeof(int));
-  (void)hipSetDevice(prev);
+  if (he == hipSuccess && res == ncclSuccess)
+    he = hipStreamCreateWithFlags(&d->own, hipStreamNonBlocking);
+  if (he == hipSuccess && res == ncclSuccess)
+    he = hipEventCreateWithFlags(&d->done, hipEventDisableTiming);
+  if (he == hipSuccess && res == ncclSuccess)
+    he = hipMallocAsync(reinterpret_cast<void**>(&d->d_flag), sizeof(int), d->own);
+  if (he == hipSuccess && res == ncclSuccess) he = hipStreamSynchronize(d->own);
   if (he != hipSuccess || res != ncclSuccess) {
     int rc = he != hipSuccess ? cec::set_error(CEC_EHIP, std::string("dist create: ") +
                                                              hipGetErrorString(he))
                               : nccl_err(res, "ncclCommInitRank");
     if (d->comm) r.comm_destroy(d->comm);
+    if (d->d_flag) (void)hipFreeAsync(d->d_flag, d->own);
+    if (d->own) {
+      (void)hipStreamSynchronize(d->own);
+      (void)hipStreamDestroy(d->own);
+    }
+    if (d->done) (void)hipEventDestroy(d->done);
+    (void)hipSetDevice(prev);
     delete d;
     return rc;
   }
+  (void)hipSetDevice(prev);
   *out = d;
   return CEC_OK;
 }
@@ -230,11 +249,16 @@ void cec_dist_destroy(cec_dist* d) {
   int prev = 0;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(d->device);
-  (void)hipDeviceSynchronize();
+  // only this handle's work: the last degraded read's tail on its caller's stream (a failed call
+  // may have left copies or transfers queued there); other streams of the device keep running
+  if (d->used) (void)hipEventSynchronize(d->done);
   if (d->comm) rccl().comm_destroy(d->comm);
-  (void)hipFree(d->stage);
-  (void)hipFree(d->pstage);
-  (void)hipFree(d->d_flag);
+  if (d->stage) (void)hipFreeAsync(d->stage, d->own);
+  if (d->pstage) (void)hipFreeAsync(d->pstage, d->own);
+  if (d->d_flag) (void)hipFreeAsync(d->d_flag, d->own);
+  (void)hipStreamSynchronize(d->own);
+  (void)hipStreamDestroy(d->own);
+  (void)hipEventDestroy(d->done);
   (void)hipSetDevice(prev);
   delete d;
 }
@@ -335,6 +359,14 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
   } restore{prev};
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
   if (d->broken) return cec::set_error(CEC_ENCCL, "dist degraded read: group aborted earlier");
+  // after the previous call's tail (it may have run on another stream), and `done` recorded after
+  // whatever this call enqueues, on every return path
+  if (d->used) DI_TRY(hipStreamWaitEvent(st, d->done, 0));
+  struct Tail {
+    cec_dist* d;
+    hipStream_t st;
+    ~Tail() { d->used = hipEventRecord(d->done, st) == hipSuccess || d->used; }
+  } tail{d, st};
 
   // Rounds of at most kRound segments of the plan (the same split on every rank) bound the
   // staging; rounds follow each other on the stream, so a round's receives land after the

@@ -225,6 +225,28 @@ int cec_audit_random_subject(const uint8_t* pallet_id, uint32_t seed, uint8_t* o
   return CEC_OK;
 }
 
+// NetSnapShot.random_list (c-pallets/audit/src/lib.rs:966-974): for seed = now + 1, now + 2, ...
+// generate_challenge_random(seed) (:1079-1096) asks the randomness for the subject
+// (MyPalletId, seed + 1) and returns the first 20 bytes of the H256 the output decodes as (an H256
+// is 32 bytes, so its loop ends on the first try); values already in the list are skipped.
+int cec_challenge_random_list(const uint8_t* randomness, size_t nrand, uint32_t need,
+                              uint8_t* out, size_t* used) {
+  if ((nrand && !randomness) || (need && !out)) return cec::set_error(CEC_EINVAL, "null");
+  constexpr size_t kB = CEC_CHALLENGE_RANDOM_BYTES;
+  uint32_t got = 0;
+  size_t i = 0;
+  for (; i < nrand && got < need; ++i) {
+    const uint8_t* v = randomness + i * CEC_RANDOMNESS_BYTES;
+    bool seen = false;
+    for (uint32_t q = 0; q < got && !seen; ++q) seen = std::memcmp(out + q * kB, v, kB) == 0;
+    if (!seen) std::memcpy(out + (got++) * kB, v, kB);
+  }
+  if (used) *used = i;
+  if (got < need)
+    return cec::set_error(CEC_EINVAL, "randomness stream exhausted before `need` values");
+  return CEC_OK;
+}
+
 int cec_audit_random_u64(const uint8_t* randomness, size_t len, uint64_t* out) {
   if (!randomness || !out) return cec::set_error(CEC_EINVAL, "null");
   if (len < 8) return cec::set_error(CEC_EINVAL, "u64 decode needs at least 8 bytes");

@@ -369,6 +369,18 @@ int cec_scale_restoral_order_complete(const uint8_t* fragment_hex, uint8_t* out,
 int cec_audit_random_subject(const uint8_t* pallet_id /* 8 bytes */, uint32_t seed,
                              uint8_t* out12);
 int cec_audit_random_u64(const uint8_t* randomness, size_t len, uint64_t* out);
+/* The challenge's random_list (NetSnapShot.random_list, c-pallets/audit/src/lib.rs:966-974): for
+ * seed = now + 1, now + 2, ... (now = the block number), generate_challenge_random(seed)
+ * (lib.rs:1079-1096) asks the randomness for the subject (MyPalletId, seed + 1) and keeps the first
+ * 20 bytes of the H256 output; values already listed are skipped, until need = 47 values.
+ * `randomness` holds nrand outputs of CEC_RANDOMNESS_BYTES each, output i being the chain's
+ * randomness for cec_audit_random_subject(pallet, now + 2 + i) (a None output as 32 zero bytes,
+ * the pallet's Default). Writes need * CEC_CHALLENGE_RANDOM_BYTES bytes to `out`; *used = outputs
+ * consumed. CEC_EINVAL when the stream runs out first. Host only. */
+#define CEC_RANDOMNESS_BYTES 32
+#define CEC_CHALLENGE_RANDOM_BYTES 20
+int cec_challenge_random_list(const uint8_t* randomness, size_t nrand, uint32_t need,
+                              uint8_t* out, size_t* used);
 /* 68-byte shard id = 64 hex chars ++ "-NNN" (index 0..999), the form Hash::from_shard_id reads
  * back (primitives/common/src/lib.rs:45-49; c-pallets/audit/src/tests.rs:267-269 builds
  * file_hash ++ "-001"). */

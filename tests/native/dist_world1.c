@@ -3,7 +3,8 @@
  * is encoded in HBM, segment s loses fragment s mod (k+m), the group rebuilds them through
  * cec_dist_degraded_read (plan, agreement all-reduce, local survivor copies, rebuild), and every
  * rebuilt fragment must equal the original; cec_dist_plan must name rank 0 for every entry, and a
- * locate callback that misses a survivor must fail with CEC_EINVAL.
+ * locate callback that misses a survivor must fail with CEC_EINVAL. Last, a dist handle and its codec
+ * are destroyed while another codec's batch runs on a side stream (destroy_under_load).
  * build: gcc -O2 -D__HIP_PLATFORM_AMD__ tests/native/dist_world1.c -Iinclude -I/opt/rocm/include
  *            -Lcess_amd -lcessec -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,... -o dist_world1 */
 #include <hip/hip_runtime_api.h>
@@ -96,9 +97,96 @@ static int run(int k, int m, size_t nseg, size_t F) {
   return 0;
 }
 
+/* GF(2^8) (0x11D) doubling of 4 packed bytes */
+static uint32_t xt4(uint32_t x) {
+  const uint32_t hi = x & 0x80808080u;
+  return ((x & 0x7F7F7F7Fu) << 1) ^ ((hi >> 7) * 0x1Du);
+}
+
+/* Destroying a dist handle (and then its codec) while another codec's long batch is still
+ * running on a side stream: the side work must complete bit-exact (RS(2,1) parity p = 3 d0 ^ 2 d1
+ * recomputed on the host), and the handle's destruction waits for its own work only. Prints
+ * whether the side stream was still busy right after each destroy (1: not drained by it). */
+static int destroy_under_load(void) {
+  const size_t F = (size_t)8 << 20, nseg = 16;
+  const int reps = 400;
+  cec_codec *c = NULL, *side_codec = NULL;
+  CHECK(cec_create(4, 2, 0, &c) == CEC_OK);
+  CHECK(cec_create(2, 1, 0, &side_codec) == CEC_OK);
+  hipStream_t side;
+  CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking) == hipSuccess);
+  uint8_t *d_data, *d_par;
+  CHECK(hipMalloc((void**)&d_data, nseg * 2 * F) == hipSuccess);
+  CHECK(hipMalloc((void**)&d_par, nseg * F) == hipSuccess);
+  CHECK(cec_fill_synthetic(d_data, 2 * F, nseg, 0, 0xCE550009u, side) == CEC_OK);
+  /* the dist handle does one degraded read first (staging allocated, `done` recorded) */
+  const size_t Fd = 65536, nd = 6;
+  store_t st = {4, 2, Fd, NULL, NULL, (uint64_t)-1, -1};
+  CHECK(hipMalloc((void**)&st.d_data, nd * 4 * Fd) == hipSuccess);
+  CHECK(hipMalloc((void**)&st.d_par, nd * 2 * Fd) == hipSuccess);
+  CHECK(cec_fill_synthetic(st.d_data, 4 * Fd, nd, 0, 0xCE550004u, NULL) == CEC_OK);
+  CHECK(cec_encode_batch(c, st.d_data, st.d_par, nd, Fd, NULL) == CEC_OK);
+  CHECK(hipDeviceSynchronize() == hipSuccess);
+  uint64_t seg[6];
+  uint8_t frag[6];
+  uint8_t* out[6];
+  for (size_t s = 0; s < nd; ++s) {
+    seg[s] = s;
+    frag[s] = (uint8_t)(s % 6);
+    CHECK(hipMalloc((void**)&out[s], Fd) == hipSuccess);
+  }
+  uint8_t id[CEC_DIST_ID_BYTES];
+  cec_dist* d = NULL;
+  CHECK(cec_dist_unique_id(id) == CEC_OK);
+  CHECK(cec_dist_create(c, id, 1, 0, &d) == CEC_OK);
+  CHECK(cec_dist_degraded_read(d, seg, frag, nd, Fd, locate, &st, out, NULL, NULL) == CEC_OK);
+  /* a long batch on the side stream, then the destroys while it runs */
+  for (int r = 0; r < reps; ++r)
+    CHECK(cec_encode_batch(side_codec, d_data, d_par, nseg, F, side) == CEC_OK);
+  cec_dist_destroy(d);
+  const int busy_dist = hipStreamQuery(side) == hipErrorNotReady;
+  cec_destroy(c);
+  const int busy_codec = hipStreamQuery(side) == hipErrorNotReady;
+  CHECK(hipStreamSynchronize(side) == hipSuccess);
+  printf("side stream busy after dist destroy: %d, after codec destroy: %d\n", busy_dist,
+         busy_codec);
+  /* the side work is complete and bit-exact */
+  uint32_t* h = malloc(nseg * 3 * F);
+  CHECK(h != NULL);
+  CHECK(hipMemcpy(h, d_data, nseg * 2 * F, hipMemcpyDeviceToHost) == hipSuccess);
+  uint32_t* hp = h + nseg * 2 * F / 4;
+  CHECK(hipMemcpy(hp, d_par, nseg * F, hipMemcpyDeviceToHost) == hipSuccess);
+  for (size_t s = 0; s < nseg; ++s) {
+    const uint32_t* d0 = h + s * 2 * F / 4;
+    const uint32_t* d1 = d0 + F / 4;
+    const uint32_t* p = hp + s * F / 4;
+    for (size_t w = 0; w < F / 4; ++w) CHECK(p[w] == (xt4(d0[w] ^ d1[w]) ^ d0[w]));
+  }
+  /* and the degraded read's outputs were right */
+  uint8_t* got = malloc(Fd);
+  uint8_t* want = malloc(Fd);
+  for (size_t s = 0; s < nd; ++s) {
+    CHECK(hipMemcpy(got, out[s], Fd, hipMemcpyDeviceToHost) == hipSuccess);
+    CHECK(hipMemcpy(want, locate(&st, s, frag[s]), Fd, hipMemcpyDeviceToHost) == hipSuccess);
+    CHECK(memcmp(got, want, Fd) == 0);
+    (void)hipFree(out[s]);
+  }
+  free(h);
+  free(got);
+  free(want);
+  (void)hipFree(st.d_data);
+  (void)hipFree(st.d_par);
+  (void)hipFree(d_data);
+  (void)hipFree(d_par);
+  (void)hipStreamDestroy(side);
+  cec_destroy(side_codec);
+  return 0;
+}
+
 int main(void) {
   if (run(2, 1, 12, (size_t)1 << 20)) return 1;
   if (run(4, 2, 9, 65536 + 64)) return 1;
+  if (destroy_under_load()) return 1;
   printf("dist world1 ok\n");
   return 0;
 }

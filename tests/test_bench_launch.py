@@ -73,3 +73,55 @@ def test_kernel_label_every_config():
     mixed = bench.kernel_label(6, 1.0, 24, False, 0, 32, 0.66)
     assert "k_fftdec_m (34%" in mixed and "k_fftdec_d (66%)" in mixed
     assert bench.kernel_label(2, None, 1, True, 0, 2) == "k_rthx"
+
+
+def _line(n, **extra):
+    line = {"metric": bench.METRIC, "value": 1.0, "unit": "GB/s", "n_gpus": n, "steps": 1,
+            "warmup": 1, "ms_per_step": 1.0, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"baseline_config": 2},
+            "roofline": {"bound": "hbm", "achieved": 1, "peak": 8000, "unit": "GB/s",
+                         "frac": 0.1, "traffic": None},
+            "cpu_baseline": {"value": 1, "unit": "GB/s", "cores": 16 * n, "kind": "port",
+                             "sample": "s", "gpus_in_use": n, "host_cpus_visible": 256}}
+    line.update(extra)
+    return line
+
+
+def test_line_keys_multi_gpu():
+    """The N > 1 default line must carry cpu_baseline at the node's CPU share and both
+    degraded-read transports (torch group, libcessec's own RCCL communicator) bit-exact."""
+    ok_leg = {"bit_exact": True, "gather_GBps": 1.0}
+    extra = {"degraded_gather": ok_leg, "degraded_gather_cabi": ok_leg,
+             "wide_degraded_gather": {"survivors": ok_leg, "partials": ok_leg},
+             "wide_degraded_gather_cabi": {"survivors": ok_leg, "partials": ok_leg}}
+    assert bench.line_problems(_line(8, extra=extra)) == []
+    # the C-ABI group may be skipped only with its reason (ranks sharing one GPU)
+    rehearsal = dict(extra, degraded_gather_cabi={"skipped": "ranks share one GPU"},
+                     wide_degraded_gather_cabi={"skipped": "ranks share one GPU"})
+    line = _line(2, extra=rehearsal)
+    line["cpu_baseline"].update(cores=16, gpus_in_use=1)
+    assert bench.line_problems(line) == []
+    # a dropped cpu_baseline, a non-bit-exact exchange or a missing transport are problems
+    no_cpu = _line(8, extra=extra)
+    del no_cpu["cpu_baseline"]
+    assert "missing cpu_baseline" in bench.line_problems(no_cpu)
+    few = _line(8, extra=extra)
+    few["cpu_baseline"]["cores"] = 16
+    assert any("CPU share" in p for p in bench.line_problems(few))
+    wrong = dict(extra, degraded_gather_cabi={"bit_exact": False})
+    assert "extra.degraded_gather_cabi not bit-exact" in bench.line_problems(_line(8, extra=wrong))
+    gone = dict(extra)
+    del gone["wide_degraded_gather_cabi"]
+    assert any("wide_degraded_gather_cabi" in p for p in bench.line_problems(_line(8, extra=gone)))
+
+
+def test_line_keys_one_gpu():
+    """The N = 1 default line carries config 5's step with checked digests and the wide-code
+    legs with their cold means."""
+    extra = {"config5": {"step_GBps": 1300.0, "digests_match_hashlib": True},
+             "wide_code": {"encode": {"ms": 0.37, "cold_ms_first30": 0.38}}}
+    assert bench.line_problems(_line(1, extra=extra)) == []
+    assert bench.line_problems(_line(1, extra=dict(extra, config5={"step_GBps": 1.0})))
+    cold_less = dict(extra, wide_code={"encode": {"ms": 0.37}})
+    assert bench.line_problems(_line(1, extra=cold_less)) == ["wide_code.encode lacks its cold mean"]

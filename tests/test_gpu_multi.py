@@ -253,3 +253,9 @@ def test_c_dist_from_c(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
     assert "dist world1 ok" in r.stdout
+    # destroy_under_load: a dist handle and its codec destroyed while another codec's batch ran
+    # on a side stream (that batch then checked bit-exact); whether the side stream was still
+    # running right after each destroy is reported (1 = the destroy did not drain the device)
+    busy = [ln for ln in r.stdout.splitlines() if ln.startswith("side stream busy")]
+    assert busy, r.stdout
+    print(busy[0])

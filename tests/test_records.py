@@ -177,3 +177,55 @@ def test_audit_random_subject():
         if len(want) == 47:
             break
     assert list(idx) == want and used == 48
+
+
+def _random_list_restated(now, randomness_of, need=47):
+    """c-pallets/audit/src/lib.rs:966-974 with generate_challenge_random (:1079-1096) inlined,
+    line for line: seed from `now`, seed += 1, increase = seed + 1, randomness of
+    (MyPalletId, increase).encode(), H256 decode, first 20 bytes, pushed unless already listed.
+    `randomness_of(subject)` stands in for T::MyRandomness (None -> Default::default())."""
+    random_list = []
+    seed = now
+    while len(random_list) < need:
+        seed = seed + 1
+        increase = seed
+        while True:
+            increase += 1
+            r_seed = randomness_of(records.AUDIT_PALLET_ID + struct.pack("<I", increase))
+            random_seed = r_seed if r_seed is not None else bytes(32)
+            if len(random_seed) >= 20:
+                random_number = random_seed[0:20]
+                break
+        if random_number not in random_list:
+            random_list.append(random_number)
+    return random_list
+
+
+@pytest.mark.parametrize("now", [0, 1, 20220509])
+def test_challenge_random_list(now):
+    """NetSnapShot.random_list: cec_challenge_random_list over the randomness outputs for
+    subjects (MyPalletId, now + 2 + i) equals the pallet's loop, duplicates and None outputs
+    included (blake2b stands in for the chain's randomness, which is chain state)."""
+    from cess_amd import audit
+
+    def rnd(subject):
+        seed = struct.unpack("<I", subject[8:])[0]
+        if seed % 11 == 3:
+            return None  # the randomness source had no output: Default (zeros)
+        # every 5th subject repeats an earlier output: the loop must skip the duplicate
+        key = seed - (seed % 5 == 0) * 2
+        return hashlib.blake2b(records.AUDIT_PALLET_ID + struct.pack("<I", key),
+                               digest_size=32).digest()
+
+    want = _random_list_restated(now, rnd)
+    outputs = [rnd(records.audit_random_subject(now + 2 + i)) for i in range(80)]
+    got, used = audit.challenge_random_list(outputs)
+    assert got == want and len(got) == audit.CHALLENGE_NEED
+    assert len(set(got)) == len(got)
+    # consumed exactly up to the 47th distinct value
+    assert audit.challenge_random_list(outputs[:used])[0] == want
+    import cess_amd
+    with pytest.raises(cess_amd.CecError):
+        audit.challenge_random_list(outputs[:used - 1])
+    with pytest.raises(ValueError):
+        audit.challenge_random_list([b"short"])
