@@ -125,3 +125,20 @@ def test_line_keys_one_gpu():
     assert bench.line_problems(_line(1, extra=dict(extra, config5={"step_GBps": 1.0})))
     cold_less = dict(extra, wide_code={"encode": {"ms": 0.37}})
     assert bench.line_problems(_line(1, extra=cold_less)) == ["wide_code.encode lacks its cold mean"]
+
+
+@pytest.mark.parametrize("name", ["bench_default_a.json", "bench_gpus2_gloo_one_gpu_a.json"])
+def test_recorded_lines_have_every_key(name):
+    """The lines this round's GPU runs printed (profiles/r04/): the N = 1 default line and the
+    one-GPU rehearsal of the N = 2 line (two gloo ranks sharing GPU 0) carry everything
+    line_problems() asks for."""
+    import json
+    path = os.path.join(ROOT, "profiles", "r04", name)
+    with open(path) as f:
+        line = json.load(f)
+    assert bench.line_problems(line) == []
+    if line["n_gpus"] > 1:
+        ex = line["extra"]
+        assert ex["degraded_gather"]["bit_exact"] and ex["degraded_gather"]["backend"] == "gloo"
+        assert all(ex["wide_degraded_gather"][x]["bit_exact"] for x in ("survivors", "partials"))
+        assert "RCCL refuses" in ex["degraded_gather_cabi"]["skipped"]
