@@ -117,6 +117,7 @@ SIGNATURES = {
                                                   POINTER(c_size_t)]),
     "cec_audit_random_subject": (c_int, [c_void_p, c_uint32, c_void_p]),
     "cec_audit_random_u64": (c_int, [c_void_p, c_size_t, POINTER(c_uint64)]),
+    "cec_survivors": (c_int, [c_int, c_int, c_void_p, c_void_p]),
     "cec_challenge_random_list": (c_int, [c_void_p, c_size_t, c_uint32, c_void_p,
                                           POINTER(c_size_t)]),
 }

@@ -570,10 +570,11 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* ou
   }
   auto& sc = c->plan_scratch();
   auto* plan = &sc.plan;
-  uint8_t flags[cec::kMaxShards];
+  uint8_t flags[cec::kMaxShards], rd[cec::kMaxShards];
   for (int i = 0; i < n; ++i) flags[i] = key[1 + i];
-  if (cec::gf_decode_plan_sys(c->k, c->m, flags, data_only, *c->E, *plan, sc.a, sc.ainv,
-                              sc.work) != 0)
+  if (!cec::survivor_set(c->k, c->m, flags, rd) ||
+      cec::gf_decode_plan_sys(c->k, c->m, flags, data_only, *c->E, *plan, sc.a, sc.ainv, sc.work,
+                              rd) != 0)
     return set_err(CEC_ETOOFEW, "fewer than k shards present");
   ProgPtr prog;
   if (plan->nout > 0) {
@@ -602,7 +603,7 @@ int get_decode(cec_codec* c, const uint8_t* present, bool data_only, ProgPtr* ou
 }
 
 // Partial decode program (the partial-product exchange of SURVEY.md §8e): the decode rows of
-// pattern `present` (survivors = its first k present shards) restricted to the survivors flagged
+// pattern `present` (survivors = survivor_set's, cec_survivors) restricted to the survivors flagged
 // in `held`. The rebuild is linear in the survivors, so the XOR of the partials over any
 // partition of the survivors is the full rebuild. No held survivor: a zero program (one input
 // column with zero coefficients), so the outputs are still written (as zeros). Cached in the
@@ -619,10 +620,11 @@ int get_partial(cec_codec* c, const uint8_t* present, const uint8_t* held, bool 
   }
   auto& sc = c->plan_scratch();
   auto* plan = &sc.plan;
-  uint8_t flags[cec::kMaxShards];
+  uint8_t flags[cec::kMaxShards], rd[cec::kMaxShards];
   for (int i = 0; i < n; ++i) flags[i] = present[i] ? 1 : 0;
-  if (cec::gf_decode_plan_sys(c->k, c->m, flags, data_only, *c->E, *plan, sc.a, sc.ainv,
-                              sc.work) != 0)
+  if (!cec::survivor_set(c->k, c->m, flags, rd) ||
+      cec::gf_decode_plan_sys(c->k, c->m, flags, data_only, *c->E, *plan, sc.a, sc.ainv, sc.work,
+                              rd) != 0)
     return set_err(CEC_ETOOFEW, "fewer than k shards present");
   ProgPtr prog;
   if (plan->nout > 0) {
@@ -685,6 +687,9 @@ bool is_reencode(const cec_codec* c, const Program& p) {
 // an output; profiles/r03/fdd_libs_ab1.jsonl).
 double fdd_cost(int nout) { return 647.0 + 5.4 * nout; }
 enum FdKind { kFdNone = 0, kFdM = 1, kFdD = 2 };
+// tuning build: CEC_OPT_CT_VARIANT of this value runs the one-block-per-wave k_fftdec_d instead of
+// the pipelined k_fftdec_dp (A/B sweeps)
+constexpr int kCtVariantFddBlock = 70;
 int fftdec_choice(int nout, int nrs, bool has_m, bool has_d) {
   const double alt = nout <= 4 ? 130.0 + 57.0 * nout : 235.0 + 33.9 * nout;
   const double m = has_m ? 280.0 + (cec::fftdec_big(nrs) ? 3.8 : 3.3) * nout * nrs : 1e30;
@@ -713,7 +718,8 @@ int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* s
   const int fk = use_fftdec(c, p);
   if ((fk == kFdM && cec::launch_fftdec(L, p.fd_side, cec::fftdec_big(p.fd_nrs), p.fd, nullptr,
                                         seg_list, nseg, st)) ||
-      (fk == kFdD && cec::launch_fftdec_d(L, p.fdd, nullptr, seg_list, nseg, st))) {
+      (fk == kFdD && cec::launch_fftdec_d(L, p.fdd, nullptr, seg_list, nseg, st,
+                                          c->opts.ct_variant != kCtVariantFddBlock))) {
     c->fd_segments += nseg;
     if (fk == kFdD) c->fdd_segments += nseg;
     return check_launch();
@@ -917,7 +923,8 @@ int launch_ps_plan(cec_codec* c, const PsPlan& p, const Layout& L, hipStream_t s
   const uint32_t* const* ptrs = static_cast<const uint32_t* const*>(p.ptrs);
   for (const auto& f : p.fd) {
     const bool ok = f.side == 2 ? cec::launch_fftdec_d(L, nullptr, ptrs + f.off, p.list + f.off,
-                                                       (uint32_t)f.count, st)
+                                                       (uint32_t)f.count, st,
+                                                       c->opts.ct_variant != kCtVariantFddBlock)
                                 : cec::launch_fftdec(L, f.side, f.big, nullptr, ptrs + f.off,
                                                      p.list + f.off, (uint32_t)f.count, st);
     if (!ok)

@@ -4,7 +4,7 @@
 // Placement: fragment f of segment s lives on rank (s + f) mod world, the GPU analogue of the
 // chain's miner assignment (random_assign_miner, c-pallets/file-bank/src/functions.rs:187-283,
 // which puts a segment's fragments on distinct miners). A degraded read gathers, for every
-// segment with lost fragments, the first k surviving fragments (the codec's survivor choice) on
+// segment with lost fragments, the k survivors the codec reads (cec_survivors) on
 // the rank that owns the segment's first lost fragment (repair restores a fragment where it
 // lives, c-pallets/file-bank/src/lib.rs:943-1122), straight into a [seg][shard][F] staging batch,
 // and rebuilds the lost fragments there with one cec_reconstruct_batch (per-segment patterns).
@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../include/cess_ec.h"
+#include "fftdec_plan.h"
 
 namespace cec {
 int set_error(int code, const std::string& msg);
@@ -105,7 +106,7 @@ struct Seg {
   uint64_t seg;
   std::vector<int> lost;  // sorted, distinct
   int decoder;
-  std::vector<int> surv;  // first k present fragments
+  std::vector<int> surv;  // the k survivors the rebuild reads (cec_survivors)
   bool partial = false;   // partial-product exchange: `holders` send one partial per lost
   std::vector<int> holders;  // ranks other than the decoder holding survivors, ascending
 };
@@ -133,8 +134,13 @@ int make_plan(int k, int m, int world, int exchange, const uint64_t* lost_seg,
       return cec::set_error(CEC_ETOOFEW, "dist plan: segment " + std::to_string(s) + " lost " +
                                              std::to_string(v.size()) + " > m fragments");
     Seg g{s, v, owner(s, v[0], world), {}};
-    for (int f = 0; f < k + m && (int)g.surv.size() < k; ++f)
-      if (!std::binary_search(v.begin(), v.end(), f)) g.surv.push_back(f);
+    {
+      uint8_t pres[256], sv[256];
+      for (int f = 0; f < k + m; ++f) pres[f] = !std::binary_search(v.begin(), v.end(), f);
+      int rc = cec_survivors(k, m, pres, sv);
+      if (rc) return rc;
+      g.surv.assign(sv, sv + k);
+    }
     size_t n_surv = 0;
     for (int f : g.surv) {
       const int o = owner(s, f, world);
@@ -189,6 +195,19 @@ int grow(uint8_t** buf, size_t* have, size_t need, hipStream_t st) {
 }  // namespace
 
 extern "C" {
+
+int cec_survivors(int k, int m, const uint8_t* present, uint8_t* survivors) {
+  if (!present || !survivors) return cec::set_error(CEC_EINVAL, "null");
+  if (k < 1 || m < 1 || k + m > cec::kMaxShards)
+    return cec::set_error(CEC_EINVAL, "need k >= 1, m >= 1, k + m <= 256");
+  uint8_t flags[cec::kMaxShards], rd[cec::kMaxShards];
+  for (int i = 0; i < k + m; ++i) flags[i] = present[i] ? 1 : 0;
+  if (!cec::survivor_set(k, m, flags, rd))
+    return cec::set_error(CEC_ETOOFEW, "fewer than k shards present");
+  for (int i = 0, o = 0; i < k + m; ++i)
+    if (rd[i]) survivors[o++] = (uint8_t)i;
+  return CEC_OK;
+}
 
 int cec_dist_unique_id(uint8_t* id) {
   if (!id) return cec::set_error(CEC_EINVAL, "null id");
@@ -563,7 +582,7 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
       if (res != ncclSuccess) return fail(res, "ncclGroupEnd");
     }
     if (!mine.empty()) {
-      // every fragment not lost is flagged present (the codec reads the first k, the gathered
+      // every fragment not lost is flagged present (the codec reads its k survivors, the gathered
       // survivors): the rebuild writes only the lost fragments, not the unused survivors
       std::vector<uint8_t> present(mine.size() * n, 0);
       for (size_t i = 0; i < mine.size(); ++i)

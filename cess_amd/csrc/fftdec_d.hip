@@ -22,6 +22,7 @@
 // lane (position): Horner over the coefficient bits, the lane's eight 0 / ~0 bit masks read from
 // LDS (the plan carries them expanded; -DCEC_FDD_BFE makes them with v_bfe_i32 instead, 0.11 ms
 // slower at 32 erasures).
+#include <algorithm>
 #include <utility>
 
 #include "fft_core.h"
@@ -156,6 +157,7 @@ __device__ __forceinline__ void mul_rt(uint32_t (&x)[8], uint32_t cv) {
 // two 16-byte LDS reads instead of eight half-rate v_bfe_i32)
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef const __attribute__((address_space(3))) u32x4 lds_u32x4;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4w;
 __device__ __forceinline__ void mul_rt_lds(uint32_t (&x)[8], const lds_u32* mk) {
   const u32x4 lo = *reinterpret_cast<lds_u32x4*>(mk), hi = *reinterpret_cast<lds_u32x4*>(mk + 4);
   const uint32_t m[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -307,7 +309,7 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const u
   const cplan_t P = (cplan_t)Pg;
 #ifndef CEC_FDD_BFE
   // the plan's per-lane masks into LDS (4 KiB: 16 bytes per thread), before any wave leaves
-  static_assert(FftDecDLayout::kWords - FftDecDLayout::kMasks == 4 * 256 &&
+  static_assert(FftDecDLayout::kMerged - FftDecDLayout::kMasks == 4 * 256 &&
                     FftDecDLayout::kMasks % 4 == 0,
                 "one 16-byte piece of the mask table per thread of the 256-thread workgroup");
   __shared__ __attribute__((aligned(16))) uint32_t lmask[2 * 16 * 4 * 8];
@@ -368,11 +370,175 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const u
   });
 }
 
+// ---- the pipelined form (k_fftdec_dp) ----------------------------------------------------------
+// Every position needs exactly one run-time multiplication: lam(t) where it is read, 1 / lam'(t)
+// where it is an output. k_fftdec_d runs both per slot (a SIMD executes both sides of a lane-
+// dependent choice), ~2,700 of its ~9,300 VALU per wave. Here a wave walks a run of consecutive
+// 512-column blocks of one segment (one pattern): the output step of block u and the input step of
+// block u + 1 share one multiplication per slot, with the merged constant of each position (the
+// plan's kMerged masks: a position is never both read and an output). The operand is the next
+// block's loaded input on read lanes and this block's FFT output elsewhere; the product goes back to
+// the registers as the next block's input (zero on unread lanes) and to memory as this block's
+// output (stored by output lanes only). The grid is the chip's resident waves (persistent); wave w
+// takes units [w U / W, (w + 1) U / W) of the U = nseg x (len / 512) (segment, block) units, and
+// starts afresh (table, full input step) where its run crosses into the next segment.
+
+// wave-private LDS: the merged-constant masks of the wave's current segment (2 KiB)
+constexpr int kMergedWords = 16 * 4 * 8;
+
+// The lane's 32 bytes of shard slot J (positions 4J + l) at column offset `col` of the segment
+__device__ __forceinline__ void dp_load(__amdgpu_buffer_rsrc_t rD, __amdgpu_buffer_rsrc_t rP,
+                                        int J, uint32_t col, uint32_t ss, bool rd,
+                                        uint32_t (&w)[8]) {
+  bld(J < 8 ? rD : rP, rd ? col : kOff, (uint32_t)(4 * (J & 7)) * ss, w);
+}
+
+template <int J>
+__device__ __forceinline__ uint32_t dp_rdmask(cplan_t P, uint32_t sh) {
+  return ((P[FftDecDLayout::kLam + J] >> sh) & 0xFF) ? 0xFFFFFFFFu : 0u;
+}
+
+__global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
+    Layout L, const uint32_t* __restrict__ plan1, const uint32_t* const* __restrict__ plans,
+    const uint32_t* __restrict__ seg_list, uint32_t nblk, uint64_t units) {
+  __shared__ __attribute__((aligned(16))) uint32_t lmask_all[4][kMergedWords];
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+  const uint64_t nwave = (uint64_t)gridDim.x * 4;
+  const uint64_t wave = (uint64_t)blockIdx.x * 4 + wid;
+  const uint64_t u0 = wave * units / nwave, u1 = (wave + 1) * units / nwave;
+  if (u0 >= u1) return;
+  lds_u32* lmask = (lds_u32*)lmask_all[wid];
+  const uint32_t ss = (uint32_t)L.shard_stride;
+
+  uint32_t X[16][8];
+  // loop state kept scalar (32-bit, wave-uniform): (segment list index, block) of the unit,
+  // stepped along the run, the units left and whether the next one starts a segment afresh (no
+  // division or 64-bit compare inside the loop: that is VALU work with every X register live)
+  uint32_t y = __builtin_amdgcn_readfirstlane((uint32_t)(u0 / nblk));
+  uint32_t blk = __builtin_amdgcn_readfirstlane((uint32_t)(u0 % nblk));
+  uint32_t left = __builtin_amdgcn_readfirstlane((uint32_t)(u1 - u0));
+  uint32_t fresh = 1;
+  for (; left; --left) {
+    const uint32_t seg = seg_list ? seg_list[y] : y;
+    const uint32_t* Pg = plans ? plans[y] : plan1;
+    {  // wave-uniform: keep the pointer (and the choice above) scalar
+      const uint64_t pv = (uint64_t)Pg;
+      Pg = (const uint32_t*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pv >> 32)) << 32) |
+                             __builtin_amdgcn_readfirstlane((uint32_t)pv));
+    }
+    const cplan_t P = (cplan_t)Pg;
+    const auto rD = rsrc(L.data + seg * L.data_seg_stride);
+    const auto rP = rsrc(L.parity + seg * L.par_seg_stride);
+    const uint32_t wave_col = blk * 512;
+    if (fresh) {
+      // this segment's merged masks (32 bytes per lane), then the block's whole input step
+      {
+        uint32_t lane;  // opaque: derived here, not kept live through the loop
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+        // a buffer resource on the (uniform) plan: 32-bit lane offsets, no 64-bit VGPR addresses
+        const auto rT = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t*>(Pg + FftDecDLayout::kMerged), (short)0, kMergedWords * 4,
+            0x00020000);
+        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rT, 32 * lane, 0, 0);
+        const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rT, 32 * lane + 16, 0, 0);
+        // the previous segment's reads of the table are complete (in order within the wave)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        *reinterpret_cast<lds_u32x4w*>(lmask + 8 * lane) = a;
+        *reinterpret_cast<lds_u32x4w*>(lmask + 8 * lane + 4) = b;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      const LaneCtx c0 = lane_ctx(wave_col, ss);
+      sfor<16>([&](auto J) CEC_FFT_AI {
+        dp_load(rD, rP, J, c0.lcol, ss, (P[FftDecDLayout::kLam + J] >> c0.sh) & 0xFF, X[J]);
+      });
+      sfor<16>([&](auto J) CEC_FFT_AI {
+        after_prev<J>(X);
+        tr8(X[J]);
+        mul_rt_lds(X[J], lmask + (J * 4 + c0.l) * 8);  // unread lanes hold zeros
+      });
+      fresh = 0;
+    }
+    fence_all(X);
+    ifft64(X, lane_ctx(0, 0).e1, lane_ctx(0, 0).e2);
+    fence_all(X);
+    {
+      const LaneCtx c = lane_ctx(0, 0);
+      derivative(X, c.e1, c.e2);
+    }
+    fence_all(X);
+    fft64_upper(X);
+    fence_all(X);
+    // the next unit continues this segment: its input step rides on this block's output step.
+    // Branch-free per slot (uniform branches here cost registers across the unrolled slots):
+    // without a next block the loads are all out of range (no memory traffic) and rd = 0; lanes
+    // that are not outputs store out of range.
+    const uint32_t next = left > 1 && blk + 1 < nblk ? 1u : 0u;
+    const uint32_t nx = next ? 0xFFFFFFFFu : 0u;
+    const LaneCtx c1 = lane_ctx(wave_col, ss);
+    const uint32_t ncol = c1.lcol + 512;  // the same lane's columns in the next block
+    sfor<16>([&](auto J) CEC_FFT_AI {
+      const uint32_t dw = P[FftDecDLayout::kDinv + J];
+      after_prev<J>(X);
+      uint32_t pre[8];
+      uint32_t col = ncol;  // the load is issued in its slot, not hoisted into earlier slots
+      if constexpr (J > 0) asm volatile("" : "+v"(col) : "v"(X[J - 1][7]));
+      dp_load(rD, rP, J, col, ss, dp_rdmask<J>(P, c1.sh) & nx, pre);
+      fft64_tail<J>(X[J], c1.e1, c1.e2);
+      const uint32_t rd = dp_rdmask<J>(P, c1.sh) & nx;
+      tr8(pre);
+      sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] = FFT_BOP3(rd, pre[Q], X[J][Q], kSel); });
+      mul_rt_lds(X[J], lmask + (J * 4 + c1.l) * 8);
+      uint32_t O[8];
+      sfor<8>([&](auto Q) CEC_FFT_AI {
+        O[Q] = X[J][Q];
+        X[J][Q] &= rd;  // next input: zero where unread
+      });
+      tr8(O);
+      bst(J < 8 ? rD : rP, ((dw >> c1.sh) & 0xFF) ? c1.lcol : kOff, (uint32_t)(4 * (J & 7)) * ss, O);
+      // the next slot starts once this slot's stored planes exist (the scheduler would otherwise
+      // overlap two slots' temporaries)
+      if constexpr (J + 1 < 16)
+        asm volatile("" : "+v"(X[J + 1][0]), "+v"(X[J + 1][1]), "+v"(X[J + 1][2]), "+v"(X[J + 1][3])
+                     : "v"(O[3]), "v"(O[7]));
+    });
+    fresh = next ^ 1u;
+    if (++blk == nblk) {
+      blk = 0;
+      ++y;
+    }
+  }
+}
+
+// Resident workgroups of k_fftdec_dp on the device (the persistent grid), cached per device.
+uint32_t fdd_resident_wgs() {
+  static uint32_t cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
+  if (!cache[dev]) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_fftdec_dp, 256, 0) != hipSuccess ||
+        cus <= 0 || per <= 0)
+      return 1024;
+    cache[dev] = (uint32_t)(cus * per);
+  }
+  return cache[dev];
+}
+
 }  // namespace
 
 bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* const* plans,
-                     const uint32_t* seg_list, uint32_t nseg, hipStream_t st) {
+                     const uint32_t* seg_list, uint32_t nseg, hipStream_t st, bool pipelined) {
   if (!fftdec_layout_ok(L)) return false;
+  if (nseg == 0) return true;
+  if (pipelined) {
+    const uint32_t nblk = (uint32_t)(L.len / 512);
+    const uint64_t units = (uint64_t)nseg * nblk;
+    const uint64_t wgs = std::min<uint64_t>(fdd_resident_wgs(), (units + 3) / 4);
+    hipLaunchKernelGGL(k_fftdec_dp, dim3((unsigned)wgs), dim3(256), 0, st, L, plan1, plans,
+                       seg_list, nblk, units);
+    return true;
+  }
   const uint64_t gx = (L.len / 512 * 64 + 255) / 256;
   for (uint32_t s0 = 0; s0 < nseg; s0 += 65535) {
     const uint32_t ny = nseg - s0 < 65535 ? nseg - s0 : 65535;

@@ -76,6 +76,59 @@ inline uint8_t lagrange(unsigned base, unsigned c, unsigned x) {
 
 }  // namespace fdp
 
+// The survivors an RS(32,32) rebuild reads (the codec's survivor choice, cec_survivors): every
+// present shard of the coset A with fewer lost shards (data on a tie), and d = (lost in A) present
+// shards of the other coset B chosen for the syndrome-row decoder below: whole present lane-pair
+// slots (positions 2j, 2j + 1) first, then a lone present position whose slot holds a lost shard
+// (packed anyway), then any. Any k present shards rebuild the same bytes (MDS); this choice keeps
+// the syndrome rows in as few slots as the pattern allows (first-k-present costs 1.3-1.5x the
+// slots at 8-24 erasures). `read` gets 64 flags. False when more than 32 shards are lost.
+inline bool fftdec_read_set(const uint8_t* present, uint8_t* read) {
+  uint32_t lost_d = 0, lost_p = 0;
+  for (int t = 0; t < 32; ++t) {
+    if (!present[t]) lost_d |= 1u << t;
+    if (!present[32 + t]) lost_p |= 1u << t;
+  }
+  const int nd = fdp::popc(lost_d), np = fdp::popc(lost_p);
+  if (nd + np > 32) return false;
+  const int side = np < nd ? 1 : 0;
+  const uint32_t DA = side ? lost_p : lost_d, EB = side ? lost_d : lost_p;
+  const unsigned baseA = side ? 32u : 0u, baseB = side ? 0u : 32u;
+  uint32_t R = 0;
+  int need = fdp::popc(DA);
+  for (int j = 0; j < 16 && need >= 2; ++j)
+    if (!(EB >> (2 * j) & 3)) {
+      R |= 3u << (2 * j);
+      need -= 2;
+    }
+  for (int pass = 0; pass < 2 && need > 0; ++pass)
+    for (int t = 0; t < 32 && need > 0; ++t) {
+      if ((EB >> t & 1) || (R >> t & 1)) continue;
+      const bool packed = (EB >> (t ^ 1) & 1) || (R >> (t ^ 1) & 1);
+      if (pass == 0 && !packed) continue;
+      R |= 1u << t;
+      --need;
+    }
+  for (int t = 0; t < 32; ++t) {
+    read[baseA + t] = !(DA >> t & 1);
+    read[baseB + t] = (R >> t & 1) ? 1 : 0;
+  }
+  return true;
+}
+
+// The survivors a rebuild of `present` reads (the C ABI's cec_survivors; k + m flags into
+// `read`): for RS(32,32) fftdec_read_set's choice, otherwise the first k present shards
+// (klauspost's). False when fewer than k shards are present.
+inline bool survivor_set(int k, int m, const uint8_t* present, uint8_t* read) {
+  if (k == 32 && m == 32) return fftdec_read_set(present, read);
+  int got = 0;
+  for (int i = 0; i < k + m; ++i) {
+    read[i] = present[i] && got < k;
+    got += read[i];
+  }
+  return got == k;
+}
+
 // Build the mode-M plan for RS(32,32) erasure pattern `present` (64 flags, shards 0..31 data,
 // 32..63 parity) that reads only the shards flagged in `read` (a subset of the present ones: the
 // codec's contract is that a rebuild reads the first k present shards, the survivors a caller
@@ -234,7 +287,11 @@ struct FftDecDLayout {
   // the same constants as bit masks, one word per (slot j, lane l, bit b): 0 or ~0 = bit b of the
   // constant of position 4j + l (the kernel's per-lane Horner masks, copied to LDS)
   static constexpr int kMasks = 48;  // [2][16][4][8]: lam, then 1 / lam'
-  static constexpr int kWords = kMasks + 2 * 16 * 4 * 8;
+  // the merged constant of each position, as the same masks: lam(t) where t is read, 1 / lam'(t)
+  // where it is an output, 0 elsewhere (a position is never both): the pipelined kernel multiplies
+  // the next column block's inputs and this block's outputs in one pass
+  static constexpr int kMerged = kMasks + 2 * 16 * 4 * 8;  // [16][4][8]
+  static constexpr int kWords = kMerged + 16 * 4 * 8;
 };
 
 // Build the mode-D plan for RS(32,32) pattern `present` (64 flags) reading only the shards flagged
@@ -269,10 +326,12 @@ inline bool fftdec_plan_d(const uint8_t* read, const uint8_t* present, bool data
   }
   if (!nout) return false;
   w[FftDecDLayout::kNout] = (uint32_t)nout;
-  for (int which = 0; which < 2; ++which)
+  for (int which = 0; which < 3; ++which)
     for (int t = 0; t < 64; ++t) {
-      const uint8_t c = (uint8_t)(w[(which ? FftDecDLayout::kDinv : FftDecDLayout::kLam) + (t >> 2)] >>
-                                  (8 * (t & 3)));
+      auto byte = [&](int base) { return (uint8_t)(w[base + (t >> 2)] >> (8 * (t & 3))); };
+      const uint8_t c = which == 0 ? byte(FftDecDLayout::kLam)
+                        : which == 1 ? byte(FftDecDLayout::kDinv)
+                                     : (uint8_t)(byte(FftDecDLayout::kLam) | byte(FftDecDLayout::kDinv));
       for (int b = 0; b < 8; ++b)
         w[FftDecDLayout::kMasks + ((which * 16 + (t >> 2)) * 4 + (t & 3)) * 8 + b] =
             (c >> b & 1) ? 0xFFFFFFFFu : 0u;

@@ -172,24 +172,33 @@ constexpr int gf_decode_plan(int k, int m, const uint8_t* present, bool data_onl
   return 0;
 }
 
-// The same plan by the code's systematic structure (run time): the first k present shards are
-// the k - d present data shards and the first d present parity shards Ps, so only the d x d block
-// A = E[Ps][D] over the missing data D is inverted: x_D = inv(A) (y_Ps ^ E[Ps][C] x_C). d^3 + d^2 k
-// products instead of the k x 2k Gauss-Jordan; the decode map is unique, so the coefficients are
-// those of gf_decode_plan (checked on every pattern of small codes, tests/native/sanitize_host.cpp).
-// `a`, `ainv`, `work` are scratch (d <= m). Returns 0, or -1 if fewer than k shards survive.
+// The same plan by the code's systematic structure (run time): the survivors (the first k present
+// shards, or the k shards flagged in `read`, a subset of the present ones) are k - d data shards
+// and d parity shards Ps, so only the d x d block A = E[Ps][D] over the unread data D is inverted:
+// x_D = inv(A) (y_Ps ^ E[Ps][C] x_C) (any d parity rows give an invertible block: the code is
+// MDS). d^3 + d^2 k products instead of the k x 2k Gauss-Jordan; the decode map from a survivor
+// set is unique, so the coefficients are those of gf_decode_plan (checked on every pattern of
+// small codes, tests/native/sanitize_host.cpp). Outputs are the shards not present (data_only:
+// data shards only). `a`, `ainv`, `work` are scratch (d <= m). Returns 0, or -1 if fewer than k
+// shards survive (or `read` does not name k present shards).
 template <int R, int C, int R2, int C2>
 int gf_decode_plan_sys(int k, int m, const uint8_t* present, bool data_only, const Mat<R, C>& e,
-                       Plan<R, C>& plan, Mat<R, C>& a, Mat<R, C>& ainv, Mat<R2, C2>& work) {
+                       Plan<R, C>& plan, Mat<R, C>& a, Mat<R, C>& ainv, Mat<R2, C2>& work,
+                       const uint8_t* read = nullptr) {
   const int n = k + m;
   plan.k = k;
   int got = 0;
+  bool in[kMaxShards] = {};
   for (int i = 0; i < n && got < k; ++i)
-    if (present[i]) plan.in_idx[got++] = (uint8_t)i;
+    if (read ? read[i] : present[i]) {
+      if (!present[i]) return -1;
+      plan.in_idx[got++] = (uint8_t)i;
+      in[i] = true;
+    }
   if (got < k) return -1;
-  int miss[kMaxShards], d = 0;  // missing data shards
+  int miss[kMaxShards], d = 0;  // data shards not read (the lost ones and, with `read`, others)
   for (int i = 0; i < k; ++i)
-    if (!present[i]) miss[d++] = i;
+    if (!in[i]) miss[d++] = i;
   const int nc = k - d;  // survivor positions [0, nc) are data, [nc, k) parity
   a.rows = a.cols = d;
   for (int r = 0; r < d; ++r)
@@ -260,6 +269,40 @@ constexpr LchSkews<K> lch_skews(uint8_t beta) {
       r.s[i][b] = lch_what(i, (uint8_t)((b << (i + 1)) ^ beta));
   return r;
 }
+// The same transforms over the 2^K points of span(v_0..v_{K-1}) for any ordered basis v (the
+// shard indices 0..63 as points, taken in another order: position p holds the point
+// phi(p) = XOR of v_i over the bits i of p). What_i is GF(2)-linear, so a skew is the XOR of
+// What_i(v_j) over the bits of its block above layer i.
+constexpr uint8_t lchb_phi(const uint8_t* v, int K, unsigned p) {
+  uint8_t x = 0;
+  for (int i = 0; i < K; ++i)
+    if (p >> i & 1) x ^= v[i];
+  return x;
+}
+constexpr uint8_t lchb_w(const uint8_t* v, int i, uint8_t x) {
+  uint8_t r = 1;
+  for (unsigned a = 0; a < (1u << i); ++a) r = gf_mul(r, (uint8_t)(x ^ lchb_phi(v, i, a)));
+  return r;
+}
+constexpr uint8_t lchb_what(const uint8_t* v, int i, uint8_t x) {
+  return gf_mul(lchb_w(v, i, x), gf_inv(lchb_w(v, i, v[i])));
+}
+template <int K>
+constexpr LchSkews<K> lchb_skews(const uint8_t* v) {
+  LchSkews<K> r{};
+  for (int i = 0; i < K; ++i)
+    for (int b = 0; b < (1 << (K - 1 - i)); ++b)
+      r.s[i][b] = lchb_what(v, i, lchb_phi(v, K, (unsigned)b << (i + 1)));
+  return r;
+}
+// the formal derivative's constants in that basis: c_j = W_j'(0) / W_j(v_j), W_j'(0) the product
+// of the nonzero points of span(v_0..v_{j-1})
+constexpr uint8_t lchb_dconst(const uint8_t* v, int j) {
+  uint8_t p = 1;
+  for (unsigned a = 1; a < (1u << j); ++a) p = gf_mul(p, lchb_phi(v, j, a));
+  return gf_mul(p, gf_inv(lchb_w(v, j, v[j])));
+}
+
 // Formal derivative in the novel basis: D(Xhat_i) = sum_{bit j of i} c_j Xhat_{i - 2^j} with
 // c_j = What_j' = W_j'(0) / W_j(v_j). W_j is linearised, so its derivative is the constant
 // prod of the nonzero points of span(v_0..v_{j-1}).

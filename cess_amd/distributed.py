@@ -63,7 +63,7 @@ class GatherPlan:
     # (segment, survivor fragment) -> (source rank, destination rank)
     moves: Dict[Tuple[int, int], Tuple[int, int]]
     # segment -> present flags (k+m) the decoder passes: every fragment not erased. The codec
-    # reads only the first k of them (`survivors`), so only those are moved; flagging the unused
+    # reads only its k survivors of them (`survivors`), so only those are moved; flagging the unused
     # ones present keeps the rebuild to the lost fragments alone (e outputs, not n - k)
     present: Dict[int, np.ndarray]
     # segment -> erased fragment indices
@@ -75,11 +75,23 @@ class GatherPlan:
     # segment -> decoding rank
     decoder: Dict[int, int] = field(default_factory=dict)
     world: int = 1
-    # segment -> the survivors the rebuild reads (first k present, index order)
+    # segment -> the survivors the rebuild reads (cec_survivors: index order)
     survivors: Dict[int, List[int]] = field(default_factory=dict)
 
 
 EXCHANGES = ("survivors", "partials", "auto")
+
+
+def survivors_of(k: int, m: int, present) -> List[int]:
+    """The k survivors a rebuild of pattern `present` reads (cec_survivors, host only): the
+    first k present fragments, or for RS(32,32) the set the FFT-domain decoders prefer. The
+    gather moves exactly these."""
+    from . import _lib
+    from .reedsolomon import check
+    flags = (ctypes.c_uint8 * (k + m))(*[1 if p else 0 for p in present])
+    out = (ctypes.c_uint8 * k)()
+    check(_lib.load().cec_survivors(k, m, flags, out), "cec_survivors")
+    return list(out)
 
 
 def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
@@ -87,7 +99,8 @@ def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
     """Plan the degraded read of `lost` = {segment: erased fragment indices}.
 
     The decoder of a segment is the home GPU of its first lost fragment (repair restores the
-    fragment where it lives). Survivors = the first k present fragments in index order (the
+    fragment where it lives). Survivors = the k fragments the codec reads (`survivors`: the
+    first k present, or for RS(32,32) the FFT-domain decoders' choice; cec_survivors) (the
     codec's survivor choice), so exactly k fragments per segment are read. `exchange`:
     "survivors" moves the survivors the decoder lacks; "partials" moves one partial rebuild per
     lost fragment from every other GPU holding survivors; "auto" takes, per segment, whichever
@@ -114,7 +127,7 @@ def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
         dec = fragment_owner(s, min(erased), world)
         segs.setdefault(dec, []).append(s)
         decoder[s] = dec
-        surv = [f for f in range(n) if f not in erased][:k]
+        surv = survivors_of(k, m, [f not in erased for f in range(n)])
         survivors[s] = surv
         flags = np.ones(n, np.uint8)
         flags[sorted(erased)] = 0
@@ -168,7 +181,7 @@ def gather_survivors(plan: GatherPlan, store: FragmentStore, k: int, m: int, ran
     staging_parity [nseg_d][m][F], present [nseg_d][k+m], segment list) on the decoding rank;
     the staging tensors hold every used survivor at its shard index; the other slots are left
     uninitialised (the lost ones are written by the rebuild, the unused survivors are flagged
-    present but never read: the codec reads the first k present).
+    present but never read: the codec reads exactly its survivors).
     Non-decoding ranks only send and return None for the staging tensors."""
     import torch
     import torch.distributed as dist

@@ -69,9 +69,16 @@ int cec_matrix(const cec_codec* codec, uint8_t* out);
  * The data is staged through HBM; calls are synchronous. */
 int cec_encode(cec_codec* codec, uint8_t* const* shards, size_t shard_len);
 /* present[i] != 0: shard i is valid. Missing shards are written in place; with data_only only
- * missing data shards are produced (ReconstructData). All present: no-op. */
+ * missing data shards are produced (ReconstructData). All present: no-op. Every rebuild (here and
+ * in the batch calls) reads exactly the k survivors cec_survivors names, nothing else flagged
+ * present: the first k present shards (klauspost's choice), or for RS(32,32) the set the
+ * FFT-domain decoders rebuild from most cheaply. Any k survivors give the same bytes. */
 int cec_reconstruct(cec_codec* codec, uint8_t* const* shards, const uint8_t* present,
                     size_t shard_len, int data_only);
+/* Host only: the k survivors (ascending shard indices) a rebuild of the pattern `present`
+ * (k + m flags) reads. A caller that moves survivors to the decoder (a multi-GPU gather, a
+ * repair service fetching from peers) moves these. CEC_ETOOFEW below k present. */
+int cec_survivors(int k, int m, const uint8_t* present, uint8_t* survivors);
 /* *ok = 1 when every parity shard equals the encode of the data shards. */
 int cec_verify(cec_codec* codec, uint8_t* const* shards, size_t shard_len, int* ok);
 
@@ -89,7 +96,7 @@ int cec_reconstruct_batch(cec_codec* codec, uint8_t* d_data, uint8_t* d_parity, 
                           int data_only, void* hip_stream);
 /* Partial rebuild (the partial-product exchange of a multi-GPU degraded read):
  * like cec_reconstruct_batch with per-segment patterns (present: nseg*(k+m) flags; survivors =
- * the first k present shards of each segment), but every missing shard receives only the
+ * cec_survivors of each segment's pattern), but every missing shard receives only the
  * contribution of the survivors flagged in `held` (nseg*(k+m) flags; flags of non-survivors are
  * ignored): out = XOR over held survivors i of D[out][i] * shard_i. Only held survivors are read.
  * The rebuild is linear, so XOR-ing the partials of a partition of the survivors (one per GPU
@@ -240,7 +247,7 @@ int cec_audit_chunks(cec_codec* codec, const uint8_t* d_data, const uint8_t* d_p
  * One process (or thread) per GPU, each with its own codec. Fragment f of segment s is stored on
  * rank (s + f) mod world, the GPU analogue of the chain's miner placement (random_assign_miner,
  * c-pallets/file-bank/src/functions.rs:187-283: a segment's fragments on distinct miners). A
- * degraded read brings the first k surviving fragments of every segment with lost fragments to
+ * degraded read brings the k survivors (cec_survivors) of every segment with lost fragments to
  * the rank that owns the segment's first lost fragment (repair restores a fragment where it
  * lives, restoral_order_complete, c-pallets/file-bank/src/lib.rs:1075-1122) by RCCL point-to-
  * point over xGMI, and rebuilds the lost fragments there. RCCL is loaded at run time; without it

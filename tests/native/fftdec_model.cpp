@@ -78,6 +78,18 @@ static int check_d(const uint8_t* read, const uint8_t* present, bool data_only, 
     if ((lam != 0) != (read[t] != 0)) ++fails;  // only the read shards are loaded
     v[t] = gf_mul(lam, cw[t]);
   }
+  // the pipelined kernel's merged constants: lam where read, 1 / lam' where an output, never both
+  for (int t = 0; t < 64; ++t) {
+    const uint8_t lam = byte(FftDecDLayout::kLam, t), di = byte(FftDecDLayout::kDinv, t);
+    if (lam && di) ++fails;
+    uint8_t merged = 0;
+    for (int b = 0; b < 8; ++b) {
+      const uint32_t mk = w[FftDecDLayout::kMerged + ((t >> 2) * 4 + (t & 3)) * 8 + b];
+      if (mk != 0 && mk != 0xFFFFFFFFu) ++fails;
+      merged |= (uint8_t)((mk & 1) << b);
+    }
+    if (merged != (lam | di)) ++fails;
+  }
   ifft64(v);
   for (int i = 0; i < 64; ++i)
     for (int j = 0; j < 6; ++j)

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../cess_amd/csrc/gf256.h"
+#include "../../cess_amd/csrc/fftdec_plan.h"
 #include "../../include/cess_ec.h"
 
 extern "C" {
@@ -191,6 +192,30 @@ static void same_plans(int k, int m, const uint8_t* present, bool data_only, con
   }
 }
 
+// the systematic plan from an explicit survivor set (`read`, k present shards): every output row
+// times the survivors' encode rows is the output's encode row, outputs = the shards not present
+static void read_set_plan(int k, int m, const uint8_t* present, const uint8_t* read,
+                          bool data_only, const Big& E) {
+  auto p = std::make_unique<BigPlan>();
+  auto a = std::make_unique<Big>();
+  auto ai = std::make_unique<Big>();
+  auto w = std::make_unique<Work>();
+  CHECK(cec::gf_decode_plan_sys(k, m, present, data_only, E, *p, *a, *ai, *w, read) == 0);
+  for (int j = 0, i = 0; i < k + m; ++i)
+    if (read[i]) CHECK(p->in_idx[j++] == i);
+  int want = 0;
+  for (int i = 0; i < k + m; ++i) want += !present[i] && (!data_only || i < k);
+  CHECK(p->nout == want);
+  for (int o = 0; o < p->nout; ++o) {
+    CHECK(!present[p->out_idx[o]]);
+    for (int c = 0; c < k; ++c) {
+      uint8_t acc = 0;
+      for (int j = 0; j < k; ++j) acc ^= cec::gf_mul(p->coef.v[o][j], E.v[p->in_idx[j]][c]);
+      CHECK(acc == E.v[p->out_idx[o]][c]);
+    }
+  }
+}
+
 static void matrices() {
   const int codes[][2] = {{2, 1}, {4, 2}, {5, 5}, {10, 4}, {3, 3}};
   for (auto& km : codes) {
@@ -237,6 +262,22 @@ static void matrices() {
       const int e = 1 + (int)(g() % m);
       for (int q = 0; q < e; ++q) present[g() % n] = 0;
       same_plans(k, m, present, t & 1, *E);
+      // survivor sets other than the first k present: random ones, and RS(32,32)'s choice
+      uint8_t read[cec::kMaxShards] = {};
+      int idx[cec::kMaxShards], np = 0;
+      for (int i = 0; i < n; ++i)
+        if (present[i]) idx[np++] = i;
+      for (int i = np - 1; i > 0; --i) std::swap(idx[i], idx[g() % (i + 1)]);
+      for (int i = 0; i < k; ++i) read[idx[i]] = 1;
+      read_set_plan(k, m, present, read, t & 1, *E);
+      if (k == 32 && m == 32) {
+        uint8_t fr[64] = {};
+        CHECK(cec::fftdec_read_set(present, fr));
+        int nr = 0;
+        for (int i = 0; i < 64; ++i) nr += fr[i];
+        CHECK(nr == 32);
+        read_set_plan(k, m, present, fr, t & 1, *E);
+      }
     }
   }
 }

@@ -114,9 +114,10 @@ def test_plan_exchange_choice():
     assert not surv.partial and set(auto.partial) == set(lost) and not auto.moves
     assert all(len(h) == G - 1 for h in auto.partial.values())
     assert auto.bytes_moved == 16 * (G - 1) * F
-    # 27-28 survivors of 32 live off the decoder
+    # 27-28 of the 32 survivors (the codec's choice, cec_survivors) live off the decoder
     want = sum(sum((s + f) % G != (2 * s) % G  # decoder: the lost fragment's home
-                   for f in [f for f in range(64) if f != s % 64][:32]) for s in range(16))
+                   for f in D.survivors_of(k, m, [f != s % 64 for f in range(64)]))
+               for s in range(16))
     assert surv.bytes_moved == want * F and want >= 16 * 27
     # RS(2,1) spread over >= 3 GPUs: 2 survivors vs 2 partials, a tie -> survivors
     l21 = {s: [s % 3] for s in range(30)}
@@ -144,10 +145,16 @@ class _OracleEnc:
         k = self.DataShards
         return [sd[i, f] if f < k else sp[i, f - k] for f in range(k + self.ParityShards)]
 
+    def _survivors(self, present):
+        # the codec's survivor choice (cec_survivors): the only shards the product reads
+        k, m = self.DataShards, self.ParityShards
+        return set(D.survivors_of(k, m, [bool(p) for p in present]))
+
     def ReconstructBatch(self, sd, sp, nseg, F, present, stream=None):
         for i in range(nseg):
             v = self._views(sd, sp, i)
-            rec = self.rs.reconstruct([v[f].numpy().copy() if present[i][f] else None
+            surv = self._survivors(present[i])
+            rec = self.rs.reconstruct([v[f].numpy().copy() if f in surv else None
                                        for f in range(len(v))])
             for f in range(len(v)):
                 if not present[i][f]:
@@ -156,13 +163,15 @@ class _OracleEnc:
     def ReconstructPartialBatch(self, sd, sp, nseg, F, present, held, stream=None):
         for i in range(nseg):
             v = self._views(sd, sp, i)
-            surv, outs, rows = self.rs.decode_plan(present[i])
+            sv = self._survivors(present[i])
+            surv, outs, rows = self.rs.decode_plan([f in sv for f in range(len(v))])
             cols = [j for j, f in enumerate(surv) if held[i][f]]
             vals = (self.o.code_rows([[r[j] for j in cols] for r in rows],
                                      [v[surv[j]].numpy() for j in cols])
                     if cols else [np.zeros(F, np.uint8) for _ in outs])
             for o_, val in zip(outs, vals):
-                v[o_].copy_(torch.from_numpy(np.asarray(val, np.uint8)))
+                if not present[i][o_]:
+                    v[o_].copy_(torch.from_numpy(np.asarray(val, np.uint8)))
 
 
 def _xor_cpu(dst, src, nsrc, stride, length):
@@ -252,3 +261,34 @@ def test_c_plan_matches_python_plan(k, m):
         D.c_plan({3: [n]}, k, m, 2)  # index outside 0..n-1
     with pytest.raises(ErrTooFewShards):
         D.c_plan({3: list(range(m + 1))}, k, m, 2)
+
+
+def test_survivor_choice():
+    """cec_survivors: k present shards; klauspost's first k present for every code but
+    RS(32,32), whose rebuilds read every present shard of the coset with fewer losses plus as
+    many of the other coset as that lost, packed into whole lane-pair slots (2j, 2j + 1) where
+    the pattern allows (the syndrome-row decoder's rows then fill the fewest slots)."""
+    rng = np.random.default_rng(3)
+    for k, m in ((2, 1), (4, 2), (10, 4), (17, 3)):
+        for _ in range(20):
+            pres = np.ones(k + m, bool)
+            pres[rng.choice(k + m, size=int(rng.integers(0, m + 1)), replace=False)] = False
+            assert D.survivors_of(k, m, pres) == [f for f in range(k + m) if pres[f]][:k]
+    for e in range(0, 33):
+        for _ in range(10):
+            pres = np.ones(64, bool)
+            pres[rng.choice(64, size=e, replace=False)] = False
+            sv = D.survivors_of(32, 32, pres)
+            assert len(sv) == 32 == len(set(sv)) and all(pres[f] for f in sv)
+            nd, np_ = (~pres[:32]).sum(), (~pres[32:]).sum()
+            a, b = (range(32, 64), range(32)) if np_ < nd else (range(32), range(32, 64))
+            assert all(f in sv for f in a if pres[f])  # all of coset A that survived
+            rb = [f - b[0] for f in sv if f in b]
+            assert len(rb) == 32 - sum(pres[f] for f in a)
+            # whole present slots are used before split ones
+            whole = sum(1 for j in range(16) if pres[b[0] + 2 * j] and pres[b[0] + 2 * j + 1])
+            used_whole = sum(1 for j in range(16) if 2 * j in rb and 2 * j + 1 in rb)
+            assert used_whole == min(whole, len(rb) // 2)
+    import cess_amd
+    with pytest.raises(cess_amd.CecError):
+        D.survivors_of(4, 2, [True, True, True, False, False, False])

@@ -177,6 +177,7 @@ pub mod sys {
         pub fn cec_audit_random_subject(pallet_id: *const u8, seed: u32, out12: *mut u8)
                                         -> c_int;
         pub fn cec_audit_random_u64(randomness: *const u8, len: usize, out: *mut u64) -> c_int;
+        pub fn cec_survivors(k: c_int, m: c_int, present: *const u8, survivors: *mut u8) -> c_int;
         pub fn cec_challenge_random_list(randomness: *const u8, nrand: usize, need: u32,
                                          out: *mut u8, used: *mut usize) -> c_int;
         pub fn cec_fill_synthetic(d_out: *mut u8, seg_bytes: usize, nseg: usize, seg0: u64,
