@@ -159,6 +159,7 @@ CEC_DIST_ID_BYTES = 128
 CEC_DIST_SURVIVOR = 0
 CEC_DIST_PARTIAL = 1
 CEC_DIST_OPT_EXCHANGE = 1
+CEC_DIST_OPT_TEST_ABORT = 2
 
 _libs = {}
 

@@ -690,9 +690,16 @@ enum FdKind { kFdNone = 0, kFdM = 1, kFdD = 2 };
 // tuning build: CEC_OPT_CT_VARIANT of this value runs the one-block-per-wave k_fftdec_d instead of
 // the pipelined k_fftdec_dp (A/B sweeps)
 constexpr int kCtVariantFddBlock = 70;
+double fdm_cost(int nout, int nrs) {
+  return 280.0 + (cec::fftdec_big(nrs) ? 3.8 : 3.3) * nout * nrs;
+}
+// A batch split between the two decoders runs one launch more; its ramp and tail cost about this
+// much beyond the per-segment costs (24 random erasures: 0.812 ms split 8/92 against 0.798 all on
+// the derivative decoder, profiles/r03/fdd_crossover_e18_28.jsonl).
+constexpr double kSplitLaunchUs = 20.0;
 int fftdec_choice(int nout, int nrs, bool has_m, bool has_d) {
   const double alt = nout <= 4 ? 130.0 + 57.0 * nout : 235.0 + 33.9 * nout;
-  const double m = has_m ? 280.0 + (cec::fftdec_big(nrs) ? 3.8 : 3.3) * nout * nrs : 1e30;
+  const double m = has_m ? fdm_cost(nout, nrs) : 1e30;
   const double d = has_d ? fdd_cost(nout) : 1e30;
   // the syndrome-row decoder only with a 15 % margin over the derivative: a batch split between
   // the two runs two smaller launches (24 random erasures: 0.854 ms split 34/66 by the bare
@@ -762,7 +769,8 @@ Layout stage_layout(cec_codec* c, size_t len) {
 // partial: pkey holds 2n flags per segment (present, then held) and the programs are partial
 // (cec_reconstruct_partial_batch).
 int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_only,
-                  std::unique_ptr<PsPlan>* out, bool partial = false, bool fdok = false) {
+                  std::unique_ptr<PsPlan>* out, bool partial = false, bool fdok = false,
+                  size_t shard_len = 0) {
   const int n = c->k + c->m;
   const int per = partial ? 2 * n : n;
   auto plan = std::make_unique<PsPlan>();
@@ -817,6 +825,30 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
     }
     progs.push_back({p, &g.second});
     if (p->single < 0 || !cec::has_decode_ct(c->k, c->m, p->single)) all_ct = false;
+  }
+  // The cost model picks per pattern; a batch whose patterns land on both decoders runs one more
+  // launch than all-derivative. Fold the syndrome-row groups into the derivative launch when the
+  // whole batch is cheaper that way (costs per segment scaled from 64 x 512 KiB).
+  if (!fdg[4].empty() && c->fftdec_mode == 0) {
+    const double scale = (double)shard_len / (512.0 * 1024.0) / 64.0;
+    double delta = 0;  // all-derivative minus split
+    int mlaunches = 0;
+    bool movable = true;
+    for (int cls = 0; cls < 4; ++cls) {
+      if (fdg[cls].empty()) continue;
+      ++mlaunches;
+      for (auto& pr : fdg[cls]) {
+        const Program& q = *pr.first;
+        movable &= q.fdd != nullptr;
+        delta += pr.second->size() * scale * (fdd_cost(q.nout) - fdm_cost(q.nout, q.fd_nrs));
+      }
+    }
+    if (mlaunches && movable && delta < kSplitLaunchUs * mlaunches) {
+      for (int cls = 0; cls < 4; ++cls) {
+        for (auto& pr : fdg[cls]) fdg[4].push_back(pr);
+        fdg[cls].clear();
+      }
+    }
   }
   std::vector<uint32_t> hl;
   std::vector<const uint32_t*> hp;
@@ -1137,9 +1169,10 @@ int cec_reconstruct_batch(cec_codec* c, uint8_t* d_data, uint8_t* d_parity, size
     pkey.push_back(fdok ? 1 : 0);
     pkey.push_back((char)c->fftdec_min);
     pkey.push_back((char)c->fftdec_mode);
+    for (int b = 0; b < 8; ++b) pkey.push_back((char)(shard_len >> (8 * b)));  // the split rule
     if (!c->ps || c->ps->key != pkey) {
       std::unique_ptr<PsPlan> plan;
-      rc = build_ps_plan(c, pkey, nseg, data_only != 0, &plan, false, fdok);
+      rc = build_ps_plan(c, pkey, nseg, data_only != 0, &plan, false, fdok, shard_len);
       if (rc) return rc;
       c->drop_plan();  // the old plan's arrays are retired: launches already enqueued keep them
       c->ps = std::move(plan);

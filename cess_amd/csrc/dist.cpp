@@ -12,8 +12,12 @@
 // send/recv; every rank issues the moves in the same (segment, fragment) order, which is what
 // pairs each send with its receive. Before any byte moves, the ranks agree (one 4-byte min
 // all-reduce) that every rank found its local survivors and holds staging for the largest
-// round, and again before every round's transfers that each finished its local steps, so a
-// local error fails on all ranks instead of leaving the others waiting in a receive.
+// round, so a caller error fails on all ranks instead of leaving the others waiting in a receive.
+// After that no rank leaves early: a local failure (a copy or rebuild that could not be enqueued)
+// skips that rank's remaining local work but it still takes part in every round's transfers (its
+// sources and staging are valid), and reports the error once all are enqueued. So the rounds are
+// enqueued back to back with no host synchronisation between them: a round's transfers overlap
+// the previous round's rebuild on the stream.
 //
 // RCCL is loaded at run time (dlopen): the rest of libcessec does not depend on it, and without
 // it the cec_dist_* entry points return CEC_ENCCL.
@@ -172,6 +176,7 @@ struct cec_dist {
   size_t pstage_bytes = 0;
   int* d_flag = nullptr;
   bool broken = false;  // the communicator was aborted after a failure inside a transfer group
+  int test_abort_round = -1;  // CEC_DIST_OPT_TEST_ABORT: fail inside this round's transfer group
   // Device memory is stream-ordered (hipMallocAsync / hipFreeAsync): hipFree performs an implicit
   // hipDeviceSynchronize, which would stall every other codec on the device. `done` is recorded on
   // the caller's stream at the end of every degraded read (its last enqueued work); destruction
@@ -287,6 +292,10 @@ int cec_dist_set_option(cec_dist* d, int option, int value) {
   if (option == CEC_DIST_OPT_EXCHANGE) {
     if (value < 0 || value > 2) return cec::set_error(CEC_EINVAL, "exchange must be 0, 1 or 2");
     d->exchange = value;
+    return CEC_OK;
+  }
+  if (option == CEC_DIST_OPT_TEST_ABORT) {
+    d->test_abort_round = value < 0 ? -1 : value;
     return CEC_OK;
   }
   return cec::set_error(CEC_EINVAL, "unknown dist option");
@@ -454,9 +463,10 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
     return cec::set_error(CEC_EINVAL, "dist degraded read: another rank failed its checks");
 
   // A local failure after the agreement (a copy, the partial rebuild, the rebuild after a round)
-  // is held in `lrc` and the rank skips its remaining local work; the ranks agree again before
-  // every round's transfers, so all of them stop there together. An error inside a transfer group
-  // aborts the communicator (peers get an RCCL error instead of waiting for this rank).
+  // is held in `lrc`: the rank skips its remaining local work but keeps issuing every round's
+  // transfers, so no peer waits for it, and returns the error at the end. An error inside a
+  // transfer group aborts the communicator (peers get an RCCL error instead of waiting for this
+  // rank).
   int lrc = CEC_OK;
   std::string lwhy;
   auto local = [&](int code) {
@@ -527,25 +537,23 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
       for (const Seg* g : pmine) ragged |= g->decoder == rank && g->holders.size() < H;
       if (ragged && !lrc) hip_ok(hipMemsetAsync(acc + acc_row, 0, H * acc_row, st), "memset");
     }
-    // every rank reached this round's transfers with its local work in place
-    rc = agree(lrc == CEC_OK, &all_ok);
-    if (rc) return rc;
-    if (lrc) return cec::set_error(lrc, "dist degraded read: " + lwhy);
-    if (!all_ok)
-      return cec::set_error(CEC_EINVAL, "dist degraded read: another rank failed a local step");
     // one group: survivor moves, then partials, each in plan order (pairs every send with its
     // receive on the peer)
     NC_TRY(r.group_start());
     size_t rj = 0;
     auto fail = [&](ncclResult_t res, const char* what) {
-      // a half-built group cannot be ended safely: abort the communicator so the peers' pending
-      // transfers fail instead of waiting for this rank
+      // end the half-built group (this thread's group state is then clean; what was enqueued is
+      // launched), then abort the communicator so those transfers and the peers' pending ones
+      // fail instead of waiting for the ones this rank never issued
       const int code = nccl_err(res, what);
+      (void)r.group_end();
       if (r.comm_abort) r.comm_abort(d->comm);
       d->comm = nullptr;
       d->broken = true;
       return code;
     };
+    if (d->test_abort_round == (int)(r0 / kRound))
+      return fail(ncclInternalError, "test abort (CEC_DIST_OPT_TEST_ABORT)");
     for (size_t i = r0; i < r1; ++i) {
       const Seg& g = plan[i];
       for (int f : g.surv) {

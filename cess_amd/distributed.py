@@ -353,6 +353,14 @@ class RcclGroup:
         check(self._lib.cec_dist_set_option(self._h, _lib.CEC_DIST_OPT_EXCHANGE,
                                             EXCHANGES.index(exchange)), "cec_dist_set_option")
 
+    def set_test_abort(self, round_index: int) -> None:
+        """Test hook (CEC_DIST_OPT_TEST_ABORT): fail inside round `round_index`'s transfer group
+        as an RCCL error there would (the group is aborted); -1 turns it off."""
+        from . import _lib
+        from .reedsolomon import check
+        check(self._lib.cec_dist_set_option(self._h, _lib.CEC_DIST_OPT_TEST_ABORT, round_index),
+              "cec_dist_set_option")
+
     def close(self) -> None:
         if self._h:
             self._lib.cec_dist_destroy(self._h)

@@ -279,6 +279,10 @@ typedef struct cec_dist_move {
  * a wide code spread over many GPUs with few erasures: RS(32,32) on 8 GPUs, one lost fragment,
  * 7 partials instead of 27-28 survivors). */
 #define CEC_DIST_OPT_EXCHANGE 1
+/* Test hook: value r >= 0 makes the next degraded reads fail inside round r's transfer group, as
+ * an RCCL error there would (the group is ended and the communicator aborted, so peers get an
+ * error instead of waiting; later calls on the handle return CEC_ENCCL). -1 = off (default). */
+#define CEC_DIST_OPT_TEST_ABORT 2
 int cec_dist_set_option(cec_dist* d, int option, int value);
 /* Host only: the plan a degraded read of the lost list runs. The list holds nlost (segment,
  * fragment) erasures, any order, duplicates allowed, at most m distinct per segment

@@ -188,6 +188,39 @@ def test_c_dist_degraded_read_world1(k, m, nseg, F, exchange):
         g.close()
 
 
+def test_c_dist_abort_in_group_world1():
+    """The in-group failure path of cec_dist_degraded_read (CEC_DIST_OPT_TEST_ABORT): the round's
+    group is ended and the communicator aborted, the call returns CEC_ENCCL, later calls on the
+    handle too, destroying it is clean, and a new group on the same thread and codec then
+    rebuilds bit-exact (the thread's RCCL group state was left consistent)."""
+    import torch
+    import cess_amd
+    from cess_amd import distributed as D
+    from cess_amd.reedsolomon import CecError
+    k, m, nseg, F = 4, 2, 6, 65536
+    full, lost = _codewords(k, m, nseg, F)
+    mine = D.local_fragments(nseg, k + m, 1, 0)
+    store = D.FragmentStore({sf: i for i, sf in enumerate(mine)},
+                            torch.from_numpy(np.stack([full[s][f] for s, f in mine])).cuda())
+    enc = cess_amd.New(k, m)
+    g = D.RcclGroup(enc, D.RcclGroup.unique_id(), 1, 0, "survivors")
+    g.set_test_abort(0)
+    with pytest.raises(CecError) as ei:
+        g.degraded_read(lost, store)
+    assert ei.value.code == -6
+    with pytest.raises(CecError) as ei:
+        g.degraded_read(lost, store)
+    assert ei.value.code == -6
+    g.close()
+    g2 = D.RcclGroup(enc, D.RcclGroup.unique_id(), 1, 0, "survivors")
+    try:
+        out = g2.degraded_read(lost, store)
+        for (s, f), t in out.items():
+            assert np.array_equal(t.cpu().numpy(), full[s][f]), (s, f)
+    finally:
+        g2.close()
+
+
 def _c_rank(rank, world, uid_path, k, m, nseg, F, q, exchange="survivors"):
     os.environ.update(HSA_ENABLE_IPC_MODE_LEGACY="0")
     import time
