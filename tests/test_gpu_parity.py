@@ -799,18 +799,21 @@ def test_fftdec_matches_oracle(torch, cess, corc, ne, ln, mode):
     enc.set_option(8, 0)
 
 
-def test_fftdec_both_decoders_one_call(torch, cess, corc):
-    """One per-segment rebuild whose patterns send half the segments to the syndrome-row decoder
-    (8 erasures) and half to the formal-derivative decoder (32, the cost model's default picks):
-    both launches of the plan write their own segments only, bit-exact with the C oracle."""
+@pytest.mark.parametrize("ln,nd_want", [(512 * 1024, 2), (2048, 8)])
+def test_fftdec_both_decoders_one_call(torch, cess, corc, ln, nd_want):
+    """One per-segment rebuild whose patterns the cost model sends 6 segments to the syndrome-row
+    decoder (8 erasures) and 2 to the formal-derivative decoder (32). At 512 KiB shards the split
+    pays for its second launch: both launches write their own segments only, bit-exact with the C
+    oracle. At 2 KiB the whole batch is cheaper on the derivative decoder alone (the batch-level
+    split rule folds the syndrome-row segments into its launch)."""
     k = m = 32
-    nseg, ln = 8, 2048
+    nseg = 8
     rng = np.random.default_rng(808)
     data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
     want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
     present = np.ones((nseg, 64), np.uint8)
     for s in range(nseg):
-        present[s, rng.choice(64, size=8 if s % 2 else 32, replace=False)] = 0
+        present[s, rng.choice(64, size=32 if s in (2, 5) else 8, replace=False)] = 0
     enc = cess.New(k, m)
     b4, b5 = enc.stat(4), enc.stat(5)
     d_data = to_dev(torch, data * present[:, :k, None])
@@ -819,7 +822,7 @@ def test_fftdec_both_decoders_one_call(torch, cess, corc):
     torch.cuda.synchronize()
     assert np.array_equal(d_data.cpu().numpy(), data)
     assert np.array_equal(d_par.cpu().numpy(), want)
-    assert enc.stat(4) - b4 == nseg and enc.stat(5) - b5 == nseg // 2
+    assert enc.stat(4) - b4 == nseg and enc.stat(5) - b5 == nd_want
 
 
 @pytest.mark.parametrize("ln", [1000, 1024 + 512])

@@ -15,9 +15,9 @@ step() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-step tests 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "fftdec or wide or host_api or dist or partial or repair"
+step tests 300 python -u -m pytest tests -m gpu --maxfail=5 -v --timeout 120 --timeout-method thread -k "fftdec or wide or host_api or dist or partial or repair"
 for e in 32 24 16; do
-  step ab_e$e 120 python -u bench.py --config 6 --erasures $e --fftdec-mode 2 --sweep -1,70 --steps 20 --warmup 30
+  step ab_e$e 120 python -u bench.py --config 6 --erasures $e --fftdec-mode 2 --sweep=-1,70 --steps 20 --warmup 30
 done
 step c6_e32 120 python -u bench.py --config 6 --erasures 32 --no-cpu-baseline
 echo done
