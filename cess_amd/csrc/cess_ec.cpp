@@ -687,9 +687,9 @@ bool is_reencode(const cec_codec* c, const Program& p) {
 // an output; profiles/r03/fdd_libs_ab1.jsonl).
 double fdd_cost(int nout) { return 647.0 + 5.4 * nout; }
 enum FdKind { kFdNone = 0, kFdM = 1, kFdD = 2 };
-// tuning build: CEC_OPT_CT_VARIANT of this value runs the one-block-per-wave k_fftdec_d instead of
-// the pipelined k_fftdec_dp (A/B sweeps)
-constexpr int kCtVariantFddBlock = 70;
+// tuning build: CEC_OPT_CT_VARIANT 70 runs the one-block-per-wave k_fftdec_d instead of the
+// pipelined k_fftdec_dp, 71 the pipelined one with LDS-DMA staging (A/B sweeps)
+int fdd_form(const cec_codec* c);
 double fdm_cost(int nout, int nrs) {
   return 280.0 + (cec::fftdec_big(nrs) ? 3.8 : 3.3) * nout * nrs;
 }
@@ -709,6 +709,10 @@ int fftdec_choice(int nout, int nrs, bool has_m, bool has_d) {
   return kFdNone;
 }
 
+int fdd_form(const cec_codec* c) {
+  return c->opts.ct_variant == 70 ? 0 : c->opts.ct_variant == 71 ? 2 : 1;
+}
+
 int use_fftdec(const cec_codec* c, const Program& p) {
   if (c->force_generic || (!p.fd && !p.fdd) || c->fftdec_min <= 0 || p.nout < c->fftdec_min)
     return kFdNone;
@@ -725,8 +729,7 @@ int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* s
   const int fk = use_fftdec(c, p);
   if ((fk == kFdM && cec::launch_fftdec(L, p.fd_side, cec::fftdec_big(p.fd_nrs), p.fd, nullptr,
                                         seg_list, nseg, st)) ||
-      (fk == kFdD && cec::launch_fftdec_d(L, p.fdd, nullptr, seg_list, nseg, st,
-                                          c->opts.ct_variant != kCtVariantFddBlock))) {
+      (fk == kFdD && cec::launch_fftdec_d(L, p.fdd, nullptr, seg_list, nseg, st, fdd_form(c)))) {
     c->fd_segments += nseg;
     if (fk == kFdD) c->fdd_segments += nseg;
     return check_launch();
@@ -955,8 +958,7 @@ int launch_ps_plan(cec_codec* c, const PsPlan& p, const Layout& L, hipStream_t s
   const uint32_t* const* ptrs = static_cast<const uint32_t* const*>(p.ptrs);
   for (const auto& f : p.fd) {
     const bool ok = f.side == 2 ? cec::launch_fftdec_d(L, nullptr, ptrs + f.off, p.list + f.off,
-                                                       (uint32_t)f.count, st,
-                                                       c->opts.ct_variant != kCtVariantFddBlock)
+                                                       (uint32_t)f.count, st, fdd_form(c))
                                 : cec::launch_fftdec(L, f.side, f.big, nullptr, ptrs + f.off,
                                                      p.list + f.off, (uint32_t)f.count, st);
     if (!ok)

@@ -398,10 +398,25 @@ __device__ __forceinline__ uint32_t dp_rdmask(cplan_t P, uint32_t sh) {
   return ((P[FftDecDLayout::kLam + J] >> sh) & 0xFF) ? 0xFFFFFFFFu : 0u;
 }
 
+// LDS-DMA form of the next block's input (kDma): a wave's ring of kRing slots, each two 1 KiB
+// pieces (the 16-byte pieces at the lane's column and 256 bytes on), filled by buffer_load ... lds
+// three slots ahead (slots 0..2 before the transforms), so the loads are in flight for a slot's
+// whole work instead of its FFT tail alone, without VGPRs. The compiler does not order a ds_read
+// after the DMA that fills it: the waits are explicit (vmcnt counts of the issue order below).
+constexpr int kRing = 3;
+typedef __attribute__((address_space(3))) void lds_void;
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool kDma>
 __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
     Layout L, const uint32_t* __restrict__ plan1, const uint32_t* const* __restrict__ plans,
     const uint32_t* __restrict__ seg_list, uint32_t nblk, uint64_t units) {
   __shared__ __attribute__((aligned(16))) uint32_t lmask_all[4][kMergedWords];
+  __shared__ __attribute__((aligned(16))) uint32_t ring_all[kDma ? 4 : 1][kRing][2][256];
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
   const uint64_t nwave = (uint64_t)gridDim.x * 4;
   const uint64_t wave = (uint64_t)blockIdx.x * 4 + wid;
@@ -423,8 +438,11 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
     const uint32_t* Pg = plans ? plans[y] : plan1;
     {  // wave-uniform: keep the pointer (and the choice above) scalar
       const uint64_t pv = (uint64_t)Pg;
-      Pg = (const uint32_t*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pv >> 32)) << 32) |
-                             __builtin_amdgcn_readfirstlane((uint32_t)pv));
+      // (readfirstlane returns int: each half goes through uint32_t, or the low half would be
+      // sign-extended into the high one)
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(pv >> 32));
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)pv);
+      Pg = (const uint32_t*)((uint64_t)hi << 32 | lo);
     }
     const cplan_t P = (cplan_t)Pg;
     const auto rD = rsrc(L.data + seg * L.data_seg_stride);
@@ -458,6 +476,21 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
       });
       fresh = 0;
     }
+    if constexpr (kDma) {  // the next block's slots 0..kRing-1, in flight during the transforms
+      if (left > 1 && blk + 1 < nblk) {
+        const LaneCtx cd = lane_ctx(wave_col, ss);
+        sfor<kRing>([&](auto J) CEC_FFT_AI {
+          lds_void* base = (lds_void*)ring_all[kDma ? wid : 0][J][0];
+          lds_void* base2 = (lds_void*)ring_all[kDma ? wid : 0][J][1];
+          const uint32_t voff = dp_rdmask<J>(P, cd.sh) ? cd.lcol + 512 : kOff;
+          const uint32_t soff = (uint32_t)(4 * (J & 7)) * ss;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(J < 8 ? rD : rP, base, 16, voff, soff, 0, 2);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(J < 8 ? rD : rP, base2, 16, voff + kPiece, soff,
+                                                   0, 2);
+        });
+        asm volatile("" ::: "memory");
+      }
+    }
     fence_all(X);
     ifft64(X, lane_ctx(0, 0).e1, lane_ctx(0, 0).e2);
     fence_all(X);
@@ -476,13 +509,40 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
     const uint32_t nx = next ? 0xFFFFFFFFu : 0u;
     const LaneCtx c1 = lane_ctx(wave_col, ss);
     const uint32_t ncol = c1.lcol + 512;  // the same lane's columns in the next block
+    // kDma: slot J of the next block into ring entry J % kRing
+    auto dma = [&](auto J) CEC_FFT_AI {
+      if constexpr (kDma && J < 16) {
+        if (next) {
+          lds_void* base = (lds_void*)ring_all[kDma ? wid : 0][J % kRing][0];
+          lds_void* base2 = (lds_void*)ring_all[kDma ? wid : 0][J % kRing][1];
+          const uint32_t voff = (dp_rdmask<J>(P, c1.sh) & nx) ? ncol : kOff;
+          const uint32_t soff = (uint32_t)(4 * (J & 7)) * ss;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(J < 8 ? rD : rP, base, 16, voff, soff, 0, 2);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(J < 8 ? rD : rP, base2, 16, voff + kPiece, soff,
+                                                   0, 2);
+        }
+      }
+    };
+    (void)dma;
     sfor<16>([&](auto J) CEC_FFT_AI {
       const uint32_t dw = P[FftDecDLayout::kDinv + J];
       after_prev<J>(X);
       uint32_t pre[8];
-      uint32_t col = ncol;  // the load is issued in its slot, not hoisted into earlier slots
-      if constexpr (J > 0) asm volatile("" : "+v"(col) : "v"(X[J - 1][7]));
-      dp_load(rD, rP, J, col, ss, dp_rdmask<J>(P, c1.sh) & nx, pre);
+      if constexpr (kDma) {
+        // VMEM issued after slot J's second piece: see the order at the slot's end
+        constexpr int after = J == 0 ? 4 : J == 1 ? 6 : J <= 13 ? 8 : J == 14 ? 6 : 4;
+        wait_vm<after>();
+        const u32x4 a = *(const __attribute__((address_space(3))) u32x4*)(
+            (const lds_u32*)ring_all[wid][J % kRing][0] + 4 * __lane_id());
+        const u32x4 b = *(const __attribute__((address_space(3))) u32x4*)(
+            (const lds_u32*)ring_all[wid][J % kRing][1] + 4 * __lane_id());
+        pre[0] = a.x; pre[1] = a.y; pre[2] = a.z; pre[3] = a.w;
+        pre[4] = b.x; pre[5] = b.y; pre[6] = b.z; pre[7] = b.w;
+      } else {
+        uint32_t col = ncol;  // the load is issued in its slot, not hoisted into earlier slots
+        if constexpr (J > 0) asm volatile("" : "+v"(col) : "v"(X[J - 1][7]));
+        dp_load(rD, rP, J, col, ss, dp_rdmask<J>(P, c1.sh) & nx, pre);
+      }
       fft64_tail<J>(X[J], c1.e1, c1.e2);
       const uint32_t rd = dp_rdmask<J>(P, c1.sh) & nx;
       tr8(pre);
@@ -495,6 +555,10 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
       });
       tr8(O);
       bst(J < 8 ? rD : rP, ((dw >> c1.sh) & 0xFF) ? c1.lcol : kOff, (uint32_t)(4 * (J & 7)) * ss, O);
+      if constexpr (kDma) {
+        asm volatile("" ::: "memory");  // the store, then the next DMA (the wait counts' order)
+        dma(std::integral_constant<int, J + kRing>{});
+      }
       // the next slot starts once this slot's stored planes exist (the scheduler would otherwise
       // overlap two slots' temporaries)
       if constexpr (J + 1 < 16)
@@ -510,6 +574,7 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
 }
 
 // Resident workgroups of k_fftdec_dp on the device (the persistent grid), cached per device.
+template <bool kDma>
 uint32_t fdd_resident_wgs() {
   static uint32_t cache[64] = {};
   int dev = 0;
@@ -517,7 +582,8 @@ uint32_t fdd_resident_wgs() {
   if (!cache[dev]) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_fftdec_dp, 256, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_fftdec_dp<kDma>, 256, 0) !=
+            hipSuccess ||
         cus <= 0 || per <= 0)
       return 1024;
     cache[dev] = (uint32_t)(cus * per);
@@ -528,14 +594,22 @@ uint32_t fdd_resident_wgs() {
 }  // namespace
 
 bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* const* plans,
-                     const uint32_t* seg_list, uint32_t nseg, hipStream_t st, bool pipelined) {
+                     const uint32_t* seg_list, uint32_t nseg, hipStream_t st, int form) {
   if (!fftdec_layout_ok(L)) return false;
   if (nseg == 0) return true;
-  if (pipelined) {
+  if (form != 0) {
     const uint32_t nblk = (uint32_t)(L.len / 512);
     const uint64_t units = (uint64_t)nseg * nblk;
-    const uint64_t wgs = std::min<uint64_t>(fdd_resident_wgs(), (units + 3) / 4);
-    hipLaunchKernelGGL(k_fftdec_dp, dim3((unsigned)wgs), dim3(256), 0, st, L, plan1, plans,
+#ifdef CEC_TUNING
+    if (form == 2) {  // the LDS-DMA form: tuning build only
+      const uint64_t wgs = std::min<uint64_t>(fdd_resident_wgs<true>(), (units + 3) / 4);
+      hipLaunchKernelGGL(k_fftdec_dp<true>, dim3((unsigned)wgs), dim3(256), 0, st, L, plan1,
+                         plans, seg_list, nblk, units);
+      return true;
+    }
+#endif
+    const uint64_t wgs = std::min<uint64_t>(fdd_resident_wgs<false>(), (units + 3) / 4);
+    hipLaunchKernelGGL(k_fftdec_dp<false>, dim3((unsigned)wgs), dim3(256), 0, st, L, plan1, plans,
                        seg_list, nblk, units);
     return true;
   }

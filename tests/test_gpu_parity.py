@@ -221,6 +221,33 @@ def test_ct_variants_identical(torch, cess, corc, k, m, ln):
     enc.set_option(2, -1)
 
 
+@pytest.mark.parametrize("variant", [70, 71, -1])
+@pytest.mark.parametrize("nseg,ln", [(1, 4096), (3, 16384), (9, 8192)])
+def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):
+    """The formal-derivative decoder's forms (tuning build): 70 one block per wave (k_fftdec_d),
+    -1 the pipelined persistent kernel (k_fftdec_dp, the product's), 71 the pipelined kernel with
+    the next block's inputs staged by LDS DMA. Runs of blocks that cross segments (per-segment
+    plans), a single segment's host-API-sized batch, 12..32 erasures: bit-exact with the oracle."""
+    k = m = 32
+    rng = np.random.default_rng(ln + nseg)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = np.ones((nseg, 64), np.uint8)
+    for s in range(nseg):
+        present[s, rng.choice(64, size=int(rng.integers(12, 33)), replace=False)] = 0
+    enc = cess.New(k, m, tuning=True)
+    enc.set_option(2, variant)
+    enc.set_option(8, 2)  # the derivative decoder for every segment
+    d_data = to_dev(torch, data * present[:, :k, None])
+    d_par = to_dev(torch, want * present[:, k:, None])
+    before = enc.stat(5)
+    enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+    torch.cuda.synchronize()
+    assert enc.stat(5) - before == nseg
+    assert np.array_equal(d_data.cpu().numpy(), data)
+    assert np.array_equal(d_par.cpu().numpy(), want)
+
+
 def test_misaligned_layout_byte_path(torch, cess, corc):
     """shard_len % 16 != 0 with nseg > 1 makes shard starts unaligned -> byte kernels."""
     for (k, m) in [(2, 1), (32, 32), (5, 3)]:
