@@ -379,9 +379,9 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const u
 // plan's kMerged masks: a position is never both read and an output). The operand is the next
 // block's loaded input on read lanes and this block's FFT output elsewhere; the product goes back to
 // the registers as the next block's input (zero on unread lanes) and to memory as this block's
-// output (stored by output lanes only). The grid is the chip's resident waves (persistent); wave w
-// takes units [w U / W, (w + 1) U / W) of the U = nseg x (len / 512) (segment, block) units, and
-// starts afresh (table, full input step) where its run crosses into the next segment.
+// output (stored by output lanes only). The grid is the chip's resident waves (persistent), G of
+// them per segment; wave i of a segment walks its blocks i, i + G, ... (one plan, no segment
+// crossings).
 
 // wave-private LDS: the merged-constant masks of the wave's current segment (2 KiB)
 constexpr int kMergedWords = 16 * 4 * 8;
@@ -400,10 +400,23 @@ __device__ __forceinline__ uint32_t dp_rdmask(cplan_t P, uint32_t sh) {
 
 // LDS-DMA form of the next block's input (kDma): a wave's ring of kRing slots, each two 1 KiB
 // pieces (the 16-byte pieces at the lane's column and 256 bytes on), filled by buffer_load ... lds
-// three slots ahead (slots 0..2 before the transforms), so the loads are in flight for a slot's
-// whole work instead of its FFT tail alone, without VGPRs. The compiler does not order a ds_read
-// after the DMA that fills it: the waits are explicit (vmcnt counts of the issue order below).
-constexpr int kRing = 3;
+// kAhead slots ahead (slots 0..kAhead-1 before the transforms), so the loads are in flight for a
+// slot's whole work instead of its FFT tail alone, without VGPRs. Slot J reads its entry, then
+// issues slot J + kAhead into entry (J + kAhead) % kRing (read one slot earlier). The compiler does
+// not order a ds_read after the DMA that fills it: the waits are explicit vmcnt counts of the issue
+// order (dma_after).
+constexpr int kRing = 4, kAhead = 3;
+// VMEM instructions issued after slot J's DMA pair and before slot J's wait: per slot the order is
+// [wait J] [DMA J + kAhead] [store J]; slots 0..kAhead-1 were issued before the transforms
+constexpr int dma_after(int J) {
+  int n = 0;
+  if (J < kAhead) n += 2 * (kAhead - 1 - J);  // the later top-of-unit pairs
+  for (int j = J < kAhead ? 0 : J - kAhead; j < J; ++j) {
+    if (j >= 0 && j + kAhead < 16 && j + kAhead > J) n += 2;  // DMA j + kAhead issued in slot j
+    if (j >= 0 && (J < kAhead || j > J - kAhead || (j == J - kAhead))) n += 2;  // store j
+  }
+  return n;
+}
 typedef __attribute__((address_space(3))) void lds_void;
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -414,14 +427,15 @@ __device__ __forceinline__ void wait_vm() {
 template <bool kDma>
 __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
     Layout L, const uint32_t* __restrict__ plan1, const uint32_t* const* __restrict__ plans,
-    const uint32_t* __restrict__ seg_list, uint32_t nblk, uint64_t units) {
+    const uint32_t* __restrict__ seg_list, uint32_t nblk, uint32_t nseg, uint32_t G) {
   __shared__ __attribute__((aligned(16))) uint32_t lmask_all[4][kMergedWords];
   __shared__ __attribute__((aligned(16))) uint32_t ring_all[kDma ? 4 : 1][kRing][2][256];
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
-  const uint64_t nwave = (uint64_t)gridDim.x * 4;
-  const uint64_t wave = (uint64_t)blockIdx.x * 4 + wid;
-  const uint64_t u0 = wave * units / nwave, u1 = (wave + 1) * units / nwave;
-  if (u0 >= u1) return;
+  // G waves per segment; wave i of a segment takes its blocks i, i + G, i + 2G, ...: the waves of
+  // a workgroup (and their neighbours) read neighbouring 512-column blocks of the same shards at
+  // any time, as the one-block-per-wave grid does (blocks of a run G apart, one plan)
+  const uint32_t wave = blockIdx.x * 4 + wid;
+  if (wave >= nseg * G) return;
   lds_u32* lmask = (lds_u32*)lmask_all[wid];
   const uint32_t ss = (uint32_t)L.shard_stride;
 
@@ -429,9 +443,11 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
   // loop state kept scalar (32-bit, wave-uniform): (segment list index, block) of the unit,
   // stepped along the run, the units left and whether the next one starts a segment afresh (no
   // division or 64-bit compare inside the loop: that is VALU work with every X register live)
-  uint32_t y = __builtin_amdgcn_readfirstlane((uint32_t)(u0 / nblk));
-  uint32_t blk = __builtin_amdgcn_readfirstlane((uint32_t)(u0 % nblk));
-  uint32_t left = __builtin_amdgcn_readfirstlane((uint32_t)(u1 - u0));
+  // (the divisions are VALU work: their results go back to scalars, or the plan pointer and
+  // every plan word would be vector loads)
+  const uint32_t y = (uint32_t)__builtin_amdgcn_readfirstlane(wave / G);
+  uint32_t blk = (uint32_t)__builtin_amdgcn_readfirstlane(wave - y * G);
+  uint32_t left = (uint32_t)__builtin_amdgcn_readfirstlane((nblk - blk + G - 1) / G);
   uint32_t fresh = 1;
   for (; left; --left) {
     const uint32_t seg = seg_list ? seg_list[y] : y;
@@ -477,12 +493,12 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
       fresh = 0;
     }
     if constexpr (kDma) {  // the next block's slots 0..kRing-1, in flight during the transforms
-      if (left > 1 && blk + 1 < nblk) {
-        const LaneCtx cd = lane_ctx(wave_col, ss);
-        sfor<kRing>([&](auto J) CEC_FFT_AI {
+      if (left > 1) {
+        const LaneCtx cd = lane_ctx(wave_col + 512 * G, ss);
+        sfor<kAhead>([&](auto J) CEC_FFT_AI {
           lds_void* base = (lds_void*)ring_all[kDma ? wid : 0][J][0];
           lds_void* base2 = (lds_void*)ring_all[kDma ? wid : 0][J][1];
-          const uint32_t voff = dp_rdmask<J>(P, cd.sh) ? cd.lcol + 512 : kOff;
+          const uint32_t voff = dp_rdmask<J>(P, cd.sh) ? cd.lcol : kOff;
           const uint32_t soff = (uint32_t)(4 * (J & 7)) * ss;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(J < 8 ? rD : rP, base, 16, voff, soff, 0, 2);
           __builtin_amdgcn_raw_ptr_buffer_load_lds(J < 8 ? rD : rP, base2, 16, voff + kPiece, soff,
@@ -505,10 +521,10 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
     // Branch-free per slot (uniform branches here cost registers across the unrolled slots):
     // without a next block the loads are all out of range (no memory traffic) and rd = 0; lanes
     // that are not outputs store out of range.
-    const uint32_t next = left > 1 && blk + 1 < nblk ? 1u : 0u;
+    const uint32_t next = left > 1 ? 1u : 0u;
     const uint32_t nx = next ? 0xFFFFFFFFu : 0u;
     const LaneCtx c1 = lane_ctx(wave_col, ss);
-    const uint32_t ncol = c1.lcol + 512;  // the same lane's columns in the next block
+    const uint32_t ncol = c1.lcol + 512 * G;  // the same lane's columns in the next block
     // kDma: slot J of the next block into ring entry J % kRing
     auto dma = [&](auto J) CEC_FFT_AI {
       if constexpr (kDma && J < 16) {
@@ -529,15 +545,19 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
       after_prev<J>(X);
       uint32_t pre[8];
       if constexpr (kDma) {
-        // VMEM issued after slot J's second piece: see the order at the slot's end
-        constexpr int after = J == 0 ? 4 : J == 1 ? 6 : J <= 13 ? 8 : J == 14 ? 6 : 4;
-        wait_vm<after>();
+        wait_vm<dma_after(J)>();
+        uint32_t lane;  // opaque: derived here, not kept live through the unit
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
         const u32x4 a = *(const __attribute__((address_space(3))) u32x4*)(
-            (const lds_u32*)ring_all[wid][J % kRing][0] + 4 * __lane_id());
+            (const lds_u32*)ring_all[wid][J % kRing][0] + 4 * lane);
         const u32x4 b = *(const __attribute__((address_space(3))) u32x4*)(
-            (const lds_u32*)ring_all[wid][J % kRing][1] + 4 * __lane_id());
+            (const lds_u32*)ring_all[wid][J % kRing][1] + 4 * lane);
         pre[0] = a.x; pre[1] = a.y; pre[2] = a.z; pre[3] = a.w;
         pre[4] = b.x; pre[5] = b.y; pre[6] = b.z; pre[7] = b.w;
+        // the ring entry this slot's DMA fills was read one slot earlier; the reads above complete
+        // before it is issued (LDS reads and LDS DMA writes are not ordered with each other)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        dma(std::integral_constant<int, J + kAhead>{});
       } else {
         uint32_t col = ncol;  // the load is issued in its slot, not hoisted into earlier slots
         if constexpr (J > 0) asm volatile("" : "+v"(col) : "v"(X[J - 1][7]));
@@ -555,10 +575,7 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
       });
       tr8(O);
       bst(J < 8 ? rD : rP, ((dw >> c1.sh) & 0xFF) ? c1.lcol : kOff, (uint32_t)(4 * (J & 7)) * ss, O);
-      if constexpr (kDma) {
-        asm volatile("" ::: "memory");  // the store, then the next DMA (the wait counts' order)
-        dma(std::integral_constant<int, J + kRing>{});
-      }
+      if constexpr (kDma) asm volatile("" ::: "memory");  // the store stays in this slot
       // the next slot starts once this slot's stored planes exist (the scheduler would otherwise
       // overlap two slots' temporaries)
       if constexpr (J + 1 < 16)
@@ -566,10 +583,7 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
                      : "v"(O[3]), "v"(O[7]));
     });
     fresh = next ^ 1u;
-    if (++blk == nblk) {
-      blk = 0;
-      ++y;
-    }
+    blk += G;
   }
 }
 
@@ -598,19 +612,27 @@ bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* con
   if (!fftdec_layout_ok(L)) return false;
   if (nseg == 0) return true;
   if (form != 0) {
+    // G waves per segment: the resident waves spread over the segments (at least one each;
+    // more segments than resident waves: one wave per segment, in rounds)
     const uint32_t nblk = (uint32_t)(L.len / 512);
-    const uint64_t units = (uint64_t)nseg * nblk;
 #ifdef CEC_TUNING
-    if (form == 2) {  // the LDS-DMA form: tuning build only
-      const uint64_t wgs = std::min<uint64_t>(fdd_resident_wgs<true>(), (units + 3) / 4);
+    const bool dma = form == 2;  // the LDS-DMA form: tuning build only
+#else
+    const bool dma = false;
+#endif
+    const uint64_t waves = 4ull * (dma ? fdd_resident_wgs<true>() : fdd_resident_wgs<false>());
+    const uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nblk, waves / nseg));
+    const uint64_t wgs = ((uint64_t)nseg * G + 3) / 4;
+    if (wgs > 0x7FFFFFFFull) return false;
+#ifdef CEC_TUNING
+    if (dma) {
       hipLaunchKernelGGL(k_fftdec_dp<true>, dim3((unsigned)wgs), dim3(256), 0, st, L, plan1,
-                         plans, seg_list, nblk, units);
+                         plans, seg_list, nblk, nseg, G);
       return true;
     }
 #endif
-    const uint64_t wgs = std::min<uint64_t>(fdd_resident_wgs<false>(), (units + 3) / 4);
     hipLaunchKernelGGL(k_fftdec_dp<false>, dim3((unsigned)wgs), dim3(256), 0, st, L, plan1, plans,
-                       seg_list, nblk, units);
+                       seg_list, nblk, nseg, G);
     return true;
   }
   const uint64_t gx = (L.len / 512 * 64 + 255) / 256;
