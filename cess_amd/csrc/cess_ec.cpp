@@ -710,7 +710,12 @@ int fftdec_choice(int nout, int nrs, bool has_m, bool has_d) {
 }
 
 int fdd_form(const cec_codec* c) {
-  return c->opts.ct_variant == 70 ? 0 : c->opts.ct_variant == 71 ? 2 : 1;
+  switch (c->opts.ct_variant) {
+    case 70: return 0;
+    case 71: return 2;
+    case 72: return 3;
+    default: return 1;
+  }
 }
 
 int use_fftdec(const cec_codec* c, const Program& p) {

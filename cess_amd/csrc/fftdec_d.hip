@@ -427,7 +427,8 @@ __device__ __forceinline__ void wait_vm() {
 template <bool kDma>
 __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
     Layout L, const uint32_t* __restrict__ plan1, const uint32_t* const* __restrict__ plans,
-    const uint32_t* __restrict__ seg_list, uint32_t nblk, uint32_t nseg, uint32_t G) {
+    const uint32_t* __restrict__ seg_list, uint32_t nblk, uint32_t nseg, uint32_t G,
+    uint32_t prio) {
   __shared__ __attribute__((aligned(16))) uint32_t lmask_all[4][kMergedWords];
   __shared__ __attribute__((aligned(16))) uint32_t ring_all[kDma ? 4 : 1][kRing][2][256];
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
@@ -449,7 +450,18 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
   uint32_t blk = (uint32_t)__builtin_amdgcn_readfirstlane(wave - y * G);
   uint32_t left = (uint32_t)__builtin_amdgcn_readfirstlane((nblk - blk + G - 1) / G);
   uint32_t fresh = 1;
+  const uint32_t total = left;
   for (; left; --left) {
+    // prio: the SIMD's arbiter favours older waves: in a long-lived (persistent) grid the oldest
+    // wave of a SIMD races ahead and the youngest is left to finish alone at one wave per SIMD. A
+    // wave's priority then follows the share of its run still ahead of it (lagging waves catch up).
+    if (prio) {
+      const uint32_t q = left * 4 / (total + 1);  // 0..3
+      if (q >= 3) __builtin_amdgcn_s_setprio(3);
+      else if (q == 2) __builtin_amdgcn_s_setprio(2);
+      else if (q == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     const uint32_t seg = seg_list ? seg_list[y] : y;
     const uint32_t* Pg = plans ? plans[y] : plan1;
     {  // wave-uniform: keep the pointer (and the choice above) scalar
@@ -627,12 +639,12 @@ bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* con
 #ifdef CEC_TUNING
     if (dma) {
       hipLaunchKernelGGL(k_fftdec_dp<true>, dim3((unsigned)wgs), dim3(256), 0, st, L, plan1,
-                         plans, seg_list, nblk, nseg, G);
+                         plans, seg_list, nblk, nseg, G, 0u);
       return true;
     }
 #endif
     hipLaunchKernelGGL(k_fftdec_dp<false>, dim3((unsigned)wgs), dim3(256), 0, st, L, plan1, plans,
-                       seg_list, nblk, nseg, G);
+                       seg_list, nblk, nseg, G, form == 3 ? 1u : 0u);
     return true;
   }
   const uint64_t gx = (L.len / 512 * 64 + 255) / 256;

@@ -221,7 +221,7 @@ def test_ct_variants_identical(torch, cess, corc, k, m, ln):
     enc.set_option(2, -1)
 
 
-@pytest.mark.parametrize("variant", [70, 71, -1])
+@pytest.mark.parametrize("variant", [70, 71, 72, -1])
 @pytest.mark.parametrize("nseg,ln", [(1, 4096), (3, 16384), (9, 8192)])
 def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):
     """The formal-derivative decoder's forms (tuning build): 70 one block per wave (k_fftdec_d),
