@@ -687,8 +687,8 @@ bool is_reencode(const cec_codec* c, const Program& p) {
 // an output; profiles/r03/fdd_libs_ab1.jsonl).
 double fdd_cost(int nout) { return 647.0 + 5.4 * nout; }
 enum FdKind { kFdNone = 0, kFdM = 1, kFdD = 2 };
-// tuning build: CEC_OPT_CT_VARIANT 70 runs the one-block-per-wave k_fftdec_d instead of the
-// pipelined k_fftdec_dp, 71 the pipelined one with LDS-DMA staging (A/B sweeps)
+// tuning build: CEC_OPT_CT_VARIANT 70 runs the pipelined persistent k_fftdec_dp instead of the
+// one-block-per-wave k_fftdec_d, 72 the same with wave priorities (A/B sweeps)
 int fdd_form(const cec_codec* c);
 double fdm_cost(int nout, int nrs) {
   return 280.0 + (cec::fftdec_big(nrs) ? 3.8 : 3.3) * nout * nrs;
@@ -711,10 +711,9 @@ int fftdec_choice(int nout, int nrs, bool has_m, bool has_d) {
 
 int fdd_form(const cec_codec* c) {
   switch (c->opts.ct_variant) {
-    case 70: return 0;
-    case 71: return 2;
+    case 70: return 1;
     case 72: return 3;
-    default: return 1;
+    default: return 0;
   }
 }
 

@@ -370,6 +370,7 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const u
   });
 }
 
+#ifdef CEC_TUNING
 // ---- the pipelined form (k_fftdec_dp) ----------------------------------------------------------
 // Every position needs exactly one run-time multiplication: lam(t) where it is read, 1 / lam'(t)
 // where it is an output. k_fftdec_d runs both per slot (a SIMD executes both sides of a lane-
@@ -398,39 +399,11 @@ __device__ __forceinline__ uint32_t dp_rdmask(cplan_t P, uint32_t sh) {
   return ((P[FftDecDLayout::kLam + J] >> sh) & 0xFF) ? 0xFFFFFFFFu : 0u;
 }
 
-// LDS-DMA form of the next block's input (kDma): a wave's ring of kRing slots, each two 1 KiB
-// pieces (the 16-byte pieces at the lane's column and 256 bytes on), filled by buffer_load ... lds
-// kAhead slots ahead (slots 0..kAhead-1 before the transforms), so the loads are in flight for a
-// slot's whole work instead of its FFT tail alone, without VGPRs. Slot J reads its entry, then
-// issues slot J + kAhead into entry (J + kAhead) % kRing (read one slot earlier). The compiler does
-// not order a ds_read after the DMA that fills it: the waits are explicit vmcnt counts of the issue
-// order (dma_after).
-constexpr int kRing = 4, kAhead = 3;
-// VMEM instructions issued after slot J's DMA pair and before slot J's wait: per slot the order is
-// [wait J] [DMA J + kAhead] [store J]; slots 0..kAhead-1 were issued before the transforms
-constexpr int dma_after(int J) {
-  int n = 0;
-  if (J < kAhead) n += 2 * (kAhead - 1 - J);  // the later top-of-unit pairs
-  for (int j = J < kAhead ? 0 : J - kAhead; j < J; ++j) {
-    if (j >= 0 && j + kAhead < 16 && j + kAhead > J) n += 2;  // DMA j + kAhead issued in slot j
-    if (j >= 0 && (J < kAhead || j > J - kAhead || (j == J - kAhead))) n += 2;  // store j
-  }
-  return n;
-}
-typedef __attribute__((address_space(3))) void lds_void;
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <bool kDma>
 __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
     Layout L, const uint32_t* __restrict__ plan1, const uint32_t* const* __restrict__ plans,
     const uint32_t* __restrict__ seg_list, uint32_t nblk, uint32_t nseg, uint32_t G,
     uint32_t prio) {
   __shared__ __attribute__((aligned(16))) uint32_t lmask_all[4][kMergedWords];
-  __shared__ __attribute__((aligned(16))) uint32_t ring_all[kDma ? 4 : 1][kRing][2][256];
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
   // G waves per segment; wave i of a segment takes its blocks i, i + G, i + 2G, ...: the waves of
   // a workgroup (and their neighbours) read neighbouring 512-column blocks of the same shards at
@@ -504,21 +477,6 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
       });
       fresh = 0;
     }
-    if constexpr (kDma) {  // the next block's slots 0..kRing-1, in flight during the transforms
-      if (left > 1) {
-        const LaneCtx cd = lane_ctx(wave_col + 512 * G, ss);
-        sfor<kAhead>([&](auto J) CEC_FFT_AI {
-          lds_void* base = (lds_void*)ring_all[kDma ? wid : 0][J][0];
-          lds_void* base2 = (lds_void*)ring_all[kDma ? wid : 0][J][1];
-          const uint32_t voff = dp_rdmask<J>(P, cd.sh) ? cd.lcol : kOff;
-          const uint32_t soff = (uint32_t)(4 * (J & 7)) * ss;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(J < 8 ? rD : rP, base, 16, voff, soff, 0, 2);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(J < 8 ? rD : rP, base2, 16, voff + kPiece, soff,
-                                                   0, 2);
-        });
-        asm volatile("" ::: "memory");
-      }
-    }
     fence_all(X);
     ifft64(X, lane_ctx(0, 0).e1, lane_ctx(0, 0).e2);
     fence_all(X);
@@ -537,40 +495,11 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
     const uint32_t nx = next ? 0xFFFFFFFFu : 0u;
     const LaneCtx c1 = lane_ctx(wave_col, ss);
     const uint32_t ncol = c1.lcol + 512 * G;  // the same lane's columns in the next block
-    // kDma: slot J of the next block into ring entry J % kRing
-    auto dma = [&](auto J) CEC_FFT_AI {
-      if constexpr (kDma && J < 16) {
-        if (next) {
-          lds_void* base = (lds_void*)ring_all[kDma ? wid : 0][J % kRing][0];
-          lds_void* base2 = (lds_void*)ring_all[kDma ? wid : 0][J % kRing][1];
-          const uint32_t voff = (dp_rdmask<J>(P, c1.sh) & nx) ? ncol : kOff;
-          const uint32_t soff = (uint32_t)(4 * (J & 7)) * ss;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(J < 8 ? rD : rP, base, 16, voff, soff, 0, 2);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(J < 8 ? rD : rP, base2, 16, voff + kPiece, soff,
-                                                   0, 2);
-        }
-      }
-    };
-    (void)dma;
     sfor<16>([&](auto J) CEC_FFT_AI {
       const uint32_t dw = P[FftDecDLayout::kDinv + J];
       after_prev<J>(X);
       uint32_t pre[8];
-      if constexpr (kDma) {
-        wait_vm<dma_after(J)>();
-        uint32_t lane;  // opaque: derived here, not kept live through the unit
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-        const u32x4 a = *(const __attribute__((address_space(3))) u32x4*)(
-            (const lds_u32*)ring_all[wid][J % kRing][0] + 4 * lane);
-        const u32x4 b = *(const __attribute__((address_space(3))) u32x4*)(
-            (const lds_u32*)ring_all[wid][J % kRing][1] + 4 * lane);
-        pre[0] = a.x; pre[1] = a.y; pre[2] = a.z; pre[3] = a.w;
-        pre[4] = b.x; pre[5] = b.y; pre[6] = b.z; pre[7] = b.w;
-        // the ring entry this slot's DMA fills was read one slot earlier; the reads above complete
-        // before it is issued (LDS reads and LDS DMA writes are not ordered with each other)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        dma(std::integral_constant<int, J + kAhead>{});
-      } else {
+      {
         uint32_t col = ncol;  // the load is issued in its slot, not hoisted into earlier slots
         if constexpr (J > 0) asm volatile("" : "+v"(col) : "v"(X[J - 1][7]));
         dp_load(rD, rP, J, col, ss, dp_rdmask<J>(P, c1.sh) & nx, pre);
@@ -587,7 +516,6 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
       });
       tr8(O);
       bst(J < 8 ? rD : rP, ((dw >> c1.sh) & 0xFF) ? c1.lcol : kOff, (uint32_t)(4 * (J & 7)) * ss, O);
-      if constexpr (kDma) asm volatile("" ::: "memory");  // the store stays in this slot
       // the next slot starts once this slot's stored planes exist (the scheduler would otherwise
       // overlap two slots' temporaries)
       if constexpr (J + 1 < 16)
@@ -600,7 +528,6 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
 }
 
 // Resident workgroups of k_fftdec_dp on the device (the persistent grid), cached per device.
-template <bool kDma>
 uint32_t fdd_resident_wgs() {
   static uint32_t cache[64] = {};
   int dev = 0;
@@ -608,7 +535,7 @@ uint32_t fdd_resident_wgs() {
   if (!cache[dev]) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_fftdec_dp<kDma>, 256, 0) !=
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_fftdec_dp, 256, 0) !=
             hipSuccess ||
         cus <= 0 || per <= 0)
       return 1024;
@@ -617,36 +544,30 @@ uint32_t fdd_resident_wgs() {
   return cache[dev];
 }
 
+#endif  // CEC_TUNING
+
 }  // namespace
 
 bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* const* plans,
                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st, int form) {
   if (!fftdec_layout_ok(L)) return false;
   if (nseg == 0) return true;
-  if (form != 0) {
-    // G waves per segment: the resident waves spread over the segments (at least one each;
-    // more segments than resident waves: one wave per segment, in rounds)
-    const uint32_t nblk = (uint32_t)(L.len / 512);
 #ifdef CEC_TUNING
-    const bool dma = form == 2;  // the LDS-DMA form: tuning build only
-#else
-    const bool dma = false;
-#endif
-    const uint64_t waves = 4ull * (dma ? fdd_resident_wgs<true>() : fdd_resident_wgs<false>());
+  if (form == 1 || form == 3) {
+    // the pipelined form: G waves per segment, the resident waves spread over the segments (at
+    // least one each; more segments than resident waves: one wave per segment, in rounds)
+    const uint32_t nblk = (uint32_t)(L.len / 512);
+    const uint64_t waves = 4ull * fdd_resident_wgs();
     const uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nblk, waves / nseg));
     const uint64_t wgs = ((uint64_t)nseg * G + 3) / 4;
     if (wgs > 0x7FFFFFFFull) return false;
-#ifdef CEC_TUNING
-    if (dma) {
-      hipLaunchKernelGGL(k_fftdec_dp<true>, dim3((unsigned)wgs), dim3(256), 0, st, L, plan1,
-                         plans, seg_list, nblk, nseg, G, 0u);
-      return true;
-    }
-#endif
-    hipLaunchKernelGGL(k_fftdec_dp<false>, dim3((unsigned)wgs), dim3(256), 0, st, L, plan1, plans,
+    hipLaunchKernelGGL(k_fftdec_dp, dim3((unsigned)wgs), dim3(256), 0, st, L, plan1, plans,
                        seg_list, nblk, nseg, G, form == 3 ? 1u : 0u);
     return true;
   }
+#else
+  (void)form;
+#endif
   const uint64_t gx = (L.len / 512 * 64 + 255) / 256;
   for (uint32_t s0 = 0; s0 < nseg; s0 += 65535) {
     const uint32_t ny = nseg - s0 < 65535 ? nseg - s0 : 65535;

@@ -89,11 +89,12 @@ bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
                    const uint32_t* const* plans, const uint32_t* seg_list, uint32_t nseg,
                    hipStream_t st);
 // The formal-derivative decoder (fftdec_d.hip, plans of fftdec_plan_d): same arguments, any side.
-// form 1: the persistent kernel that merges a block's output multiplication with the next
-// block's input multiplication (k_fftdec_dp); 2: the same with the next block's inputs staged in
-// LDS by buffer_load ... lds; 0: one block per wave (k_fftdec_d).
+// form 0: one 512-column block per wave (k_fftdec_d, the product's). Tuning build only: 1 the
+// persistent kernel that merges a block's output multiplication with the next block's input
+// multiplication (k_fftdec_dp), 3 the same with wave priorities by remaining work (DESIGN.md §4:
+// 9 % fewer VALU per block, slower overall).
 bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* const* plans,
-                     const uint32_t* seg_list, uint32_t nseg, hipStream_t st, int form = 1);
+                     const uint32_t* seg_list, uint32_t nseg, hipStream_t st, int form = 0);
 
 // Whether a compile-time single-erasure decode kernel exists for (k, m, missing).
 bool has_decode_ct(int k, int m, int missing);

@@ -221,13 +221,14 @@ def test_ct_variants_identical(torch, cess, corc, k, m, ln):
     enc.set_option(2, -1)
 
 
-@pytest.mark.parametrize("variant", [70, 71, 72, -1])
+@pytest.mark.parametrize("variant", [70, 72, -1])
 @pytest.mark.parametrize("nseg,ln", [(1, 4096), (3, 16384), (9, 8192)])
 def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):
-    """The formal-derivative decoder's forms (tuning build): 70 one block per wave (k_fftdec_d),
-    -1 the pipelined persistent kernel (k_fftdec_dp, the product's), 71 the pipelined kernel with
-    the next block's inputs staged by LDS DMA. Runs of blocks that cross segments (per-segment
-    plans), a single segment's host-API-sized batch, 12..32 erasures: bit-exact with the oracle."""
+    """The formal-derivative decoder's forms (tuning build): -1 one block per wave (k_fftdec_d,
+    the product's), 70 the pipelined persistent kernel (k_fftdec_dp: a wave merges a block's
+    output multiplication with the next block's input one), 72 the same with wave priorities.
+    Several segments (per-segment plans), a single segment's host-API-sized batch, 12..32
+    erasures: bit-exact with the oracle."""
     k = m = 32
     rng = np.random.default_rng(ln + nseg)
     data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
