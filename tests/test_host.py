@@ -308,11 +308,7 @@ def test_product_kernel_occupancy():
               "k_rtbILi1E": 80, "k_rtbILi2E": 80, "k_fft3232_verify": 224,
               "k_fftdec_m": 256, "k_fftdec_mILj0ELb0E": 168, "k_fftdec_mILj1ELb0E": 168,
               "k_fftdec_d": 168}
-    # k_fftdec_dp (the pipelined derivative decoder) keeps its 128-register array live through
-    # the merge of two blocks' multiplications: two registers go to scratch once per 512-column
-    # block (two stores and two loads beside ~8,400 VALU), the rest of its state stays in VGPRs
-    scratch_cap = {"k_fftdec_dp": 12}
-    budget["k_fftdec_dp"] = 168
+    scratch_cap = {}
     for pat, cap in budget.items():
         ks = {n: r for n, r in res.items() if pat in n}
         assert ks, pat
