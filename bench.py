@@ -389,6 +389,20 @@ def launch_ranks(n: int, argv) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def erasure_patterns(k: int, m: int, nseg: int, ne: int, seed: int,
+                     lose_parity: bool = False) -> np.ndarray:
+    """Configs 6 / 7: [nseg][k + m] present flags, ne random erasures per segment (or every
+    parity shard lost); tests/test_host.py replays the chooser on the same patterns."""
+    rng = np.random.default_rng(seed)
+    present = np.ones((nseg, k + m), np.uint8)
+    for s_ in range(nseg):
+        if lose_parity:
+            present[s_, k:] = 0
+        else:
+            present[s_, rng.choice(k + m, size=ne, replace=False)] = 0
+    return present
+
+
 def kernel_label(config: int, fd_frac, erasures: int, generic: bool, rt_mode: int, k: int,
                  fdd_frac=0) -> str:
     """The dominant kernel of a bench line. Config 6: fd_frac = share of the timed rebuilds the
@@ -800,14 +814,9 @@ def main() -> None:
                 else np.full(nseg, args.erase))
         present[np.arange(nseg), lost] = 0
     elif args.config in (6, 7):
-        rng = np.random.default_rng(seg0 + args.config)
-        present = np.ones((nseg, k + m), np.uint8)
         ne = (args.erasures or m) if args.config == 6 else 1
-        for s_ in range(nseg):
-            if args.lose_parity and args.config == 6:
-                present[s_, k:] = 0
-            else:
-                present[s_, rng.choice(k + m, size=ne, replace=False)] = 0
+        present = erasure_patterns(k, m, nseg, ne, seed=seg0 + args.config,
+                                   lose_parity=args.lose_parity and args.config == 6)
     d_hex = None
     gather = None
     if args.config == 4:

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/cess_ec.h"
+#include "fftdec_cost.h"
 #include "fftdec_plan.h"
 #include "gf256.h"
 #include "kernels.h"
@@ -674,41 +675,14 @@ bool is_reencode(const cec_codec* c, const Program& p) {
   return true;
 }
 
-// The FFT-domain decoder costs T1 plus (outputs x syndrome slots) Horner rows; k_rthx costs
-// about the same per output at every pattern. Fitted to RS(32,32) rebuilds of 64 segments of
-// 512 KiB, random patterns (bench.py --config 6 --erasures e; profiles/r03/fd_lds_split.jsonl):
-// k_fftdec_m ~ 0.280 ms + 3.3 us per (output, slot) at up to four slots (three waves per SIMD;
-// 0.296 before its last FFT layer ran only on the slots it reads),
-// ~3.8 us past four (two waves); k_rthx ~ 0.235 ms + 33.9 us per output; up to four outputs the
-// alternative is k_rtb, ~0.13 ms + 57 us per output (5.9 / 4.9 / 3.9 / 3.4 TB/s
-// at one to four outputs).
-// The formal-derivative decoder k_fftdec_d costs nearly the same at every pattern: 0.69 ms at 8
-// outputs, 0.82 at 32 (the last FFT layers, the division and the stores only for slots holding
-// an output; profiles/r03/fdd_libs_ab1.jsonl).
-double fdd_cost(int nout) { return 647.0 + 5.4 * nout; }
-enum FdKind { kFdNone = 0, kFdM = 1, kFdD = 2 };
+// The decoder choice per pattern and per batch: fftdec_cost.h (tested on CPU against the
+// recorded warm sweep, tests/test_host.py::test_fftdec_chooser_on_recorded_costs).
+using cec::kFdD;
+using cec::kFdM;
+using cec::kFdNone;
+
 // tuning build: CEC_OPT_CT_VARIANT 70 runs the pipelined persistent k_fftdec_dp instead of the
 // one-block-per-wave k_fftdec_d, 72 the same with wave priorities (A/B sweeps)
-int fdd_form(const cec_codec* c);
-double fdm_cost(int nout, int nrs) {
-  return 280.0 + (cec::fftdec_big(nrs) ? 3.8 : 3.3) * nout * nrs;
-}
-// A batch split between the two decoders runs one launch more; its ramp and tail cost about this
-// much beyond the per-segment costs (24 random erasures: 0.812 ms split 8/92 against 0.798 all on
-// the derivative decoder, profiles/r03/fdd_crossover_e18_28.jsonl).
-constexpr double kSplitLaunchUs = 20.0;
-int fftdec_choice(int nout, int nrs, bool has_m, bool has_d) {
-  const double alt = nout <= 4 ? 130.0 + 57.0 * nout : 235.0 + 33.9 * nout;
-  const double m = has_m ? fdm_cost(nout, nrs) : 1e30;
-  const double d = has_d ? fdd_cost(nout) : 1e30;
-  // the syndrome-row decoder only with a 15 % margin over the derivative: a batch split between
-  // the two runs two smaller launches (24 random erasures: 0.854 ms split 34/66 by the bare
-  // costs, 0.797 all on the derivative)
-  if (m < alt && m < 0.85 * d) return kFdM;
-  if (d < alt) return kFdD;
-  return kFdNone;
-}
-
 int fdd_form(const cec_codec* c) {
   switch (c->opts.ct_variant) {
     case 70: return 1;
@@ -722,7 +696,8 @@ int use_fftdec(const cec_codec* c, const Program& p) {
     return kFdNone;
   if (c->fftdec_mode == 1) return p.fd ? kFdM : kFdNone;
   if (c->fftdec_mode == 2) return p.fdd ? kFdD : kFdNone;
-  return fftdec_choice(p.nout, p.fd_nrs, p.fd != nullptr, p.fdd != nullptr);
+  return cec::fftdec_choice(p.nout, p.fd_nrs, cec::fftdec_big(p.fd_nrs), p.fd != nullptr,
+                            p.fdd != nullptr);
 }
 
 int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* seg_list,
@@ -837,20 +812,18 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
   // launch than all-derivative. Fold the syndrome-row groups into the derivative launch when the
   // whole batch is cheaper that way (costs per segment scaled from 64 x 512 KiB).
   if (!fdg[4].empty() && c->fftdec_mode == 0) {
-    const double scale = (double)shard_len / (512.0 * 1024.0) / 64.0;
-    double delta = 0;  // all-derivative minus split
+    std::vector<cec::FdmGroup> mg;
     int mlaunches = 0;
-    bool movable = true;
     for (int cls = 0; cls < 4; ++cls) {
       if (fdg[cls].empty()) continue;
       ++mlaunches;
       for (auto& pr : fdg[cls]) {
         const Program& q = *pr.first;
-        movable &= q.fdd != nullptr;
-        delta += pr.second->size() * scale * (fdd_cost(q.nout) - fdm_cost(q.nout, q.fd_nrs));
+        mg.push_back({pr.second->size(), q.nout, q.fd_nrs, cec::fftdec_big(q.fd_nrs),
+                      q.fdd != nullptr});
       }
     }
-    if (mlaunches && movable && delta < kSplitLaunchUs * mlaunches) {
+    if (cec::fftdec_fold(mg, mlaunches, shard_len)) {
       for (int cls = 0; cls < 4; ++cls) {
         for (auto& pr : fdg[cls]) fdg[4].push_back(pr);
         fdg[cls].clear();

@@ -167,6 +167,65 @@ def test_fftdec_plans_model(tmp_path):
     assert "0 failures; mode D:" in r.stdout and r.stdout.strip().endswith(" 0 failures")
 
 
+def _chooser_lines(exe, batches):
+    """Run tests/native/fftdec_chooser.cpp over [(present [nseg][64], shard_len)]."""
+    text = []
+    for present, shard_len in batches:
+        text.append(f"{len(present)} {shard_len}")
+        text += ["".join("1" if f else "0" for f in row) for row in present]
+    r = subprocess.run([exe], input="\n".join(text) + "\n", capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = []
+    for line in r.stdout.splitlines():
+        tok = line.split()
+        out.append(dict(zip(tok[::2], map(float, tok[1::2]))))
+    assert len(out) == len(batches)
+    return out
+
+
+def test_fftdec_chooser_on_recorded_costs(tmp_path):
+    """The RS(32,32) decoder chooser (cess_amd/csrc/fftdec_cost.h, the rule cess_ec.cpp applies
+    per pattern and per batch) replayed on CPU over bench.py's config-6 patterns against the warm
+    sweep recorded on the MI355X (tests/golden/fftdec_sweep_r04.json, from
+    profiles/r04/c6_sweep_warm30.jsonl by tools/fftdec_sweep_golden.py): its split matches the one
+    the library ran, the batch it picks never loses to the best single decoder by more than the
+    run-to-run noise, and its cost model predicts every all-on-one-decoder leg."""
+    import json
+    import bench
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "fftdec_sweep_r04.json")))
+    exe = str(tmp_path / "fftdec_chooser")
+    subprocess.run(["g++", "-std=c++20", "-O1", "-fconstexpr-ops-limit=2000000000",
+                    os.path.join(ROOT, "tests", "native", "fftdec_chooser.cpp"), "-o", exe],
+                   check=True)
+    nseg, flen = gold["segments"], gold["fragment_bytes"]
+    es = sorted(map(int, gold["ms"]))
+    got = _chooser_lines(exe, [(bench.erasure_patterns(32, 32, nseg, e, seed=6), flen)
+                               for e in es])
+    for e, g in zip(es, got):
+        rec = gold["ms"][str(e)]
+        us = {leg: rec[leg] * 1e3 for leg in ("m", "d", "rt", "auto")}
+        # the choice is the one the library made in the recorded run (its kernel label)
+        label = rec["auto_kernel"]
+        if label == "k_fftdec_m":
+            assert g["m"] == nseg, (e, g)
+        elif label == "k_fftdec_d":
+            assert g["d"] == nseg, (e, g)
+        else:
+            pm, pd = map(int, re.findall(r"\((\d+)%", label)[:2])
+            assert (round(100 * g["m"] / nseg), round(100 * g["d"] / nseg)) == (pm, pd), (e, g)
+        # ... and never loses to the best single decoder (1.5 % = the sweep's run-to-run spread:
+        # the auto and all-derivative legs of one assignment differ by up to 0.9 %)
+        best = min(us["m"], us["d"], us["rt"])
+        assert us["auto"] <= 1.015 * best, (e, us)
+        # the model behind it: every single-decoder leg within 3 % in the band where the choice
+        # is close (16..32 erasures), within 10 % below it; the chosen split within 5 %
+        tol = 0.03 if e >= 16 else 0.10
+        for leg, key in (("m", "cost_m"), ("d", "cost_d"), ("rt", "cost_rt")):
+            assert abs(g[key] - us[leg]) <= tol * us[leg], (e, leg, g[key], us[leg])
+        assert abs(g["cost_chosen"] - us["auto"]) <= 0.05 * us["auto"], (e, g, us)
+
+
 @pytest.mark.parametrize("k,flen", [(2, 4096), (2, 1000), (3, 64), (1, 77)])
 def test_segment_hash_shares_fragment0_stream(k, flen):
     """The host path hashes fragment 0 once for both its own hash and the segment's
