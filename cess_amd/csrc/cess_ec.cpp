@@ -21,6 +21,7 @@
 #include <deque>
 #include <list>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -212,10 +213,48 @@ using ProgPtr = std::shared_ptr<const Program>;
 // per plan: an upload from pinned memory is a DMA enqueue, one from pageable memory is staged by
 // the runtime (measured: 64 new RS(32,32) patterns per call cost ~0.9 ms of host time beyond the
 // kernel with pageable images). Blocks of >= 1 MiB, kept for reuse; reset() after the sync.
+// hipHostFree, like hipFree, synchronises the whole device, so destroying a codec must not free
+// its arena's blocks: they go to this process-wide cache (up to kCap bytes) for the next arena.
+// The cache is never destroyed (the HIP runtime may be gone by the time static destructors run).
+struct PinnedCache {
+  static constexpr size_t kCap = size_t(64) << 20;
+  std::mutex mu;
+  std::vector<std::pair<uint8_t*, size_t>> blocks;
+  size_t bytes = 0;
+  static PinnedCache& get() {
+    static PinnedCache* c = new PinnedCache;
+    return *c;
+  }
+  // a cached block of at least `need` bytes (the smallest), or {nullptr, 0}
+  std::pair<uint8_t*, size_t> take(size_t need) {
+    std::lock_guard<std::mutex> g(mu);
+    size_t best = blocks.size();
+    for (size_t i = 0; i < blocks.size(); ++i)
+      if (blocks[i].second >= need && (best == blocks.size() || blocks[i].second < blocks[best].second))
+        best = i;
+    if (best == blocks.size()) return {nullptr, 0};
+    auto b = blocks[best];
+    blocks.erase(blocks.begin() + best);
+    bytes -= b.second;
+    return b;
+  }
+  void give(uint8_t* p, size_t cap) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (bytes + cap <= kCap) {
+        blocks.push_back({p, cap});
+        bytes += cap;
+        return;
+      }
+    }
+    (void)hipHostFree(p);  // past the cap: the rare device-wide synchronisation
+  }
+};
+
 class PinnedArena {
  public:
   ~PinnedArena() {
-    for (auto& b : blocks_) (void)hipHostFree(b.p);
+    for (auto& b : blocks_) PinnedCache::get().give(b.p, b.cap);
   }
   // `bytes` of zeroed page-locked memory valid until reset(), or nullptr (caller falls back)
   uint32_t* take(size_t bytes) {
@@ -224,8 +263,14 @@ class PinnedArena {
       if (blocks_[cur_].used + bytes <= blocks_[cur_].cap) break;
     if (cur_ == blocks_.size()) {
       Block b{nullptr, std::max(bytes, size_t(1) << 20), 0};
-      if (hipHostMalloc(reinterpret_cast<void**>(&b.p), b.cap, hipHostMallocDefault) != hipSuccess)
+      auto cached = PinnedCache::get().take(b.cap);
+      if (cached.first) {
+        b.p = cached.first;
+        b.cap = cached.second;
+      } else if (hipHostMalloc(reinterpret_cast<void**>(&b.p), b.cap, hipHostMallocDefault) !=
+                 hipSuccess) {
         return nullptr;
+      }
       blocks_.push_back(b);
     }
     Block& b = blocks_[cur_];

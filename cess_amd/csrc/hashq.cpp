@@ -77,7 +77,11 @@ int cec_hashq_create(int device, size_t capacity, void* hip_stream, cec_hashq** 
   q->device = device;
   q->stream = reinterpret_cast<hipStream_t>(hip_stream);
   q->cap = (uint32_t)capacity;
-  hipError_t e = hipMalloc(&q->tab, capacity * sizeof(cec::ShaChain));
+  // stream-ordered (hipFree would synchronise the whole device at destroy): every use of the
+  // table is a launch on q->stream
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&q->tab),
+                                capacity * sizeof(cec::ShaChain), q->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(q->stream);
   if (e != hipSuccess) {
     delete q;
     return cec::set_error(CEC_ENOMEM, std::string("hashq table: ") + hipGetErrorString(e));
@@ -89,9 +93,8 @@ int cec_hashq_create(int device, size_t capacity, void* hip_stream, cec_hashq** 
 void cec_hashq_destroy(cec_hashq* q) {
   if (!q) return;
   (void)hipSetDevice(q->device);
-  // launches still queued on the stream read the table
-  (void)hipStreamSynchronize(q->stream);
-  (void)hipFree(q->tab);
+  // freed in stream order, after the launches still queued on the stream that read the table
+  (void)hipFreeAsync(q->tab, q->stream);
   delete q;
 }
 

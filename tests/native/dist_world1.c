@@ -103,10 +103,12 @@ static uint32_t xt4(uint32_t x) {
   return ((x & 0x7F7F7F7Fu) << 1) ^ ((hi >> 7) * 0x1Du);
 }
 
-/* Destroying a dist handle (and then its codec) while another codec's long batch is still
- * running on a side stream: the side work must complete bit-exact (RS(2,1) parity p = 3 d0 ^ 2 d1
- * recomputed on the host), and the handle's destruction waits for its own work only. Prints
- * whether the side stream was still busy right after each destroy (1: not drained by it). */
+/* Destroying a codec, then a dist handle and its codec, each while another codec's long batch
+ * (~25 ms) is still running on a side stream: the side work must complete bit-exact (RS(2,1)
+ * parity p = 3 d0 ^ 2 d1 recomputed on the host), and a destruction should wait for its own
+ * work only. Prints whether the side stream was still busy right after each destroy (1: not
+ * drained by it; 0 after the dist destroy can come from RCCL's ncclCommDestroy, whose internal
+ * synchronisation is not ours). */
 static int destroy_under_load(void) {
   const size_t F = (size_t)8 << 20, nseg = 16;
   const int reps = 400;
@@ -140,16 +142,53 @@ static int destroy_under_load(void) {
   CHECK(cec_dist_unique_id(id) == CEC_OK);
   CHECK(cec_dist_create(c, id, 1, 0, &d) == CEC_OK);
   CHECK(cec_dist_degraded_read(d, seg, frag, nd, Fd, locate, &st, out, NULL, NULL) == CEC_OK);
-  /* a long batch on the side stream, then the destroys while it runs */
-  for (int r = 0; r < reps; ++r)
-    CHECK(cec_encode_batch(side_codec, d_data, d_par, nseg, F, side) == CEC_OK);
-  cec_dist_destroy(d);
-  const int busy_dist = hipStreamQuery(side) == hipErrorNotReady;
-  cec_destroy(c);
-  const int busy_codec = hipStreamQuery(side) == hipErrorNotReady;
-  CHECK(hipStreamSynchronize(side) == hipSuccess);
-  printf("side stream busy after dist destroy: %d, after codec destroy: %d\n", busy_dist,
-         busy_codec);
+  /* a codec that used the host API (stage) and the pool (a per-segment rebuild's plan) */
+  cec_codec* lone = NULL;
+  CHECK(cec_create(4, 2, 0, &lone) == CEC_OK);
+  {
+    uint8_t* hs[6];
+    uint8_t pres[6] = {1, 0, 1, 1, 1, 1};
+    for (int i = 0; i < 6; ++i) {
+      hs[i] = malloc(4096);
+      CHECK(hs[i] != NULL);
+      memset(hs[i], i * 7 + 1, 4096);
+    }
+    CHECK(cec_encode(lone, hs, 4096) == CEC_OK);
+    CHECK(cec_reconstruct(lone, hs, pres, 4096, 0) == CEC_OK);
+    for (int i = 0; i < 6; ++i) free(hs[i]);
+    uint8_t bp[6 * 6];
+    for (size_t s = 0; s < nd * 6; ++s) bp[s] = (s % 6) != (s / 6) % 6;
+    CHECK(cec_reconstruct_batch(lone, st.d_data, st.d_par, nd, Fd, bp, 0, 0, NULL) == CEC_OK);
+    CHECK(hipDeviceSynchronize() == hipSuccess);
+  }
+  hipEvent_t t0, t1;
+  CHECK(hipEventCreate(&t0) == hipSuccess && hipEventCreate(&t1) == hipSuccess);
+  /* a long batch on the side stream, then a destroy while it runs: the lone codec first, then
+   * (a second batch) the dist handle and its codec */
+  int busy[3];
+  float ms[2];
+  for (int phase = 0; phase < 2; ++phase) {
+    CHECK(hipEventRecord(t0, side) == hipSuccess);
+    for (int r = 0; r < reps; ++r)
+      CHECK(cec_encode_batch(side_codec, d_data, d_par, nseg, F, side) == CEC_OK);
+    CHECK(hipEventRecord(t1, side) == hipSuccess);
+    if (phase == 0) {
+      cec_destroy(lone);
+      busy[0] = hipStreamQuery(side) == hipErrorNotReady;
+    } else {
+      cec_dist_destroy(d);
+      busy[1] = hipStreamQuery(side) == hipErrorNotReady;
+      cec_destroy(c);
+      busy[2] = hipStreamQuery(side) == hipErrorNotReady;
+    }
+    CHECK(hipStreamSynchronize(side) == hipSuccess);
+    CHECK(hipEventElapsedTime(&ms[phase], t0, t1) == hipSuccess);
+  }
+  printf("side stream busy after codec destroy: %d (batch %.1f ms); after dist destroy: %d, after "
+         "its codec's destroy: %d (batch %.1f ms)\n",
+         busy[0], ms[0], busy[1], busy[2], ms[1]);
+  (void)hipEventDestroy(t0);
+  (void)hipEventDestroy(t1);
   /* the side work is complete and bit-exact */
   uint32_t* h = malloc(nseg * 3 * F);
   CHECK(h != NULL);
