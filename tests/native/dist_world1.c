@@ -8,6 +8,7 @@
  * build: gcc -O2 -D__HIP_PLATFORM_AMD__ tests/native/dist_world1.c -Iinclude -I/opt/rocm/include
  *            -Lcess_amd -lcessec -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,... -o dist_world1 */
 #include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -165,16 +166,30 @@ static int destroy_under_load(void) {
   CHECK(hipEventCreate(&t0) == hipSuccess && hipEventCreate(&t1) == hipSuccess);
   /* a long batch on the side stream, then a destroy while it runs: the lone codec first, then
    * (a second batch) the dist handle and its codec */
-  int busy[3];
-  float ms[2];
-  for (int phase = 0; phase < 2; ++phase) {
-    CHECK(hipEventRecord(t0, side) == hipSuccess);
-    for (int r = 0; r < reps; ++r)
-      CHECK(cec_encode_batch(side_codec, d_data, d_par, nseg, F, side) == CEC_OK);
-    CHECK(hipEventRecord(t1, side) == hipSuccess);
+  int busy[4];
+  float ms[3];
+  for (int phase = 0; phase < 3; ++phase) {
+    if (phase < 2) {
+      CHECK(hipEventRecord(t0, side) == hipSuccess);
+      for (int r = 0; r < reps; ++r)
+        CHECK(cec_encode_batch(side_codec, d_data, d_par, nseg, F, side) == CEC_OK);
+      CHECK(hipEventRecord(t1, side) == hipSuccess);
+    }
     if (phase == 0) {
       cec_destroy(lone);
       busy[0] = hipStreamQuery(side) == hipErrorNotReady;
+    } else if (phase == 2) {
+      /* control: RCCL's own communicator teardown, no libcessec involved */
+      ncclUniqueId uid;
+      ncclComm_t comm;
+      CHECK(ncclGetUniqueId(&uid) == ncclSuccess);
+      CHECK(ncclCommInitRank(&comm, 1, uid, 0) == ncclSuccess);
+      CHECK(hipEventRecord(t0, side) == hipSuccess);
+      for (int r = 0; r < reps; ++r)
+        CHECK(cec_encode_batch(side_codec, d_data, d_par, nseg, F, side) == CEC_OK);
+      CHECK(hipEventRecord(t1, side) == hipSuccess);
+      (void)ncclCommDestroy(comm);
+      busy[3] = hipStreamQuery(side) == hipErrorNotReady;
     } else {
       cec_dist_destroy(d);
       busy[1] = hipStreamQuery(side) == hipErrorNotReady;
@@ -185,8 +200,8 @@ static int destroy_under_load(void) {
     CHECK(hipEventElapsedTime(&ms[phase], t0, t1) == hipSuccess);
   }
   printf("side stream busy after codec destroy: %d (batch %.1f ms); after dist destroy: %d, after "
-         "its codec's destroy: %d (batch %.1f ms)\n",
-         busy[0], ms[0], busy[1], busy[2], ms[1]);
+         "its codec's destroy: %d (batch %.1f ms); after a bare ncclCommDestroy: %d (batch %.1f ms)\n",
+         busy[0], ms[0], busy[1], busy[2], ms[1], busy[3], ms[2]);
   (void)hipEventDestroy(t0);
   (void)hipEventDestroy(t1);
   /* the side work is complete and bit-exact */

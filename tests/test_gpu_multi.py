@@ -281,14 +281,18 @@ def test_c_dist_from_c(tmp_path):
     exe = tmp_path / "dist_world1"
     subprocess.run(["gcc", "-O2", "-D__HIP_PLATFORM_AMD__", f"{ROOT}/tests/native/dist_world1.c",
                     f"-I{ROOT}/include", "-I/opt/rocm/include", f"-L{ROOT}/cess_amd", "-lcessec",
-                    "-L/opt/rocm/lib", "-lamdhip64",
+                    "-L/opt/rocm/lib", "-lamdhip64", "-lrccl",
                     f"-Wl,-rpath,{ROOT}/cess_amd:/opt/rocm/lib", "-o", str(exe)], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
     assert "dist world1 ok" in r.stdout
-    # destroy_under_load: a dist handle and its codec destroyed while another codec's batch ran
-    # on a side stream (that batch then checked bit-exact); whether the side stream was still
-    # running right after each destroy is reported (1 = the destroy did not drain the device)
+    # destroy_under_load: a codec, then a dist handle and its codec, destroyed while another
+    # codec's ~25 ms batch ran on a side stream (that batch then checked bit-exact); whether the
+    # side stream was still running right after each destroy is reported (1 = the destroy did not
+    # drain the device), with a bare ncclCommDestroy as the control for the dist handle's
     busy = [ln for ln in r.stdout.splitlines() if ln.startswith("side stream busy")]
     assert busy, r.stdout
     print(busy[0])
+    # a codec's teardown waits for its own stream only (r04: stream-ordered frees, pinned blocks
+    # cached instead of hipHostFree)
+    assert busy[0].startswith("side stream busy after codec destroy: 1"), busy[0]
