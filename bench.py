@@ -389,6 +389,61 @@ def launch_ranks(n: int, argv) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def cabi_legs(ex_out, gather_leg, degraded_gather, enc, code, world, rank, dev, deadline,
+              emit):
+    """The degraded read through libcessec's own RCCL communicator (cec_dist_*, the C ABI a Go /
+    Rust host uses) at world > 1, on the same placement as the torch legs: RS(2,1) survivors and
+    RS(32,32) both exchanges. They run last, after every other measurement, under a watchdog: a
+    rank that fails or stalls inside the collective exchange would otherwise hold every rank in
+    it, so past `deadline` seconds each rank records the legs as not finished, rank 0 prints the
+    line it has (`emit`), and the process ends (os._exit: the peers are stuck in RCCL)."""
+    import threading
+    import torch
+    import torch.distributed as dist
+    import cess_amd
+    k, m, F = code
+    done = threading.Event()
+    legs = ("degraded_gather_cabi", "wide_degraded_gather_cabi")
+
+    def watchdog():
+        if done.wait(deadline):
+            return
+        for name in legs:
+            if name not in ex_out:
+                ex_out[name] = {"error": f"not finished after {deadline:.0f} s (a rank failed or "
+                                         "stalled inside the cec_dist exchange)"}
+        emit()
+        os._exit(0)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    transport = "libcessec cec_dist_degraded_read (own RCCL communicator)"
+    try:
+        leg = gather_leg(degraded_gather(enc, k, m, F, world, rank, dev, 64, "survivors", "cabi"))
+        leg["transport"] = transport
+        ex_out[legs[0]] = leg
+        wk, wm, wF = CONFIGS[5][:3]
+        wenc = cess_amd.New(wk, wm, device=dev.index)
+        wide = {}
+        for ex in ("survivors", "partials"):
+            wide[ex] = gather_leg(degraded_gather(wenc, wk, wm, wF, world, rank, dev, 32, ex,
+                                                  "cabi"), code=(wk, wF))
+            wide[ex]["transport"] = transport
+        ex_out[legs[1]] = wide
+        wenc.close()
+    except Exception as e:  # noqa: BLE001 - reported in the line
+        ok = 0
+        for name in legs:
+            ex_out.setdefault(name, {"error": f"{type(e).__name__}: {e}"})
+    else:
+        ok = 1
+    # every rank that got here agrees (cec_dist fails a caller error on all ranks alike); a rank
+    # stuck in the exchange never arrives, and the watchdog then ends the ones waiting here
+    if world > 1:
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    done.set()
+
+
 def erasure_patterns(k: int, m: int, nseg: int, ne: int, seed: int,
                      lose_parity: bool = False) -> np.ndarray:
     """Configs 6 / 7: [nseg][k + m] present flags, ne random erasures per segment (or every
@@ -675,6 +730,8 @@ def line_problems(out: dict) -> list:
             elif "skipped" in leg:
                 if "cabi" not in name:
                     bad.append(f"extra.{name} skipped")
+            elif "error" in leg:
+                bad.append(f"extra.{name}: {leg['error']}")
             elif leg.get("bit_exact") is not True:
                 bad.append(f"extra.{name} not bit-exact")
     return bad
@@ -719,6 +776,9 @@ def main() -> None:
                     help="RS(32,32) rebuilds: 0 = the cost model's pick of the FFT-domain decoders "
                          "and k_rthx (library default), 1 = always the syndrome-row decoder, "
                          "2 = always the formal-derivative decoder (CEC_OPT_FFTDEC_MODE)")
+    ap.add_argument("--cabi-deadline", type=float, default=240.0,
+                    help="world > 1: seconds the C-ABI (cec_dist) exchange legs may take before "
+                         "the line is printed without them")
     ap.add_argument("--erasures", type=int, default=0,
                     help="config 6: random erasures per segment (default m)")
     ap.add_argument("--lose-parity", action="store_true",
@@ -1070,6 +1130,7 @@ def main() -> None:
                 "backend": (backend if world > 1 else "local (one GPU: no bytes move)"),
                 "bit_exact": not bad}
 
+    cabi_pending = False
     if args.config == 4:
         out["degraded_gather"] = gather_leg(gather)
     elif world > 1 and not args.no_extra and args.config == 2:
@@ -1088,6 +1149,7 @@ def main() -> None:
             ex: gather_leg(degraded_gather(wenc, wk, wm, wF, world, rank, dev, 32, ex),
                            code=(wk, wF))
             for ex in ("survivors", "partials")}
+        wenc.close()
         if "CESS_DEVICE" in os.environ:
             # ranks sharing one GPU (the one-GPU rehearsal): RCCL refuses a communicator with
             # two ranks on one device ("Duplicate GPU detected"), so the C-ABI group cannot form
@@ -1096,16 +1158,7 @@ def main() -> None:
             ex_out["degraded_gather_cabi"] = {"skipped": why}
             ex_out["wide_degraded_gather_cabi"] = {"skipped": why}
         else:
-            ex_out["degraded_gather_cabi"] = gather_leg(
-                degraded_gather(enc, k, m, F, world, rank, dev, 64, "survivors", "cabi"))
-            ex_out["wide_degraded_gather_cabi"] = {
-                ex: gather_leg(degraded_gather(wenc, wk, wm, wF, world, rank, dev, 32, ex,
-                                               "cabi"), code=(wk, wF))
-                for ex in ("survivors", "partials")}
-            for leg_ in [ex_out["degraded_gather_cabi"],
-                         *ex_out["wide_degraded_gather_cabi"].values()]:
-                leg_["transport"] = "libcessec cec_dist_degraded_read (own RCCL communicator)"
-        wenc.close()
+            cabi_pending = True  # run last, under a deadline (cabi_legs below)
 
     if not args.no_extra and args.config == 2:
         # decode rate in the same process (BASELINE config 3 workload, same bytes)
@@ -1156,6 +1209,11 @@ def main() -> None:
         out["cpu_baseline"]["node_GBps_gpu"] = out["value"]
         if args.config == 5:
             out["cpu_baseline"]["sha256"] = cpu_sha256(k, m, F, args.cpu_seconds / 2)
+
+    if cabi_pending:
+        cabi_legs(out["extra"], gather_leg, degraded_gather, enc, (k, m, F), world, rank, dev,
+                  args.cabi_deadline, lambda: print(json.dumps(out), flush=True) if rank == 0
+                  else None)
 
     if world > 1:
         dist.barrier()

@@ -1,5 +1,6 @@
 """bench.py's `--gpus N` contract (CPU): N ranks or a non-zero exit, never a silent one-GPU line.
 The driver's multi-GPU scaling run is `bench.py --gpus N` (under torchrun or alone)."""
+import json
 import os
 import subprocess
 import sys
@@ -142,3 +143,46 @@ def test_recorded_lines_have_every_key(name):
         assert ex["degraded_gather"]["bit_exact"] and ex["degraded_gather"]["backend"] == "gloo"
         assert all(ex["wide_degraded_gather"][x]["bit_exact"] for x in ("survivors", "partials"))
         assert "RCCL refuses" in ex["degraded_gather_cabi"]["skipped"]
+
+
+def test_cabi_legs_watchdog_ends_a_stalled_exchange(tmp_path):
+    """bench.cabi_legs (the C-ABI exchange legs of the N > 1 line, run last): an exchange that
+    never returns (a peer stuck in RCCL) does not cost the line. Past the deadline the legs are
+    recorded as not finished, the line is printed, and the process exits 0."""
+    import subprocess
+    import sys
+    script = tmp_path / "stall.py"
+    script.write_text(
+        "import json, sys, time\n"
+        f"sys.path.insert(0, {str(ROOT)!r})\n"
+        "import torch\n"
+        "import bench\n"
+        "out = {'extra': {}}\n"
+        "def stall(*a, **k):\n"
+        "    time.sleep(3600)\n"
+        "bench.cabi_legs(out['extra'], lambda g, **k: g, stall, None, (2, 1, 4096), 1, 0,\n"
+        "                torch.device('cpu'), 2.0, lambda: print(json.dumps(out), flush=True))\n"
+        "print('not reached')\n")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and "not reached" not in r.stdout, r.stdout
+    ex = json.loads(lines[0])["extra"]
+    for name in ("degraded_gather_cabi", "wide_degraded_gather_cabi"):
+        assert "not finished after 2 s" in ex[name]["error"], ex
+
+
+def test_cabi_legs_error_is_reported():
+    """An exchange leg that raises is recorded as an error in the line (and flagged by
+    line_problems), not a crash."""
+    import torch
+    ex = {}
+
+    def boom(*a, **k):
+        raise RuntimeError("cec_dist_create: no RCCL")
+
+    bench.cabi_legs(ex, lambda g, **k: g, boom, None, (2, 1, 4096), 1, 0, torch.device("cpu"),
+                    30.0, lambda: None)
+    assert ex["degraded_gather_cabi"]["error"] == "RuntimeError: cec_dist_create: no RCCL"
+    line = {"config": {"baseline_config": 2}, "n_gpus": 2, "extra": ex}
+    assert any("cec_dist_create: no RCCL" in p for p in bench.line_problems(line))
