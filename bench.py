@@ -408,12 +408,14 @@ def cabi_legs(ex_out, gather_leg, degraded_gather, enc, code, world, rank, dev, 
     def watchdog():
         if done.wait(deadline):
             return
-        for name in legs:
-            if name not in ex_out:
-                ex_out[name] = {"error": f"not finished after {deadline:.0f} s (a rank failed or "
-                                         "stalled inside the cec_dist exchange)"}
-        emit()
-        os._exit(0)
+        try:
+            for name in legs:
+                if name not in ex_out:
+                    ex_out[name] = {"error": f"not finished after {deadline:.0f} s (a rank failed "
+                                             "or stalled inside the cec_dist exchange)"}
+            emit()
+        finally:
+            os._exit(0)
 
     threading.Thread(target=watchdog, daemon=True).start()
     transport = "libcessec cec_dist_degraded_read (own RCCL communicator)"
