@@ -216,45 +216,52 @@ using ProgPtr = std::shared_ptr<const Program>;
 // hipHostFree, like hipFree, synchronises the whole device, so destroying a codec must not free
 // its arena's blocks: they go to this process-wide cache (up to kCap bytes) for the next arena.
 // The cache is never destroyed (the HIP runtime may be gone by the time static destructors run).
+// Blocks are reused on the device they were allocated under only.
 struct PinnedCache {
   static constexpr size_t kCap = size_t(64) << 20;
+  struct Block {
+    uint8_t* p;
+    size_t cap;
+    int device;
+  };
   std::mutex mu;
-  std::vector<std::pair<uint8_t*, size_t>> blocks;
+  std::vector<Block> blocks;
   size_t bytes = 0;
   static PinnedCache& get() {
     static PinnedCache* c = new PinnedCache;
     return *c;
   }
-  // a cached block of at least `need` bytes (the smallest), or {nullptr, 0}
-  std::pair<uint8_t*, size_t> take(size_t need) {
+  // a cached block of at least `need` bytes of `device` (the smallest), or {nullptr, 0, device}
+  Block take(size_t need, int device) {
     std::lock_guard<std::mutex> g(mu);
     size_t best = blocks.size();
     for (size_t i = 0; i < blocks.size(); ++i)
-      if (blocks[i].second >= need && (best == blocks.size() || blocks[i].second < blocks[best].second))
+      if (blocks[i].device == device && blocks[i].cap >= need &&
+          (best == blocks.size() || blocks[i].cap < blocks[best].cap))
         best = i;
-    if (best == blocks.size()) return {nullptr, 0};
-    auto b = blocks[best];
+    if (best == blocks.size()) return {nullptr, 0, device};
+    const Block b = blocks[best];
     blocks.erase(blocks.begin() + best);
-    bytes -= b.second;
+    bytes -= b.cap;
     return b;
   }
-  void give(uint8_t* p, size_t cap) {
+  void give(const Block& b) {
     {
       std::lock_guard<std::mutex> g(mu);
-      if (bytes + cap <= kCap) {
-        blocks.push_back({p, cap});
-        bytes += cap;
+      if (bytes + b.cap <= kCap) {
+        blocks.push_back(b);
+        bytes += b.cap;
         return;
       }
     }
-    (void)hipHostFree(p);  // past the cap: the rare device-wide synchronisation
+    (void)hipHostFree(b.p);  // past the cap: the rare device-wide synchronisation
   }
 };
 
 class PinnedArena {
  public:
   ~PinnedArena() {
-    for (auto& b : blocks_) PinnedCache::get().give(b.p, b.cap);
+    for (auto& b : blocks_) PinnedCache::get().give({b.p, b.cap, device_});
   }
   // `bytes` of zeroed page-locked memory valid until reset(), or nullptr (caller falls back)
   uint32_t* take(size_t bytes) {
@@ -263,10 +270,11 @@ class PinnedArena {
       if (blocks_[cur_].used + bytes <= blocks_[cur_].cap) break;
     if (cur_ == blocks_.size()) {
       Block b{nullptr, std::max(bytes, size_t(1) << 20), 0};
-      auto cached = PinnedCache::get().take(b.cap);
-      if (cached.first) {
-        b.p = cached.first;
-        b.cap = cached.second;
+      if (blocks_.empty() && hipGetDevice(&device_) != hipSuccess) return nullptr;
+      const PinnedCache::Block cached = PinnedCache::get().take(b.cap, device_);
+      if (cached.p) {
+        b.p = cached.p;
+        b.cap = cached.cap;
       } else if (hipHostMalloc(reinterpret_cast<void**>(&b.p), b.cap, hipHostMallocDefault) !=
                  hipSuccess) {
         return nullptr;
@@ -292,6 +300,7 @@ class PinnedArena {
   };
   std::vector<Block> blocks_;
   size_t cur_ = 0;
+  int device_ = -1;  // the device current when the first block was taken (the codec's)
 };
 
 // With `keep`, the images are written into that arena and the uploads are left in flight: the
