@@ -736,11 +736,23 @@ using cec::kFdM;
 using cec::kFdNone;
 
 // tuning build: CEC_OPT_CT_VARIANT 70 runs the pipelined persistent k_fftdec_dp instead of the
-// one-block-per-wave k_fftdec_d, 72 the same with wave priorities (A/B sweeps)
+// one-block-per-wave k_fftdec_d, 72 the same with wave priorities, 73 k_fftdec_d with its quad
+// exchanges through the LDS crossbar, 74..78 that in some phases only: the derivative, IFFT +
+// derivative, the FFT tail, the IFFT, derivative + tail (A/B sweeps)
+// tuning build: CEC_OPT_CT_VARIANT 79 runs k_fftdec_m with its IFFT's cross-lane exchanges through
+// the LDS crossbar
+int fdm_form(const cec_codec* c) { return c->opts.ct_variant == 79 ? 1 : 0; }
+
 int fdd_form(const cec_codec* c) {
   switch (c->opts.ct_variant) {
     case 70: return 1;
     case 72: return 3;
+    case 73: return 4;
+    case 74: return 5;
+    case 75: return 6;
+    case 76: return 7;
+    case 77: return 8;
+    case 78: return 9;
     default: return 0;
   }
 }
@@ -761,7 +773,7 @@ int do_decode(cec_codec* c, const Program& p, const Layout& L, const uint32_t* s
     return do_encode(c, L, seg_list, nseg, st);
   const int fk = use_fftdec(c, p);
   if ((fk == kFdM && cec::launch_fftdec(L, p.fd_side, cec::fftdec_big(p.fd_nrs), p.fd, nullptr,
-                                        seg_list, nseg, st)) ||
+                                        seg_list, nseg, st, fdm_form(c))) ||
       (fk == kFdD && cec::launch_fftdec_d(L, p.fdd, nullptr, seg_list, nseg, st, fdd_form(c)))) {
     c->fd_segments += nseg;
     if (fk == kFdD) c->fdd_segments += nseg;
@@ -991,7 +1003,8 @@ int launch_ps_plan(cec_codec* c, const PsPlan& p, const Layout& L, hipStream_t s
     const bool ok = f.side == 2 ? cec::launch_fftdec_d(L, nullptr, ptrs + f.off, p.list + f.off,
                                                        (uint32_t)f.count, st, fdd_form(c))
                                 : cec::launch_fftdec(L, f.side, f.big, nullptr, ptrs + f.off,
-                                                     p.list + f.off, (uint32_t)f.count, st);
+                                                     p.list + f.off, (uint32_t)f.count, st,
+                                                     fdm_form(c));
     if (!ok)
       return set_err(CEC_EINVAL, "FFT-domain decode plan on a layout it does not fit");
     c->fd_segments += f.count;

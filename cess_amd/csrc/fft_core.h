@@ -122,6 +122,13 @@ __device__ __forceinline__ uint32_t partner(uint32_t v) {
   // quad_perm [1, 0, 3, 2]: lane l reads lane l ^ 1
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);
 }
+// the same through the LDS crossbar (ds_swizzle, quad-permute mode) when SWZ: no VALU issue slot
+// (every DPP form issues at half rate on gfx950), LDS latency instead
+template <bool SWZ>
+__device__ __forceinline__ uint32_t partner_x(uint32_t v) {
+  if constexpr (SWZ) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x80B1);
+  else return partner(v);
+}
 
 template <bool NT>
 __device__ __forceinline__ void ld32(const uint8_t* p, uint32_t (&w)[8]) {
@@ -146,7 +153,7 @@ __device__ __forceinline__ void st32(uint8_t* p, const uint32_t (&w)[8]) {
 
 // IFFT over the coset BETA ^ {0..31}: values -> novel-basis coefficients. em = even-lane mask.
 // Layer i: b ^= a; a ^= s*b (i = 0 .. 4).
-template <unsigned BETA>
+template <unsigned BETA, bool SWZ = false>
 __device__ __forceinline__ void ifft32(uint32_t (&X)[16][8], uint32_t em) {
   using T = Skews<BETA>;
   // layer 0 (positions 2j, 2j + 1: across the lane pair). Z = a ^ b on both lanes; even lane ->
@@ -154,7 +161,7 @@ __device__ __forceinline__ void ifft32(uint32_t (&X)[16][8], uint32_t em) {
   sfor<16>([&](auto J) CEC_FFT_AI {
     constexpr unsigned s = T::s.s[0][J];
     uint32_t Z[8];
-    sfor<8>([&](auto Q) CEC_FFT_AI { Z[Q] = X[J][Q] ^ partner(X[J][Q]); });
+    sfor<8>([&](auto Q) CEC_FFT_AI { Z[Q] = X[J][Q] ^ partner_x<SWZ>(X[J][Q]); });
     if constexpr (s == 0) {
       sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] = FFT_BOP3(em, X[J][Q], Z[Q], kSel); });
     } else {

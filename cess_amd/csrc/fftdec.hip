@@ -90,7 +90,7 @@ constexpr int kSmallNr = 4;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef const __attribute__((address_space(3))) u32x4 lds_u32x4;
 
-template <unsigned SIDE, int NLO, int NHI, int LR>
+template <unsigned SIDE, int NLO, int NHI, int LR, bool SWZ>
 __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64_t col,
                                            cplan_t P, lds_u32* lw) {
   constexpr unsigned BA = SIDE ? 32u : 0u, BB = SIDE ? 0u : 32u;
@@ -125,7 +125,7 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
                                              soff, 0, 2);
   }
   sfor<16>([&](auto J) CEC_FFT_AI { tr8(X[J]); });
-  ifft32<BA>(X, em);
+  ifft32<BA, SWZ>(X, em);
   // q on coset B; its last layer only on the slots whose q is read (syndrome rows R, erased
   // outputs of B: the plan's kPslots, numbered before the swaps below)
   fft32_upper<BB>(X);
@@ -259,8 +259,9 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
 }
 
 // plans: per listed segment (y) its plan, or `plan1` for every segment. BIG: plans with more than
-// kSmallNr syndrome slots (the host sorts them, fftdec_big).
-template <unsigned SIDE, bool BIG>
+// kSmallNr syndrome slots (the host sorts them, fftdec_big). SWZ: the IFFT's cross-lane layer
+// exchanges through the LDS crossbar (tuning build, variant 79).
+template <unsigned SIDE, bool BIG, bool SWZ = false>
 __global__ __launch_bounds__(256) CEC_FD_ATTR void k_fftdec_m(Layout L, const uint32_t* __restrict__ plan1,
                                                   const uint32_t* const* __restrict__ plans,
                                                   const uint32_t* __restrict__ seg_list,
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(256) CEC_FD_ATTR void k_fftdec_m(Layout L, const ui
   const uint64_t col = (gp >> 5) * 1024 + (gp & 31) * 16;
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * LR * 512];
   if (col >= L.len) return;  // whole waves leave together
-  dec_m_cols<SIDE, NLO, NHI, LR>(L, seg, col, (cplan_t)P,
+  dec_m_cols<SIDE, NLO, NHI, LR, SWZ>(L, seg, col, (cplan_t)P,
                                  (lds_u32*)(lds + (threadIdx.x >> 6) * (LR * 512)));
 }
 
@@ -290,11 +291,18 @@ bool fftdec_layout_ok(const Layout& L) {
 
 bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
                    const uint32_t* const* plans, const uint32_t* seg_list, uint32_t nseg,
-                   hipStream_t st) {
+                   hipStream_t st, int form) {
   if (!fftdec_layout_ok(L) || (side != 0 && side != 1)) return false;
   const uint64_t gx = (L.len / 32 * 2 + 255) / 256;
   auto kern = side ? (big ? k_fftdec_m<1, true> : k_fftdec_m<1, false>)
                    : (big ? k_fftdec_m<0, true> : k_fftdec_m<0, false>);
+#ifdef CEC_TUNING
+  if (form == 1)
+    kern = side ? (big ? k_fftdec_m<1, true, true> : k_fftdec_m<1, false, true>)
+                : (big ? k_fftdec_m<0, true, true> : k_fftdec_m<0, false, true>);
+#else
+  (void)form;
+#endif
   for (uint32_t s0 = 0; s0 < nseg; s0 += 65535) {
     const uint32_t ny = nseg - s0 < 65535 ? nseg - s0 : 65535;
     hipLaunchKernelGGL(kern, dim3((unsigned)gx, ny), dim3(256), 0, st, L, plan1, plans, seg_list,

@@ -83,22 +83,21 @@ __device__ __forceinline__ void after_prev(uint32_t (&X)[16][8]) {
   if constexpr (J > 0) asm volatile("" : "+v"(X[J][0]) : "v"(X[J - 1][7]));
 }
 
-// quad partners: lane l reads lane l ^ 1 / l ^ 2
-// (DPP moves issue at half rate; -DCEC_FDD_SWZ moves them through the LDS crossbar instead:
-// ds_swizzle in quad-permute mode, no VALU issue slot, but measured slower: 0.94 vs 0.915 ms)
+// quad partners: lane l reads lane l ^ 1 / l ^ 2. SWZ = false: DPP quad_perm, folded by the
+// compiler into the consuming v_and / v_xor where it can; every DPP form (v_mov_b32_dpp and the
+// VOP2 ops with a DPP operand alike) issues at half rate on gfx950 (profiles/r04/
+// valu_bench_r04.jsonl), so the 768 exchanges per block are ~1,500 issue slots. SWZ = true (tuning
+// build, variant 73): ds_swizzle in quad-permute mode through the LDS crossbar, no VALU slot,
+// LDS latency instead.
+template <bool SWZ>
 __device__ __forceinline__ uint32_t qp1(uint32_t v) {
-#ifdef CEC_FDD_SWZ
-  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x80B1);
-#else
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);  // [1,0,3,2]
-#endif
+  if constexpr (SWZ) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x80B1);
+  else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);  // [1,0,3,2]
 }
+template <bool SWZ>
 __device__ __forceinline__ uint32_t qp2(uint32_t v) {
-#ifdef CEC_FDD_SWZ
-  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x804E);
-#else
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);  // [2,3,0,1]
-#endif
+  if constexpr (SWZ) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x804E);
+  else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);  // [2,3,0,1]
 }
 
 struct Skews64 {
@@ -179,6 +178,7 @@ __device__ __forceinline__ void mul_rt_lds(uint32_t (&x)[8], const lds_u32* mk) 
 
 // IFFT_64 (values -> coefficients), layer i: b ^= a; a ^= s*b. e1 / e2: lanes with bit 0 / bit 1
 // of l clear (the lower position of a layer-0 / layer-1 pair).
+template <bool SWZ>
 __device__ __forceinline__ void ifft64(uint32_t (&X)[16][8], uint32_t e1, uint32_t e2) {
   using S = Skews64;
   // layer 0 (lanes l, l ^ 1). Z = a ^ b on both lanes; lower -> a ^ s*Z, upper -> Z
@@ -187,7 +187,7 @@ __device__ __forceinline__ void ifft64(uint32_t (&X)[16][8], uint32_t e1, uint32
     static_assert(S::s.s[0][2 * J + 1] == (s ^ 2u), "layer-0 skew is linear in t");
     after_prev<J>(X);
     uint32_t Z[8];
-    sfor<8>([&](auto Q) CEC_FFT_AI { Z[Q] = X[J][Q] ^ qp1(X[J][Q]); });
+    sfor<8>([&](auto Q) CEC_FFT_AI { Z[Q] = X[J][Q] ^ qp1<SWZ>(X[J][Q]); });
     if constexpr (s == 0) {
       sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] ^= Z[Q]; });
     } else {
@@ -201,7 +201,7 @@ __device__ __forceinline__ void ifft64(uint32_t (&X)[16][8], uint32_t e1, uint32
     constexpr unsigned s = S::s.s[1][J];
     after_prev<J>(X);
     uint32_t Z[8];
-    sfor<8>([&](auto Q) CEC_FFT_AI { Z[Q] = X[J][Q] ^ qp2(X[J][Q]); });
+    sfor<8>([&](auto Q) CEC_FFT_AI { Z[Q] = X[J][Q] ^ qp2<SWZ>(X[J][Q]); });
     if constexpr (s == 0) {
       sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] = FFT_BOP3(e2, X[J][Q], Z[Q], kSel); });
     } else {
@@ -238,14 +238,14 @@ __device__ __forceinline__ void fft64_upper(uint32_t (&X)[16][8]) {
     });
   });
 }
-template <int J>
+template <int J, bool SWZ>
 __device__ __forceinline__ void fft64_tail(uint32_t (&x)[8], uint32_t e1, uint32_t e2) {
   using S = Skews64;
   {  // layer 1 (lanes l, l ^ 2). P = b on both lanes: lower -> a ^ s*P, upper -> b ^ a ^ s*P
     constexpr unsigned s = S::s.s[1][J];
     uint32_t P[8];
     sfor<8>([&](auto Q) CEC_FFT_AI {
-      const uint32_t y = qp2(x[Q]);
+      const uint32_t y = qp2<SWZ>(x[Q]);
       P[Q] = FFT_BOP3(e2, y, x[Q], kSel);
       x[Q] = FFT_BOP3(x[Q], y, e2, kXandN);
     });
@@ -255,7 +255,7 @@ __device__ __forceinline__ void fft64_tail(uint32_t (&x)[8], uint32_t e1, uint32
     constexpr unsigned s = S::s.s[0][2 * J];
     uint32_t P[8];
     sfor<8>([&](auto Q) CEC_FFT_AI {
-      const uint32_t y = qp1(x[Q]);
+      const uint32_t y = qp1<SWZ>(x[Q]);
       P[Q] = FFT_BOP3(e1, y, x[Q], kSel);
       x[Q] = FFT_BOP3(x[Q], y, e1, kXandN);
     });
@@ -266,13 +266,14 @@ __device__ __forceinline__ void fft64_tail(uint32_t (&x)[8], uint32_t e1, uint32
 
 // g'[t] = XOR over the bits b not set in t of c_b g[t + 2^b], in place in ascending j (every
 // term reads a higher register, or this register of another lane, before it is overwritten)
+template <bool SWZ>
 __device__ __forceinline__ void derivative(uint32_t (&X)[16][8], uint32_t e1, uint32_t e2) {
   sfor<16>([&](auto J) CEC_FFT_AI {
     after_prev<J>(X);
     uint32_t acc[8], z[8];
     sfor<8>([&](auto Q) CEC_FFT_AI {
-      acc[Q] = qp1(X[J][Q]) & e1;  // b = 0: c_0 = 1, partner t + 1 on lanes with bit 0 clear
-      z[Q] = qp2(X[J][Q]) & e2;    // b = 1: t + 2 on lanes with bit 1 clear
+      acc[Q] = qp1<SWZ>(X[J][Q]) & e1;  // b = 0: c_0 = 1, partner t + 1 on lanes with bit 0 clear
+      z[Q] = qp2<SWZ>(X[J][Q]) & e2;    // b = 1: t + 2 on lanes with bit 1 clear
     });
     mul_acc<DConst<1>::v, false>(acc, z, z);
     sfor<4>([&](auto B) CEC_FFT_AI {  // b = B + 2: register j + 2^B
@@ -299,6 +300,9 @@ __device__ __forceinline__ LaneCtx lane_ctx(uint32_t wave_col, uint32_t ss) {
   return c;
 }
 
+// SWZ: which phases exchange through the LDS crossbar (bit 0 the IFFT's layers 0, 1, bit 1 the
+// derivative, bit 2 the FFT's layers 1, 0), the others through DPP
+template <int SWZ>
 __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const uint32_t* __restrict__ plan1,
                                                   const uint32_t* const* __restrict__ plans,
                                                   const uint32_t* __restrict__ seg_list,
@@ -344,9 +348,9 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const u
 #endif
   });
   fence_all(X);
-  ifft64(X, e1, e2);
+  ifft64<(SWZ & 1) != 0>(X, e1, e2);
   fence_all(X);
-  derivative(X, e1, e2);
+  derivative<(SWZ & 2) != 0>(X, e1, e2);
   fence_all(X);
   fft64_upper(X);
   fence_all(X);
@@ -357,7 +361,7 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const u
     const uint32_t dw = P[FftDecDLayout::kDinv + J];
     after_prev<J>(X);
     if (dw) {
-      fft64_tail<J>(X[J], c1.e1, c1.e2);
+      fft64_tail<J, (SWZ & 4) != 0>(X[J], c1.e1, c1.e2);
 #ifdef CEC_FDD_BFE
       mul_rt(X[J], dw >> c1.sh);
 #else
@@ -478,11 +482,11 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
       fresh = 0;
     }
     fence_all(X);
-    ifft64(X, lane_ctx(0, 0).e1, lane_ctx(0, 0).e2);
+    ifft64<false>(X, lane_ctx(0, 0).e1, lane_ctx(0, 0).e2);
     fence_all(X);
     {
       const LaneCtx c = lane_ctx(0, 0);
-      derivative(X, c.e1, c.e2);
+      derivative<false>(X, c.e1, c.e2);
     }
     fence_all(X);
     fft64_upper(X);
@@ -504,7 +508,7 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_dp(
         if constexpr (J > 0) asm volatile("" : "+v"(col) : "v"(X[J - 1][7]));
         dp_load(rD, rP, J, col, ss, dp_rdmask<J>(P, c1.sh) & nx, pre);
       }
-      fft64_tail<J>(X[J], c1.e1, c1.e2);
+      fft64_tail<J, false>(X[J], c1.e1, c1.e2);
       const uint32_t rd = dp_rdmask<J>(P, c1.sh) & nx;
       tr8(pre);
       sfor<8>([&](auto Q) CEC_FFT_AI { X[J][Q] = FFT_BOP3(rd, pre[Q], X[J][Q], kSel); });
@@ -569,9 +573,22 @@ bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* con
   (void)form;
 #endif
   const uint64_t gx = (L.len / 512 * 64 + 255) / 256;
+  auto kern = k_fftdec_d<0>;
+#ifdef CEC_TUNING
+  // quad exchanges through the LDS crossbar: form 4 in every phase, 5..9 in some (the SWZ mask)
+  switch (form) {
+    case 4: kern = k_fftdec_d<7>; break;
+    case 5: kern = k_fftdec_d<2>; break;
+    case 6: kern = k_fftdec_d<3>; break;
+    case 7: kern = k_fftdec_d<4>; break;
+    case 8: kern = k_fftdec_d<1>; break;
+    case 9: kern = k_fftdec_d<6>; break;
+    default: break;
+  }
+#endif
   for (uint32_t s0 = 0; s0 < nseg; s0 += 65535) {
     const uint32_t ny = nseg - s0 < 65535 ? nseg - s0 : 65535;
-    hipLaunchKernelGGL(k_fftdec_d, dim3((unsigned)gx, ny), dim3(256), 0, st, L, plan1, plans,
+    hipLaunchKernelGGL(kern, dim3((unsigned)gx, ny), dim3(256), 0, st, L, plan1, plans,
                        seg_list, s0);
   }
   return true;

@@ -85,14 +85,17 @@ bool launch_fft_rs3232_verify(const Layout& L, uint8_t* ok, uint32_t nseg, hipSt
 // when the layout does not fit (fftdec_layout_ok).
 bool fftdec_layout_ok(const Layout& L);
 bool fftdec_big(int nrs);
+// form 0: the product's; tuning build only: 1 the IFFT's cross-lane exchanges through the LDS
+// crossbar (ds_swizzle) instead of DPP.
 bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
                    const uint32_t* const* plans, const uint32_t* seg_list, uint32_t nseg,
-                   hipStream_t st);
+                   hipStream_t st, int form = 0);
 // The formal-derivative decoder (fftdec_d.hip, plans of fftdec_plan_d): same arguments, any side.
 // form 0: one 512-column block per wave (k_fftdec_d, the product's). Tuning build only: 1 the
 // persistent kernel that merges a block's output multiplication with the next block's input
 // multiplication (k_fftdec_dp), 3 the same with wave priorities by remaining work (DESIGN.md §4:
-// 9 % fewer VALU per block, slower overall).
+// 9 % fewer VALU per block, slower overall), 4 k_fftdec_d with its quad exchanges through the LDS
+// crossbar (ds_swizzle) instead of DPP.
 bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* const* plans,
                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st, int form = 0);
 

@@ -221,12 +221,14 @@ def test_ct_variants_identical(torch, cess, corc, k, m, ln):
     enc.set_option(2, -1)
 
 
-@pytest.mark.parametrize("variant", [70, 72, -1])
+@pytest.mark.parametrize("variant", [70, 72, 73, 74, 75, 76, 77, 78, -1])
 @pytest.mark.parametrize("nseg,ln", [(1, 4096), (3, 16384), (9, 8192)])
 def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):
     """The formal-derivative decoder's forms (tuning build): -1 one block per wave (k_fftdec_d,
     the product's), 70 the pipelined persistent kernel (k_fftdec_dp: a wave merges a block's
-    output multiplication with the next block's input one), 72 the same with wave priorities.
+    output multiplication with the next block's input one), 72 the same with wave priorities, 73
+    k_fftdec_d with its quad exchanges through the LDS crossbar (ds_swizzle) instead of DPP, 74..78
+    that in some of its phases only.
     Several segments (per-segment plans), a single segment's host-API-sized batch, 12..32
     erasures: bit-exact with the oracle."""
     k = m = 32
@@ -245,6 +247,32 @@ def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):
     enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
     torch.cuda.synchronize()
     assert enc.stat(5) - before == nseg
+    assert np.array_equal(d_data.cpu().numpy(), data)
+    assert np.array_equal(d_par.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("variant", [79, -1])
+@pytest.mark.parametrize("nseg,ln,lo,hi", [(1, 4096, 4, 8), (5, 16384, 4, 16), (9, 8192, 9, 20)])
+def test_fftdec_m_forms_identical(torch, cess, corc, variant, nseg, ln, lo, hi):
+    """The syndrome-row decoder's forms (tuning build): -1 the product's, 79 its IFFT's cross-lane
+    exchanges through the LDS crossbar (ds_swizzle) instead of DPP. Per-segment plans of both
+    size classes and both sides (lo..hi erasures): bit-exact with the oracle."""
+    k = m = 32
+    rng = np.random.default_rng(ln + nseg + lo)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    want = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = np.ones((nseg, 64), np.uint8)
+    for s in range(nseg):
+        present[s, rng.choice(64, size=int(rng.integers(lo, hi + 1)), replace=False)] = 0
+    enc = cess.New(k, m, tuning=True)
+    enc.set_option(2, variant)
+    enc.set_option(8, 1)  # the syndrome-row decoder for every segment
+    d_data = to_dev(torch, data * present[:, :k, None])
+    d_par = to_dev(torch, want * present[:, k:, None])
+    before = enc.stat(4)
+    enc.ReconstructBatch(d_data, d_par, nseg, ln, present)
+    torch.cuda.synchronize()
+    assert enc.stat(4) - before == nseg
     assert np.array_equal(d_data.cpu().numpy(), data)
     assert np.array_equal(d_par.cpu().numpy(), want)
 

@@ -25,10 +25,10 @@ CEC_PROBE(p_mul, {
     mul_rt_lds(X[J], (const lds_u32*)probe_masks + (J * 4 + (threadIdx.x & 3)) * 8);
   });
 })
-CEC_PROBE(p_ifft64, { ifft64(X, e1, e2); })
-CEC_PROBE(p_derivative, { derivative(X, e1, e2); })
+CEC_PROBE(p_ifft64, { ifft64<false>(X, e1, e2); })
+CEC_PROBE(p_derivative, { derivative<false>(X, e1, e2); })
 CEC_PROBE(p_fft64_upper, { fft64_upper(X); })
 CEC_PROBE(p_fft64_tail, {
-  sfor<16>([&](auto J) CEC_FFT_AI { after_prev<J>(X); fft64_tail<J>(X[J], e1, e2); });
+  sfor<16>([&](auto J) CEC_FFT_AI { after_prev<J>(X); fft64_tail<J, false>(X[J], e1, e2); });
 })
 }  // namespace cec

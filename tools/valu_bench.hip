@@ -8,6 +8,7 @@
 // build: hipcc --offload-arch=gfx950 -O3 tools/valu_bench.hip -o tools/valu_bench
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <vector>
 #include <algorithm>
@@ -63,6 +64,13 @@
 #define O_39(i) "v_bitop3_b32 %" #i ", %" #i ", %8, %9 bitop3:0x78\n\t"
 #define O_40(i) "v_max_u32 %" #i ", %" #i ", %8\n\t"
 #define O_41(i) "v_lshlrev_b16_e64 %" #i ", 1, %" #i "\n\t"
+#define O_44(i) "v_xor_b32_dpp %" #i ", %" #i ", %8 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+#define O_45(i) "v_and_b32_dpp %" #i ", %" #i ", %8 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+// lane-half swaps write both operands: eight per asm over the eight chains (a ring of pairs)
+#define SWAPS(INS)                                                                          \
+  asm volatile(INS " %0, %1\n\t" INS " %2, %3\n\t" INS " %4, %5\n\t" INS " %6, %7\n\t" INS   \
+               " %1, %2\n\t" INS " %3, %4\n\t" INS " %5, %6\n\t" INS " %7, %0\n\t"               \
+               : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7));
 
 template <int OPI>
 __global__ void k_valu(uint32_t* out, uint64_t* cyc, int iters, uint32_t a, uint32_t b) {
@@ -115,13 +123,17 @@ __global__ void k_valu(uint32_t* out, uint64_t* cyc, int iters, uint32_t a, uint
     if constexpr (OPI == 39) { REP8(CHAINS(O_39)) }
     if constexpr (OPI == 40) { REP8(CHAINS(O_40)) }
     if constexpr (OPI == 41) { REP8(CHAINS(O_41)) }
+    if constexpr (OPI == 42) { REP8(SWAPS("v_permlane32_swap_b32")) }
+    if constexpr (OPI == 43) { REP8(SWAPS("v_permlane16_swap_b32")) }
+    if constexpr (OPI == 44) { REP8(CHAINS(O_44)) }
+    if constexpr (OPI == 45) { REP8(CHAINS(O_45)) }
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;
   if (threadIdx.x % 64 == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
 }
 
-static const char* kNames[] = {"v_bitop3_b32", "v_perm_b32", "v_lshlrev_b32", "v_alignbit_b32", "v_add3_u32", "v_add_u32", "v_xor_b32", "v_lshl_or_b32", "v_fma_f32", "v_and_b32", "v_mul_u32_u24", "v_mad_u32_u24", "v_pk_add_u16", "v_pk_lshlrev_b16", "v_cndmask_b32", "v_bfi_b32", "v_sub_u32", "v_or3_b32", "v_and_or_b32", "v_xad_u32", "v_lshl_add_u32", "v_bfe_u32", "v_lshrrev_b32", "v_mul_lo_u32", "v_mov_b32_dpp", "v_add_u32_sdwa", "v_lshlrev_b16", "v_lshlrev_b32_by7", "v_lshrrev_b32_by1", "v_lshlrev_b32_vreg", "v_or_b32", "v_not_b32", "v_mov_b32", "v_add_co_u32", "v_ashrrev_i32", "v_bitop3_b16", "v_add_u16", "v_xor_b32_e64_lit", "v_and_b32_lit", "v_bitop3_lit", "v_max_u32", "v_lshlrev_b16_by1_e64"};
+static const char* kNames[] = {"v_bitop3_b32", "v_perm_b32", "v_lshlrev_b32", "v_alignbit_b32", "v_add3_u32", "v_add_u32", "v_xor_b32", "v_lshl_or_b32", "v_fma_f32", "v_and_b32", "v_mul_u32_u24", "v_mad_u32_u24", "v_pk_add_u16", "v_pk_lshlrev_b16", "v_cndmask_b32", "v_bfi_b32", "v_sub_u32", "v_or3_b32", "v_and_or_b32", "v_xad_u32", "v_lshl_add_u32", "v_bfe_u32", "v_lshrrev_b32", "v_mul_lo_u32", "v_mov_b32_dpp", "v_add_u32_sdwa", "v_lshlrev_b16", "v_lshlrev_b32_by7", "v_lshrrev_b32_by1", "v_lshlrev_b32_vreg", "v_or_b32", "v_not_b32", "v_mov_b32", "v_add_co_u32", "v_ashrrev_i32", "v_bitop3_b16", "v_add_u16", "v_xor_b32_e64_lit", "v_and_b32_lit", "v_bitop3_lit", "v_max_u32", "v_lshlrev_b16_by1_e64", "v_permlane32_swap_b32", "v_permlane16_swap_b32", "v_xor_b32_dpp", "v_and_b32_dpp"};
 
 template <int OPI>
 void run(int waves_per_simd, int cus) {
@@ -169,7 +181,7 @@ void run_all() {
 template <int... I>
 void run_list(std::integer_sequence<int, I...>, int from) { ((I >= from ? run_all<I>() : void()), ...); }
 
-int main() {
-  run_list(std::make_integer_sequence<int, 42>{}, 27);
+int main(int argc, char** argv) {
+  run_list(std::make_integer_sequence<int, 46>{}, argc > 1 ? atoi(argv[1]) : 27);
   return 0;
 }
