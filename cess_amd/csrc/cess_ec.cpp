@@ -738,10 +738,21 @@ using cec::kFdNone;
 // tuning build: CEC_OPT_CT_VARIANT 70 runs the pipelined persistent k_fftdec_dp instead of the
 // one-block-per-wave k_fftdec_d, 72 the same with wave priorities, 73 k_fftdec_d with its quad
 // exchanges through the LDS crossbar, 74..78 that in some phases only: the derivative, IFFT +
-// derivative, the FFT tail, the IFFT, derivative + tail (A/B sweeps)
-// tuning build: CEC_OPT_CT_VARIANT 79 runs k_fftdec_m with its IFFT's cross-lane exchanges through
-// the LDS crossbar
-int fdm_form(const cec_codec* c) { return c->opts.ct_variant == 79 ? 1 : 0; }
+// derivative (the product's), the FFT tail, the IFFT, derivative + tail; 83 DPP in every phase
+// (the round-3 form) (A/B sweeps)
+// tuning build: CEC_OPT_CT_VARIANT 79..82 run k_fftdec_m with pair exchanges through the LDS
+// crossbar: the IFFT's (the product's); + the FFT's last layer; + the nibble packs; all three;
+// 84 DPP everywhere (the round-3 form). launch_fftdec's form is 1 + that mask.
+int fdm_form(const cec_codec* c) {
+  switch (c->opts.ct_variant) {
+    case 79: return 2;
+    case 80: return 4;
+    case 81: return 6;
+    case 82: return 8;
+    case 84: return 1;
+    default: return 0;
+  }
+}
 
 int fdd_form(const cec_codec* c) {
   switch (c->opts.ct_variant) {
@@ -753,6 +764,7 @@ int fdd_form(const cec_codec* c) {
     case 76: return 7;
     case 77: return 8;
     case 78: return 9;
+    case 83: return 10;
     default: return 0;
   }
 }

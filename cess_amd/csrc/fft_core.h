@@ -200,12 +200,12 @@ __device__ __forceinline__ void fft32_upper(uint32_t (&X)[16][8]) {
   });
 }
 // layer 0 of that FFT on register slot J (positions 2J, 2J + 1: across the lane pair)
-template <unsigned BETA, int J>
+template <unsigned BETA, int J, bool SWZ = false>
 __device__ __forceinline__ void fft32_l0(uint32_t (&x)[8], uint32_t em, uint32_t om) {
   constexpr unsigned s = Skews<BETA>::s.s[0][J];
   uint32_t P[8];
   sfor<8>([&](auto Q) CEC_FFT_AI {
-    const uint32_t y = partner(x[Q]);
+    const uint32_t y = partner_x<SWZ>(x[Q]);
     P[Q] = FFT_BOP3(em, y, x[Q], kSel);
     x[Q] = FFT_BOP3(x[Q], om, y, kXand);
   });

@@ -74,9 +74,11 @@ __device__ __forceinline__ void fence(uint32_t (&x)[8]) {
 // Each lane reads its partner's plane (DPP straight from the register, no wait states) and rotates
 // it (rot: 28 on lane 0, the partner's low nibbles go up; 4 on lane 1, its high nibbles go down)
 // into the half it does not keep.
+template <bool SWZ>
 __device__ __forceinline__ void pack_slot(uint32_t (&x)[8], uint32_t keep, uint32_t rot) {
   sfor<8>([&](auto Q) CEC_FFT_AI {
-    const uint32_t y = __builtin_amdgcn_alignbit(partner(x[Q]), partner(x[Q]), rot);
+    const uint32_t p = partner_x<SWZ>(x[Q]);
+    const uint32_t y = __builtin_amdgcn_alignbit(p, p, rot);
     x[Q] = FFT_BOP3(keep, x[Q], y, kSel);
   });
 }
@@ -90,7 +92,9 @@ constexpr int kSmallNr = 4;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef const __attribute__((address_space(3))) u32x4 lds_u32x4;
 
-template <unsigned SIDE, int NLO, int NHI, int LR, bool SWZ>
+// SWZ: which pair exchanges go through the LDS crossbar (bit 0 the IFFT's layer 0, bit 1 the FFT's
+// layer 0 on the slots read, bit 2 the nibble packs), the others through DPP
+template <unsigned SIDE, int NLO, int NHI, int LR, int SWZ>
 __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64_t col,
                                            cplan_t P, lds_u32* lw) {
   constexpr unsigned BA = SIDE ? 32u : 0u, BB = SIDE ? 0u : 32u;
@@ -125,7 +129,7 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
                                              soff, 0, 2);
   }
   sfor<16>([&](auto J) CEC_FFT_AI { tr8(X[J]); });
-  ifft32<BA, SWZ>(X, em);
+  ifft32<BA, (SWZ & 1) != 0>(X, em);
   // q on coset B; its last layer only on the slots whose q is read (syndrome rows R, erased
   // outputs of B: the plan's kPslots, numbered before the swaps below)
   fft32_upper<BB>(X);
@@ -133,7 +137,7 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
   const uint32_t pslots = P[FftDecLayout::kPslots];
   sfor<16>([&](auto J) CEC_FFT_AI {
     if constexpr (J > 0) asm volatile("" : "+v"(X[J][0]) : "v"(X[J - 1][7]));
-    if ((pslots >> J) & 1) fft32_l0<BB, J>(X[J], em, om);
+    if ((pslots >> J) & 1) fft32_l0<BB, J, (SWZ & 2) != 0>(X[J], em, om);
   });
   // X is complete here: the phases below start from it (keeps the compiler from interleaving the
   // transform's tail with them, which costs registers)
@@ -190,13 +194,13 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
         asm volatile("" : "+v"(X[I][0]), "+v"(X[I][1]), "+v"(X[I][2]), "+v"(X[I][3]),
                      "+v"(X[I][4]), "+v"(X[I][5]), "+v"(X[I][6]), "+v"(X[I][7])
                      : "v"(X[I - 1][7]));
-      pack_slot(X[I], keep, rot);
+      pack_slot<(SWZ & 4) != 0>(X[I], keep, rot);
     });
     sfor<16 - NR>([&](auto D) CEC_FFT_AI {
       constexpr int J = NR + D;
       if ((npk >> J) & 1) {
         asm volatile("");  // a branch, not a select over every slot
-        pack_slot(X[J], keep, rot);
+        pack_slot<(SWZ & 4) != 0>(X[J], keep, rot);
       }
     });
     for (uint32_t o = 0; o < nout; ++o) {
@@ -259,9 +263,12 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
 }
 
 // plans: per listed segment (y) its plan, or `plan1` for every segment. BIG: plans with more than
-// kSmallNr syndrome slots (the host sorts them, fftdec_big). SWZ: the IFFT's cross-lane layer
-// exchanges through the LDS crossbar (tuning build, variant 79).
-template <unsigned SIDE, bool BIG, bool SWZ = false>
+// kSmallNr syndrome slots (the host sorts them, fftdec_big). SWZ: the exchanges through the LDS
+// crossbar (dec_m_cols). The product's: the IFFT's (kFdmSwz = 1), 0.7-3.1 % faster than DPP at 5..16
+// erasures; the FFT's last layer and the nibble packs through the crossbar are slower (the packs
+// take the small class past 168 VGPRs), profiles/r04/fdm_swz_*.txt.
+constexpr int kFdmSwz = 1;
+template <unsigned SIDE, bool BIG, int SWZ>
 __global__ __launch_bounds__(256) CEC_FD_ATTR void k_fftdec_m(Layout L, const uint32_t* __restrict__ plan1,
                                                   const uint32_t* const* __restrict__ plans,
                                                   const uint32_t* __restrict__ seg_list,
@@ -294,12 +301,22 @@ bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
                    hipStream_t st, int form) {
   if (!fftdec_layout_ok(L) || (side != 0 && side != 1)) return false;
   const uint64_t gx = (L.len / 32 * 2 + 255) / 256;
-  auto kern = side ? (big ? k_fftdec_m<1, true> : k_fftdec_m<1, false>)
-                   : (big ? k_fftdec_m<0, true> : k_fftdec_m<0, false>);
+  auto kern = side ? (big ? k_fftdec_m<1, true, kFdmSwz> : k_fftdec_m<1, false, kFdmSwz>)
+                   : (big ? k_fftdec_m<0, true, kFdmSwz> : k_fftdec_m<0, false, kFdmSwz>);
 #ifdef CEC_TUNING
-  if (form == 1)
-    kern = side ? (big ? k_fftdec_m<1, true, true> : k_fftdec_m<1, false, true>)
-                : (big ? k_fftdec_m<0, true, true> : k_fftdec_m<0, false, true>);
+  auto pick = [&](auto S) {
+    constexpr int M = decltype(S)::value;
+    kern = side ? (big ? k_fftdec_m<1, true, M> : k_fftdec_m<1, false, M>)
+                : (big ? k_fftdec_m<0, true, M> : k_fftdec_m<0, false, M>);
+  };
+  switch (form) {  // form = 1 + the SWZ mask
+    case 1: pick(std::integral_constant<int, 0>{}); break;
+    case 2: pick(std::integral_constant<int, 1>{}); break;
+    case 4: pick(std::integral_constant<int, 3>{}); break;
+    case 6: pick(std::integral_constant<int, 5>{}); break;
+    case 8: pick(std::integral_constant<int, 7>{}); break;
+    default: break;
+  }
 #else
   (void)form;
 #endif

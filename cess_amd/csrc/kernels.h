@@ -85,8 +85,9 @@ bool launch_fft_rs3232_verify(const Layout& L, uint8_t* ok, uint32_t nseg, hipSt
 // when the layout does not fit (fftdec_layout_ok).
 bool fftdec_layout_ok(const Layout& L);
 bool fftdec_big(int nrs);
-// form 0: the product's; tuning build only: 1 the IFFT's cross-lane exchanges through the LDS
-// crossbar (ds_swizzle) instead of DPP.
+// form 0: the product's (the IFFT's pair exchanges through the LDS crossbar, the others through
+// DPP); tuning build only: 1 + a mask of the exchanges through the crossbar (bit 0 the IFFT's, 1 the
+// FFT's last layer, 2 the nibble packs).
 bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
                    const uint32_t* const* plans, const uint32_t* seg_list, uint32_t nseg,
                    hipStream_t st, int form = 0);
@@ -94,8 +95,8 @@ bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
 // form 0: one 512-column block per wave (k_fftdec_d, the product's). Tuning build only: 1 the
 // persistent kernel that merges a block's output multiplication with the next block's input
 // multiplication (k_fftdec_dp), 3 the same with wave priorities by remaining work (DESIGN.md §4:
-// 9 % fewer VALU per block, slower overall), 4 k_fftdec_d with its quad exchanges through the LDS
-// crossbar (ds_swizzle) instead of DPP.
+// 9 % fewer VALU per block, slower overall), 4..10 k_fftdec_d with other masks of the phases whose
+// quad exchanges go through the LDS crossbar (ds_swizzle) instead of DPP (fftdec_d.hip kFddSwz).
 bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* const* plans,
                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st, int form = 0);
 

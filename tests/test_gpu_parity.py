@@ -221,14 +221,14 @@ def test_ct_variants_identical(torch, cess, corc, k, m, ln):
     enc.set_option(2, -1)
 
 
-@pytest.mark.parametrize("variant", [70, 72, 73, 74, 75, 76, 77, 78, -1])
+@pytest.mark.parametrize("variant", [70, 72, 73, 74, 75, 76, 77, 78, 83, -1])
 @pytest.mark.parametrize("nseg,ln", [(1, 4096), (3, 16384), (9, 8192)])
 def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):
     """The formal-derivative decoder's forms (tuning build): -1 one block per wave (k_fftdec_d,
     the product's), 70 the pipelined persistent kernel (k_fftdec_dp: a wave merges a block's
     output multiplication with the next block's input one), 72 the same with wave priorities, 73
-    k_fftdec_d with its quad exchanges through the LDS crossbar (ds_swizzle) instead of DPP, 74..78
-    that in some of its phases only.
+    k_fftdec_d with its quad exchanges through the LDS crossbar (ds_swizzle) in every phase, 74..78
+    in some (75 = the product's: IFFT and derivative), 83 DPP in every phase.
     Several segments (per-segment plans), a single segment's host-API-sized batch, 12..32
     erasures: bit-exact with the oracle."""
     k = m = 32
@@ -251,11 +251,12 @@ def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):
     assert np.array_equal(d_par.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("variant", [79, -1])
+@pytest.mark.parametrize("variant", [79, 80, 81, 82, 84, -1])
 @pytest.mark.parametrize("nseg,ln,lo,hi", [(1, 4096, 4, 8), (5, 16384, 4, 16), (9, 8192, 9, 20)])
 def test_fftdec_m_forms_identical(torch, cess, corc, variant, nseg, ln, lo, hi):
-    """The syndrome-row decoder's forms (tuning build): -1 the product's, 79 its IFFT's cross-lane
-    exchanges through the LDS crossbar (ds_swizzle) instead of DPP. Per-segment plans of both
+    """The syndrome-row decoder's forms (tuning build): -1 the product's (the IFFT's pair exchanges
+    through the LDS crossbar), 79..82 the crossbar for the IFFT's; + the FFT's last layer; + the
+    nibble packs; all three, 84 DPP everywhere. Per-segment plans of both
     size classes and both sides (lo..hi erasures): bit-exact with the oracle."""
     k = m = 32
     rng = np.random.default_rng(ln + nseg + lo)

@@ -31,6 +31,8 @@ def counts(obj: str):
                 c["dpp" if "quad_perm" in line else "valu"] += 1
                 if tok[0].startswith("v_lshlrev"):
                     c["half_shift"] += 1
+            elif tok and tok[0].startswith("ds_swizzle"):
+                c["swizzle"] += 1
         out[name] = c
     return out
 
@@ -42,7 +44,8 @@ def main() -> None:
                         "-c", os.path.join(HERE, "fdd_phases.hip"), "-o", obj], check=True)
         c = counts(obj)
     base = c["p_none"]
-    per = {k: {x: c[k][x] - base[x] for x in ("valu", "dpp", "half_shift")} for k in c}
+    per = {k: {x: c[k][x] - base[x] for x in ("valu", "dpp", "half_shift", "swizzle")}
+           for k in c}
     rows = [("transposes in + out (2 x 16 tr8)", 2, "p_tr8"),
             ("run-time multiplies in + out (2 x 16)", 2, "p_mul"),
             ("IFFT_64 (layers 0, 1 cross-lane; 2..5 in-lane)", 1, "p_ifft64"),
@@ -51,12 +54,14 @@ def main() -> None:
             ("FFT_64 layers 1, 0 (cross-lane, 16 slots)", 1, "p_fft64_tail")]
     tot = collections.Counter()
     print("k_fftdec_d per 512-column block and wave at 32 erasures (VALU incl. DPP; DPP; "
-          "half-rate left shifts)")
+          "half-rate left shifts; ds_swizzle, no VALU slot)")
     for what, times, k in rows:
         v = {x: times * per[k][x] for x in per[k]}
         tot.update(v)
-        print(f"{what:52s} {v['valu'] + v['dpp']:6d} {v['dpp']:5d} {v['half_shift']:5d}")
-    print(f"{'sum':52s} {tot['valu'] + tot['dpp']:6d} {tot['dpp']:5d} {tot['half_shift']:5d}")
+        print(f"{what:52s} {v['valu'] + v['dpp']:6d} {v['dpp']:5d} {v['half_shift']:5d} "
+              f"{v['swizzle']:5d}")
+    print(f"{'sum':52s} {tot['valu'] + tot['dpp']:6d} {tot['dpp']:5d} {tot['half_shift']:5d} "
+          f"{tot['swizzle']:5d}")
 
 
 if __name__ == "__main__":

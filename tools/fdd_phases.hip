@@ -1,7 +1,8 @@
 // Probe kernels for the per-phase instruction count of k_fftdec_d (tools/fdd_phase_count.py):
 // each runs one phase of the decoder (cess_amd/csrc/fftdec_d.hip, included as is) on the 16 x 8
 // register slots of a lane, between fences, so the difference of its VALU count against p_none is
-// that phase's instructions on the shipped code path (same helpers, same occupancy attribute).
+// that phase's instructions on the shipped code path (same helpers and exchange forms, kFddSwz;
+// same occupancy attribute).
 #include "../cess_amd/csrc/fftdec_d.hip"
 
 namespace cec {
@@ -25,10 +26,10 @@ CEC_PROBE(p_mul, {
     mul_rt_lds(X[J], (const lds_u32*)probe_masks + (J * 4 + (threadIdx.x & 3)) * 8);
   });
 })
-CEC_PROBE(p_ifft64, { ifft64<false>(X, e1, e2); })
-CEC_PROBE(p_derivative, { derivative<false>(X, e1, e2); })
+CEC_PROBE(p_ifft64, { ifft64<(kFddSwz & 1) != 0>(X, e1, e2); })
+CEC_PROBE(p_derivative, { derivative<(kFddSwz & 2) != 0>(X, e1, e2); })
 CEC_PROBE(p_fft64_upper, { fft64_upper(X); })
 CEC_PROBE(p_fft64_tail, {
-  sfor<16>([&](auto J) CEC_FFT_AI { after_prev<J>(X); fft64_tail<J, false>(X[J], e1, e2); });
+  sfor<16>([&](auto J) CEC_FFT_AI { after_prev<J>(X); fft64_tail<J, (kFddSwz & 4) != 0>(X[J], e1, e2); });
 })
 }  // namespace cec
