@@ -264,10 +264,10 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
 
 // plans: per listed segment (y) its plan, or `plan1` for every segment. BIG: plans with more than
 // kSmallNr syndrome slots (the host sorts them, fftdec_big). SWZ: the exchanges through the LDS
-// crossbar (dec_m_cols). The product's: the IFFT's (kFdmSwz = 1), 0.7-3.1 % faster than DPP at 5..16
-// erasures; the FFT's last layer and the nibble packs through the crossbar are slower (the packs
-// take the small class past 168 VGPRs), profiles/r04/fdm_swz_*.txt.
-constexpr int kFdmSwz = 1;
+// crossbar (dec_m_cols). The product's: DPP everywhere (kFdmSwz = 0); the IFFT's exchange through
+// the crossbar is no faster one form per process (profiles/r04/swz_standalone_runs.jsonl), the
+// nibble packs through it take the small class past 168 VGPRs.
+constexpr int kFdmSwz = 0;
 template <unsigned SIDE, bool BIG, int SWZ>
 __global__ __launch_bounds__(256) CEC_FD_ATTR void k_fftdec_m(Layout L, const uint32_t* __restrict__ plan1,
                                                   const uint32_t* const* __restrict__ plans,

@@ -87,8 +87,8 @@ __device__ __forceinline__ void after_prev(uint32_t (&X)[16][8]) {
 // compiler into the consuming v_and / v_xor where it can; every DPP form (v_mov_b32_dpp and the
 // VOP2 ops with a DPP operand alike) issues at half rate on gfx950 (profiles/r04/
 // valu_bench_r04.jsonl), so the 768 exchanges per block are ~1,500 issue slots. SWZ = true:
-// ds_swizzle in quad-permute mode through the LDS crossbar, no VALU slot, LDS latency instead (the
-// product takes it in the IFFT and the derivative, k_fftdec_d's kFddSwz).
+// ds_swizzle in quad-permute mode through the LDS crossbar, no VALU slot, LDS latency instead
+// (tuning forms; k_fftdec_d's kFddSwz).
 template <bool SWZ>
 __device__ __forceinline__ uint32_t qp1(uint32_t v) {
   if constexpr (SWZ) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x80B1);
@@ -301,10 +301,11 @@ __device__ __forceinline__ LaneCtx lane_ctx(uint32_t wave_col, uint32_t ss) {
 }
 
 // SWZ: which phases exchange through the LDS crossbar (bit 0 the IFFT's layers 0, 1, bit 1 the
-// derivative, bit 2 the FFT's layers 1, 0), the others through DPP. The product's: the IFFT and the
-// derivative (kFddSwz = 3): 4.4-4.5 % faster than DPP everywhere at 20 and 32 erasures, the FFT's
-// tail through the crossbar slower (interleaved A/B of every mask, profiles/r04/fdd_swz_*.txt).
-constexpr int kFddSwz = 3;
+// derivative, bit 2 the FFT's layers 1, 0), the others through DPP. The product's: DPP everywhere
+// (kFddSwz = 0). The crossbar in the IFFT and the derivative looked 4.4 % faster in an in-process
+// A/B that alternates the forms launch by launch, but one form per process, as the line and a real
+// rebuild run it, the two are equal within 1 % (profiles/r04/swz_standalone_runs.jsonl).
+constexpr int kFddSwz = 0;
 template <int SWZ>
 __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const uint32_t* __restrict__ plan1,
                                                   const uint32_t* const* __restrict__ plans,
@@ -579,7 +580,7 @@ bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* con
   auto kern = k_fftdec_d<kFddSwz>;
 #ifdef CEC_TUNING
   // other exchange masks (SWZ): form 4 the crossbar in every phase, 5..9 in some, 10 DPP in every
-  // phase (the round-3 form)
+  // phase (= the product's)
   switch (form) {
     case 4: kern = k_fftdec_d<7>; break;
     case 5: kern = k_fftdec_d<2>; break;

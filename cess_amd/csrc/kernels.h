@@ -85,9 +85,8 @@ bool launch_fft_rs3232_verify(const Layout& L, uint8_t* ok, uint32_t nseg, hipSt
 // when the layout does not fit (fftdec_layout_ok).
 bool fftdec_layout_ok(const Layout& L);
 bool fftdec_big(int nrs);
-// form 0: the product's (the IFFT's pair exchanges through the LDS crossbar, the others through
-// DPP); tuning build only: 1 + a mask of the exchanges through the crossbar (bit 0 the IFFT's, 1 the
-// FFT's last layer, 2 the nibble packs).
+// form 0: the product's (every pair exchange through DPP); tuning build only: 1 + a mask of the
+// exchanges through the LDS crossbar (bit 0 the IFFT's, 1 the FFT's last layer, 2 the nibble packs).
 bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
                    const uint32_t* const* plans, const uint32_t* seg_list, uint32_t nseg,
                    hipStream_t st, int form = 0);

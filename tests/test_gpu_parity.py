@@ -228,7 +228,7 @@ def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):
     the product's), 70 the pipelined persistent kernel (k_fftdec_dp: a wave merges a block's
     output multiplication with the next block's input one), 72 the same with wave priorities, 73
     k_fftdec_d with its quad exchanges through the LDS crossbar (ds_swizzle) in every phase, 74..78
-    in some (75 = the product's: IFFT and derivative), 83 DPP in every phase.
+    in some, 83 DPP in every phase through the tuning form.
     Several segments (per-segment plans), a single segment's host-API-sized batch, 12..32
     erasures: bit-exact with the oracle."""
     k = m = 32
@@ -254,9 +254,9 @@ def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):
 @pytest.mark.parametrize("variant", [79, 80, 81, 82, 84, -1])
 @pytest.mark.parametrize("nseg,ln,lo,hi", [(1, 4096, 4, 8), (5, 16384, 4, 16), (9, 8192, 9, 20)])
 def test_fftdec_m_forms_identical(torch, cess, corc, variant, nseg, ln, lo, hi):
-    """The syndrome-row decoder's forms (tuning build): -1 the product's (the IFFT's pair exchanges
-    through the LDS crossbar), 79..82 the crossbar for the IFFT's; + the FFT's last layer; + the
-    nibble packs; all three, 84 DPP everywhere. Per-segment plans of both
+    """The syndrome-row decoder's forms (tuning build): -1 the product's (DPP exchanges), 79..82
+    the LDS crossbar for the IFFT's; + the FFT's last layer; + the nibble packs; all three, 84 DPP
+    everywhere through the tuning form. Per-segment plans of both
     size classes and both sides (lo..hi erasures): bit-exact with the oracle."""
     k = m = 32
     rng = np.random.default_rng(ln + nseg + lo)
