@@ -926,6 +926,9 @@ def main() -> None:
             enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
 
     if args.sweep:
+        # forms alternate launch by launch in one process: a screen, not a verdict — forms whose
+        # power or LDS use differ can come out a few per cent apart here and equal one per process
+        # (profiles/r04/swz_standalone_runs.jsonl); confirm with --variant, one form per process
         step = step_codec  # noqa: F811
         variants = [int(v) for v in args.sweep.split(",")]
         times = {v: [] for v in variants}
