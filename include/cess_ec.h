@@ -98,10 +98,11 @@ int cec_reconstruct_batch(cec_codec* codec, uint8_t* d_data, uint8_t* d_parity, 
  * like cec_reconstruct_batch with per-segment patterns (present: nseg*(k+m) flags; survivors =
  * cec_survivors of each segment's pattern), but every missing shard receives only the
  * contribution of the survivors flagged in `held` (nseg*(k+m) flags; flags of non-survivors are
- * ignored): out = XOR over held survivors i of D[out][i] * shard_i. Only held survivors are read.
- * The rebuild is linear, so XOR-ing the partials of a partition of the survivors (one per GPU
- * holding some of them, cec_xor_batch) gives the missing shard; a segment with no held survivor
- * gets zeros. A GPU then sends one partial per lost fragment instead of its survivors. */
+ * ignored): out = XOR over held survivors i of D[out][i] * shard_i. Only held survivors are read
+ * (a segment with no held survivor gets zeros: its program multiplies one survivor slot of the
+ * batch, whatever it holds, by zero coefficients). The rebuild is linear, so XOR-ing the partials
+ * of a partition of the survivors (one per GPU holding some of them, cec_xor_batch) gives the
+ * missing shard. A GPU then sends one partial per lost fragment instead of its survivors. */
 int cec_reconstruct_partial_batch(cec_codec* codec, uint8_t* d_data, uint8_t* d_parity,
                                   size_t nseg, size_t shard_len, const uint8_t* present,
                                   const uint8_t* held, int data_only, void* hip_stream);
