@@ -447,14 +447,18 @@ def cabi_legs(ex_out, gather_leg, degraded_gather, enc, code, world, rank, dev, 
 
 
 def erasure_patterns(k: int, m: int, nseg: int, ne: int, seed: int,
-                     lose_parity: bool = False) -> np.ndarray:
+                     lose_parity: bool = False, run: bool = False) -> np.ndarray:
     """Configs 6 / 7: [nseg][k + m] present flags, ne random erasures per segment (or every
-    parity shard lost); tests/test_host.py replays the chooser on the same patterns."""
+    parity shard lost; or, `run`, ne consecutive shard indices from a random start, wrapping: a
+    correlated loss such as neighbouring miners of the placement going down together);
+    tests/test_host.py replays the chooser on the same patterns."""
     rng = np.random.default_rng(seed)
     present = np.ones((nseg, k + m), np.uint8)
     for s_ in range(nseg):
         if lose_parity:
             present[s_, k:] = 0
+        elif run:
+            present[s_, (int(rng.integers(0, k + m)) + np.arange(ne)) % (k + m)] = 0
         else:
             present[s_, rng.choice(k + m, size=ne, replace=False)] = 0
     return present
@@ -778,6 +782,9 @@ def main() -> None:
                     help="RS(32,32) rebuilds: 0 = the cost model's pick of the FFT-domain decoders "
                          "and k_rthx (library default), 1 = always the syndrome-row decoder, "
                          "2 = always the formal-derivative decoder (CEC_OPT_FFTDEC_MODE)")
+    ap.add_argument("--erasure-run", action="store_true",
+                    help="config 6: the erasures of a segment are consecutive shard indices "
+                         "(random start, wrapping) instead of random ones")
     ap.add_argument("--cabi-deadline", type=float, default=240.0,
                     help="world > 1: seconds the C-ABI (cec_dist) exchange legs may take before "
                          "the line is printed without them")
@@ -845,6 +852,8 @@ def main() -> None:
     k, m, F, nseg_cfg, desc = CONFIGS[args.config]
     if args.config == 6 and args.erasures:
         desc = desc.replace("32 random erasures", f"{args.erasures} random erasures")
+    if args.config == 6 and args.erasure_run:
+        desc = desc.replace("random erasures", "consecutive erasures")
     if args.segments:
         nseg_cfg = args.segments
         desc = f"{desc} [{args.segments} segments per GPU = {args.segments * k * F / 2**30:g} GiB]"
@@ -878,7 +887,8 @@ def main() -> None:
     elif args.config in (6, 7):
         ne = (args.erasures or m) if args.config == 6 else 1
         present = erasure_patterns(k, m, nseg, ne, seed=seg0 + args.config,
-                                   lose_parity=args.lose_parity and args.config == 6)
+                                   lose_parity=args.lose_parity and args.config == 6,
+                                   run=args.erasure_run and args.config == 6)
     d_hex = None
     gather = None
     if args.config == 4:

@@ -738,8 +738,8 @@ using cec::kFdNone;
 // tuning build: CEC_OPT_CT_VARIANT 70 runs the pipelined persistent k_fftdec_dp instead of the
 // one-block-per-wave k_fftdec_d, 72 the same with wave priorities, 73 k_fftdec_d with its quad
 // exchanges through the LDS crossbar, 74..78 that in some phases only: the derivative, IFFT +
-// derivative, the FFT tail, the IFFT, derivative + tail; 83 DPP in every phase (= the product's)
-// (A/B sweeps)
+// derivative, the FFT tail, the IFFT, derivative + tail; 83 DPP in every phase (= the product's);
+// 85 the product's without the skip of unread input slots (A/B sweeps)
 // tuning build: CEC_OPT_CT_VARIANT 79..82 run k_fftdec_m with pair exchanges through the LDS
 // crossbar: the IFFT's; + the FFT's last layer; + the nibble packs; all three; 84 DPP everywhere
 // (= the product's). launch_fftdec's form is 1 + that mask.
@@ -765,6 +765,7 @@ int fdd_form(const cec_codec* c) {
     case 77: return 8;
     case 78: return 9;
     case 83: return 10;
+    case 85: return 11;
     default: return 0;
   }
 }

@@ -306,7 +306,9 @@ __device__ __forceinline__ LaneCtx lane_ctx(uint32_t wave_col, uint32_t ss) {
 // A/B that alternates the forms launch by launch, but one form per process, as the line and a real
 // rebuild run it, the two are equal within 1 % (profiles/r04/swz_standalone_runs.jsonl).
 constexpr int kFddSwz = 0;
-template <int SWZ>
+// SKIP: a slot none of whose four positions is read (all erased or unused: its loads returned
+// zeros) skips its transpose and its multiplication by lam (zero in, zero out); a uniform branch
+template <int SWZ, bool SKIP = true>
 __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const uint32_t* __restrict__ plan1,
                                                   const uint32_t* const* __restrict__ plans,
                                                   const uint32_t* __restrict__ seg_list,
@@ -344,12 +346,14 @@ __global__ __launch_bounds__(256) CEC_FDD_ATTR void k_fftdec_d(Layout L, const u
   });
   sfor<16>([&](auto J) CEC_FFT_AI {
     after_prev<J>(X);
-    tr8(X[J]);
+    if (!SKIP || P[FftDecDLayout::kLam + J]) {
+      tr8(X[J]);
 #ifdef CEC_FDD_BFE
-    mul_rt(X[J], P[FftDecDLayout::kLam + J] >> sh);
+      mul_rt(X[J], P[FftDecDLayout::kLam + J] >> sh);
 #else
-    mul_rt_lds(X[J], (const lds_u32*)lmask + (J * 4 + l) * 8);
+      mul_rt_lds(X[J], (const lds_u32*)lmask + (J * 4 + l) * 8);
 #endif
+    }
   });
   fence_all(X);
   ifft64<(SWZ & 1) != 0>(X, e1, e2);
@@ -589,6 +593,7 @@ bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* con
     case 8: kern = k_fftdec_d<1>; break;
     case 9: kern = k_fftdec_d<6>; break;
     case 10: kern = k_fftdec_d<0>; break;
+    case 11: kern = k_fftdec_d<0, false>; break;  // no skip of unread input slots
     default: break;
   }
 #endif

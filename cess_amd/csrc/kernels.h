@@ -95,7 +95,8 @@ bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
 // persistent kernel that merges a block's output multiplication with the next block's input
 // multiplication (k_fftdec_dp), 3 the same with wave priorities by remaining work (DESIGN.md §4:
 // 9 % fewer VALU per block, slower overall), 4..10 k_fftdec_d with other masks of the phases whose
-// quad exchanges go through the LDS crossbar (ds_swizzle) instead of DPP (fftdec_d.hip kFddSwz).
+// quad exchanges go through the LDS crossbar (ds_swizzle) instead of DPP (fftdec_d.hip kFddSwz),
+// 11 the product's without the skip of unread input slots.
 bool launch_fftdec_d(const Layout& L, const uint32_t* plan1, const uint32_t* const* plans,
                      const uint32_t* seg_list, uint32_t nseg, hipStream_t st, int form = 0);
 

@@ -221,14 +221,15 @@ def test_ct_variants_identical(torch, cess, corc, k, m, ln):
     enc.set_option(2, -1)
 
 
-@pytest.mark.parametrize("variant", [70, 72, 73, 74, 75, 76, 77, 78, 83, -1])
+@pytest.mark.parametrize("variant", [70, 72, 73, 74, 75, 76, 77, 78, 83, 85, -1])
 @pytest.mark.parametrize("nseg,ln", [(1, 4096), (3, 16384), (9, 8192)])
 def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):
     """The formal-derivative decoder's forms (tuning build): -1 one block per wave (k_fftdec_d,
     the product's), 70 the pipelined persistent kernel (k_fftdec_dp: a wave merges a block's
     output multiplication with the next block's input one), 72 the same with wave priorities, 73
     k_fftdec_d with its quad exchanges through the LDS crossbar (ds_swizzle) in every phase, 74..78
-    in some, 83 DPP in every phase through the tuning form.
+    in some, 83 DPP in every phase through the tuning form, 85 without the skip of unread input
+    slots.
     Several segments (per-segment plans), a single segment's host-API-sized batch, 12..32
     erasures: bit-exact with the oracle."""
     k = m = 32
