@@ -742,7 +742,8 @@ using cec::kFdNone;
 // 85 the product's without the skip of unread input slots (A/B sweeps)
 // tuning build: CEC_OPT_CT_VARIANT 79..82 run k_fftdec_m with pair exchanges through the LDS
 // crossbar: the IFFT's; + the FFT's last layer; + the nibble packs; all three; 84 DPP everywhere
-// (= the product's). launch_fftdec's form is 1 + that mask.
+// (= the product's). launch_fftdec's form is 1 + that mask; 86 (form 10) the product's without
+// the skip of unread input slots.
 int fdm_form(const cec_codec* c) {
   switch (c->opts.ct_variant) {
     case 79: return 2;
@@ -750,6 +751,7 @@ int fdm_form(const cec_codec* c) {
     case 81: return 6;
     case 82: return 8;
     case 84: return 1;
+    case 86: return 10;
     default: return 0;
   }
 }

@@ -94,7 +94,9 @@ typedef const __attribute__((address_space(3))) u32x4 lds_u32x4;
 
 // SWZ: which pair exchanges go through the LDS crossbar (bit 0 the IFFT's layer 0, bit 1 the FFT's
 // layer 0 on the slots read, bit 2 the nibble packs), the others through DPP
-template <unsigned SIDE, int NLO, int NHI, int LR, int SWZ>
+// SKIP: a lane-pair slot of coset A with neither position read (both erased: zeros loaded) skips
+// its transpose (zero in, zero out)
+template <unsigned SIDE, int NLO, int NHI, int LR, int SWZ, bool SKIP>
 __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64_t col,
                                            cplan_t P, lds_u32* lw) {
   constexpr unsigned BA = SIDE ? 32u : 0u, BB = SIDE ? 0u : 32u;
@@ -128,7 +130,9 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_u32*)(lw + i * 512 + 256), 16, voff + 512,
                                              soff, 0, 2);
   }
-  sfor<16>([&](auto J) CEC_FFT_AI { tr8(X[J]); });
+  sfor<16>([&](auto J) CEC_FFT_AI {
+    if (!SKIP || ((presA >> (2 * J)) & 3)) tr8(X[J]);
+  });
   ifft32<BA, (SWZ & 1) != 0>(X, em);
   // q on coset B; its last layer only on the slots whose q is read (syndrome rows R, erased
   // outputs of B: the plan's kPslots, numbered before the swaps below)
@@ -268,7 +272,7 @@ __device__ __forceinline__ void dec_m_cols(const Layout& L, uint32_t seg, uint64
 // the crossbar is no faster one form per process (profiles/r04/swz_standalone_runs.jsonl), the
 // nibble packs through it take the small class past 168 VGPRs.
 constexpr int kFdmSwz = 0;
-template <unsigned SIDE, bool BIG, int SWZ>
+template <unsigned SIDE, bool BIG, int SWZ, bool SKIP = true>
 __global__ __launch_bounds__(256) CEC_FD_ATTR void k_fftdec_m(Layout L, const uint32_t* __restrict__ plan1,
                                                   const uint32_t* const* __restrict__ plans,
                                                   const uint32_t* __restrict__ seg_list,
@@ -281,7 +285,7 @@ __global__ __launch_bounds__(256) CEC_FD_ATTR void k_fftdec_m(Layout L, const ui
   const uint64_t col = (gp >> 5) * 1024 + (gp & 31) * 16;
   __shared__ __attribute__((aligned(16))) uint32_t lds[4 * LR * 512];
   if (col >= L.len) return;  // whole waves leave together
-  dec_m_cols<SIDE, NLO, NHI, LR, SWZ>(L, seg, col, (cplan_t)P,
+  dec_m_cols<SIDE, NLO, NHI, LR, SWZ, SKIP>(L, seg, col, (cplan_t)P,
                                  (lds_u32*)(lds + (threadIdx.x >> 6) * (LR * 512)));
 }
 
@@ -315,6 +319,10 @@ bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
     case 4: pick(std::integral_constant<int, 3>{}); break;
     case 6: pick(std::integral_constant<int, 5>{}); break;
     case 8: pick(std::integral_constant<int, 7>{}); break;
+    case 10:  // the product's without the skip of unread slots
+      kern = side ? (big ? k_fftdec_m<1, true, 0, false> : k_fftdec_m<1, false, 0, false>)
+                  : (big ? k_fftdec_m<0, true, 0, false> : k_fftdec_m<0, false, 0, false>);
+      break;
     default: break;
   }
 #else

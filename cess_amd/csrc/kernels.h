@@ -86,7 +86,8 @@ bool launch_fft_rs3232_verify(const Layout& L, uint8_t* ok, uint32_t nseg, hipSt
 bool fftdec_layout_ok(const Layout& L);
 bool fftdec_big(int nrs);
 // form 0: the product's (every pair exchange through DPP); tuning build only: 1 + a mask of the
-// exchanges through the LDS crossbar (bit 0 the IFFT's, 1 the FFT's last layer, 2 the nibble packs).
+// exchanges through the LDS crossbar (bit 0 the IFFT's, 1 the FFT's last layer, 2 the nibble packs),
+// 10 the product's without the skip of unread input slots.
 bool launch_fftdec(const Layout& L, int side, bool big, const uint32_t* plan1,
                    const uint32_t* const* plans, const uint32_t* seg_list, uint32_t nseg,
                    hipStream_t st, int form = 0);

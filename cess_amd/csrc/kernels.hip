@@ -1394,7 +1394,7 @@ void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_
 }  // namespace
 
 #ifdef CEC_TUNING
-int max_ct_variant() { return 85; }  // 70, 72..78, 83, 85: the derivative decoder forms, 79..82, 84 the syndrome-row decoder's (cess_ec.cpp fdd_form)
+int max_ct_variant() { return 86; }  // 70, 72..78, 83, 85: the derivative decoder forms, 79..82, 84, 86 the syndrome-row decoder's (cess_ec.cpp fdd_form)
 #else
 int max_ct_variant() { return 0; }
 #endif

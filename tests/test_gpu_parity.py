@@ -252,7 +252,7 @@ def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):
     assert np.array_equal(d_par.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("variant", [79, 80, 81, 82, 84, -1])
+@pytest.mark.parametrize("variant", [79, 80, 81, 82, 84, 86, -1])
 @pytest.mark.parametrize("nseg,ln,lo,hi", [(1, 4096, 4, 8), (5, 16384, 4, 16), (9, 8192, 9, 20)])
 def test_fftdec_m_forms_identical(torch, cess, corc, variant, nseg, ln, lo, hi):
     """The syndrome-row decoder's forms (tuning build): -1 the product's (DPP exchanges), 79..82
