@@ -19,7 +19,8 @@ def main(src: str, dst: str) -> None:
            "steps": None, "ms": {}}
     for i in range(0, len(rows), len(legs)):
         group = rows[i:i + len(legs)]
-        e = int(re.search(r"(\d+) random erasures", group[0]["config"]["workload"]).group(1))
+        e = int(re.search(r"(\d+) (?:random|consecutive) erasures",
+                          group[0]["config"]["workload"]).group(1))
         cfg = group[0]["config"]
         out["fragment_bytes"] = cfg["fragment_bytes"]
         out["segments"] = cfg["segments_per_gpu"]
