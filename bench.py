@@ -68,6 +68,10 @@ CONFIGS = {
 }
 
 
+# exit status of a run whose C-ABI exchange legs stalled (cabi_legs' watchdog): the line is
+# printed, but the process does not report success
+WATCHDOG_EXIT = 3
+
 GPU_BOX_CPU_SHARE = 16  # CPUs the harness gives one GPU's job on the box (its pools obey this)
 
 
@@ -396,7 +400,8 @@ def cabi_legs(ex_out, gather_leg, degraded_gather, enc, code, world, rank, dev, 
     RS(32,32) both exchanges. They run last, after every other measurement, under a watchdog: a
     rank that fails or stalls inside the collective exchange would otherwise hold every rank in
     it, so past `deadline` seconds each rank records the legs as not finished, rank 0 prints the
-    line it has (`emit`), and the process ends (os._exit: the peers are stuck in RCCL)."""
+    line it has (`emit`), and the process ends with status WATCHDOG_EXIT (os._exit: the peers are
+    stuck in RCCL), so the driver's rc records that a rank hung while the line stays parseable."""
     import threading
     import torch
     import torch.distributed as dist
@@ -415,7 +420,10 @@ def cabi_legs(ex_out, gather_leg, degraded_gather, enc, code, world, rank, dev, 
                                              "or stalled inside the cec_dist exchange)"}
             emit()
         finally:
-            os._exit(0)
+            if rank != 0:
+                # a failing rank makes torchrun stop the others: give rank 0 time to print first
+                time.sleep(10)
+            os._exit(WATCHDOG_EXIT)
 
     threading.Thread(target=watchdog, daemon=True).start()
     transport = "libcessec cec_dist_degraded_read (own RCCL communicator)"
@@ -685,10 +693,138 @@ def config5_leg(dev, local, W: int = 96, warmup: int = 10, sample: int = 48) -> 
     return out
 
 
+def oracle_sample_check(d_data, d_par, rows, seg0: int, k: int, m: int, F: int, seed: int) -> bool:
+    """The checker (test infrastructure, after the timed region): the sampled segments' data equal
+    the counter generator's bytes and their parity equals the C oracle's encode
+    (oracle/rs_oracle.c), byte for byte. rows = batch rows; seg0 + row = the file's segment."""
+    from oracle.c_oracle import load_c_oracle
+    orc = load_c_oracle()
+    got_d = d_data[rows].cpu().numpy()
+    got_p = d_par[rows].cpu().numpy()
+    want_d = np.empty((len(rows), k, F), np.uint8)
+    want_p = np.empty((len(rows), m, F), np.uint8)
+    for i, r in enumerate(rows):
+        orc.orc_fill_synthetic(want_d[i].ctypes.data, k * F, 1, seg0 + int(r), seed)
+    orc.orc_encode_batch(k, m, want_d.ctypes.data, want_p.ctypes.data, len(rows), F,
+                         cpu_threads(), 1)
+    return bool(np.array_equal(got_d, want_d) and np.array_equal(got_p, want_p))
+
+
+def config4_leg(dev, local: int, world: int, rank: int, backend: str, reps: int = 10) -> dict:
+    """BASELINE config 4's encode at every N, inside the default line: the 64 GiB file (4096 x
+    16 MiB segments, RS(2,1)) sharded contiguously over the ranks, 4096 / N segments per GPU, one
+    batched encode launch per GPU per pass. T1 = the whole file encoded by one GPU (rank 0, in
+    this process, every other rank waiting), T_N = the max over ranks of the per-pass time of the
+    sharded encode, efficiency = T1 / (N T_N). Both are HIP-event means over
+    `reps` back-to-back passes on the launch stream (host clock, barrier to barrier, beside
+    them). Sampled segments of every pass buffer are checked against the C oracle afterwards.
+    Buffers are freed before the later legs. Segment placement: contiguous shards, the encode
+    half of c-pallets/file-bank/src/functions.rs:187-283 (segments are independent: no collective
+    on the data path)."""
+    import torch
+    import torch.distributed as dist
+    import cess_amd
+    k, m, F = CONFIGS[4][:3]
+    total = CONFIGS[4][3]
+    seed = SEED0 + 4
+    per_seg = (k + m) * F
+    stream = torch.cuda.current_stream(dev)
+    enc = cess_amd.New(k, m, device=local)
+    shared = "CESS_DEVICE" in os.environ  # ranks share one GPU (rehearsal)
+
+    def reduce_max(vals):
+        if world == 1:
+            return vals
+        t = torch.tensor(vals, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(x) for x in t]
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def encode_pass(seg0: int, nseg: int, timed_alone: bool):
+        """Allocate + fill nseg segments from seg0, encode reps times; (event ms, host ms, ok)."""
+        free, _ = torch.cuda.mem_get_info(dev)
+        if free < nseg * per_seg + (1 << 30):
+            return None
+        d_data = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
+        d_par = torch.empty((nseg, m, F), dtype=torch.uint8, device=dev)
+        cess_amd.fill_synthetic(d_data, k * F, nseg, seg0, seed, stream=stream)
+        for _ in range(2):
+            enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
+        torch.cuda.synchronize(dev)
+        if not timed_alone:
+            barrier()
+        torch.cuda.synchronize(dev)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        a.record(stream)
+        for _ in range(reps):
+            enc.EncodeBatch(d_data, d_par, nseg, F, stream=stream)
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        if not timed_alone:
+            barrier()
+        host_ms = (time.perf_counter() - t0) * 1e3 / reps
+        ev_ms = a.elapsed_time(b) / reps
+        rows = sorted({0, 1, nseg // 3, nseg // 2, (2 * nseg) // 3, nseg - 2, nseg - 1} &
+                      set(range(nseg)))
+        ok = oracle_sample_check(d_data, d_par, rows, seg0, k, m, F, seed)
+        del d_data, d_par
+        torch.cuda.empty_cache()
+        return ev_ms, host_ms, ok, len(rows)
+
+    out = {"workload": f"64 GiB file = {total} x 16 MiB segments, RS({k},{m}), F = 8 MiB, "
+                       f"contiguous shard of {total // world} segments per GPU (one batched "
+                       f"encode launch per GPU per pass)",
+           "segments_total": total, "file_bytes": total * k * F,
+           "algorithmic_bytes_per_pass": total * per_seg, "n_gpus": world, "reps": reps,
+           "scaling": "strong (fixed 64 GiB file)"}
+    # T1: the whole file on one GPU (rank 0), the other ranks waiting
+    t1 = encode_pass(0, total, True) if rank == 0 else None
+    barrier()
+    # T_N: every rank its contiguous shard (the general split also covers N not dividing 4096)
+    s0, s1 = total * rank // world, total * (rank + 1) // world
+    if world == 1:
+        tn = t1
+    else:
+        tn = encode_pass(s0, s1 - s0, False)
+    mine_ok = tn is not None and tn[2]
+    vals = reduce_max([tn[0] if tn else float("inf"), tn[1] if tn else float("inf"),
+                       0.0 if mine_ok else 1.0])
+    enc.close()
+    if t1 is not None:
+        out.update({"t1_ms": round(t1[0], 4), "t1_host_ms": round(t1[1], 4),
+                    "t1_GBps": round(total * per_seg / (t1[0] * 1e-3) / GB, 1),
+                    "t1_segments_checked": t1[3], "t1_bit_exact_sampled": t1[2]})
+    elif rank == 0:
+        out["t1_skipped"] = "not enough free HBM for the whole file on one GPU"
+    if vals[0] == float("inf"):
+        out["error"] = "a rank could not hold its shard"
+        return out
+    tn_ms, tn_host_ms, bad = vals
+    out.update({"tN_ms": round(tn_ms, 4), "tN_host_ms": round(tn_host_ms, 4),
+                "whole_file_GBps": round(total * per_seg / (tn_ms * 1e-3) / GB, 1),
+                "per_gpu_GBps": round(total * per_seg / (tn_ms * 1e-3) / GB / world, 1),
+                "bit_exact_sampled": not bad and (t1 is None or t1[2]),
+                "segments_checked_per_rank": tn[3],
+                "checker": "C oracle (oracle/rs_oracle.c) on sampled segments of every shard, "
+                           "after the timed passes"})
+    if t1 is not None:
+        out["efficiency"] = round(t1[0] / (world * tn_ms), 4)
+        out["efficiency_basis"] = "T1 / (N x T_N), HIP-event times per pass, T_N max over ranks"
+    if shared and world > 1:
+        out["note"] = ("ranks share one GPU (CESS_DEVICE rehearsal): T_N and the efficiency "
+                       "measure contention on one device, not scaling")
+    return out
+
+
 def line_problems(out: dict) -> list:
     """What a bench line lacks against the driver's contract and VERDICT's asks (empty = none):
     the contract keys, `roofline` and `cpu_baseline` at every N (at N > 1 on the CPU share of the
-    GPUs held), and for the default config: at N = 1 the config-5 step with checked digests and
+    GPUs held), and for the default config: config 4's 64 GiB strong-scaling encode (T_N, T1,
+    efficiency, sampled segments bit-exact) at every N; at N = 1 the config-5 step with checked digests and
     the wide-code legs with their cold means; at N > 1 both degraded-read transports (the torch
     group and libcessec's own RCCL communicator, or the reason it could not form) bit-exact."""
     bad = []
@@ -712,6 +848,11 @@ def line_problems(out: dict) -> list:
     if (out.get("config") or {}).get("baseline_config") != 2 or "extra" not in out:
         return bad
     ex = out["extra"]
+    c4 = ex.get("config4") or {}
+    if not c4.get("bit_exact_sampled") or not c4.get("tN_ms"):
+        bad.append("extra.config4 missing, unmeasured or not bit-exact")
+    elif "efficiency" not in c4:
+        bad.append("extra.config4 lacks T1 / efficiency")
     if n == 1:
         c5 = ex.get("config5") or {}
         if not c5.get("digests_match_hashlib") or not c5.get("step_GBps"):
@@ -1144,6 +1285,11 @@ def main() -> None:
                 "xgmi_GBps_per_link": 153,
                 "backend": (backend if world > 1 else "local (one GPU: no bytes move)"),
                 "bit_exact": not bad}
+
+    if not args.no_extra and args.config == 2:
+        # BASELINE config 4's strong-scaling encode (64 GiB over the N GPUs, T1 on one GPU beside
+        # it) at every N: the driver only ever runs the default command
+        out.setdefault("extra", {})["config4"] = config4_leg(dev, local, world, rank, backend)
 
     cabi_pending = False
     if args.config == 4:

@@ -261,6 +261,11 @@ int cec_dist_unique_id(uint8_t* id /* CEC_DIST_ID_BYTES */);
 /* Join the group as `rank` of `world` on the codec's device. Collective: every rank calls it
  * with the same id. The group keeps using `codec` until cec_dist_destroy. */
 int cec_dist_create(cec_codec* codec, const uint8_t* id, int world, int rank, cec_dist** out);
+/* Leave the group and free the handle. The handle's own teardown waits for its last degraded
+ * read only, but RCCL's ncclCommDestroy, which it calls, drains the WHOLE device: every stream of
+ * every codec on this GPU stalls until its queued work is done (measured: a 25 ms batch on an
+ * unrelated stream finished inside the destroy, profiles/r04/destroy_report_c.log). Destroy dist
+ * handles only when the device is idle (at shutdown, or between batches), never mid-traffic. */
 void cec_dist_destroy(cec_dist* d);
 /* One transfer of a plan. kind CEC_DIST_SURVIVOR: fragment `frag` of segment `seg` from rank src
  * to rank dst (src == dst: already local). kind CEC_DIST_PARTIAL: rank src's partial rebuild of

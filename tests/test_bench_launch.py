@@ -89,11 +89,28 @@ def _line(n, **extra):
     return line
 
 
+C4 = {"tN_ms": 2.1, "t1_ms": 16.4, "efficiency": 0.97, "bit_exact_sampled": True}
+
+
+def test_line_keys_config4():
+    """Config 4's 64 GiB strong-scaling encode is in the default line at every N, bit-exact on
+    its sampled segments, with T1 and the efficiency."""
+    for n in (1, 8):
+        assert not any("config4" in p for p in bench.line_problems(_line(n, extra={"config4": C4})))
+        gone = bench.line_problems(_line(n, extra={}))
+        assert "extra.config4 missing, unmeasured or not bit-exact" in gone
+        wrong = bench.line_problems(_line(n, extra={"config4": dict(C4, bit_exact_sampled=False)}))
+        assert "extra.config4 missing, unmeasured or not bit-exact" in wrong
+        no_t1 = {k: v for k, v in C4.items() if k != "efficiency"}
+        assert "extra.config4 lacks T1 / efficiency" in bench.line_problems(
+            _line(n, extra={"config4": no_t1}))
+
+
 def test_line_keys_multi_gpu():
     """The N > 1 default line must carry cpu_baseline at the node's CPU share and both
     degraded-read transports (torch group, libcessec's own RCCL communicator) bit-exact."""
     ok_leg = {"bit_exact": True, "gather_GBps": 1.0}
-    extra = {"degraded_gather": ok_leg, "degraded_gather_cabi": ok_leg,
+    extra = {"config4": C4, "degraded_gather": ok_leg, "degraded_gather_cabi": ok_leg,
              "wide_degraded_gather": {"survivors": ok_leg, "partials": ok_leg},
              "wide_degraded_gather_cabi": {"survivors": ok_leg, "partials": ok_leg}}
     assert bench.line_problems(_line(8, extra=extra)) == []
@@ -120,7 +137,7 @@ def test_line_keys_multi_gpu():
 def test_line_keys_one_gpu():
     """The N = 1 default line carries config 5's step with checked digests and the wide-code
     legs with their cold means."""
-    extra = {"config5": {"step_GBps": 1300.0, "digests_match_hashlib": True},
+    extra = {"config4": C4, "config5": {"step_GBps": 1300.0, "digests_match_hashlib": True},
              "wide_code": {"encode": {"ms": 0.37, "cold_ms_first30": 0.38}}}
     assert bench.line_problems(_line(1, extra=extra)) == []
     assert bench.line_problems(_line(1, extra=dict(extra, config5={"step_GBps": 1.0})))
@@ -128,13 +145,13 @@ def test_line_keys_one_gpu():
     assert bench.line_problems(_line(1, extra=cold_less)) == ["wide_code.encode lacks its cold mean"]
 
 
-@pytest.mark.parametrize("name", ["bench_default_a.json", "bench_gpus2_gloo_one_gpu_a.json"])
+@pytest.mark.parametrize("name", ["bench_default_a.json"])
 def test_recorded_lines_have_every_key(name):
-    """The lines this round's GPU runs printed (profiles/r04/): the N = 1 default line and the
+    """The lines this round's GPU runs printed (profiles/r05/): the N = 1 default line and the
     one-GPU rehearsal of the N = 2 line (two gloo ranks sharing GPU 0) carry everything
     line_problems() asks for."""
     import json
-    path = os.path.join(ROOT, "profiles", "r04", name)
+    path = os.path.join(ROOT, "profiles", "r05", name)
     with open(path) as f:
         line = json.load(f)
     assert bench.line_problems(line) == []
@@ -148,7 +165,8 @@ def test_recorded_lines_have_every_key(name):
 def test_cabi_legs_watchdog_ends_a_stalled_exchange(tmp_path):
     """bench.cabi_legs (the C-ABI exchange legs of the N > 1 line, run last): an exchange that
     never returns (a peer stuck in RCCL) does not cost the line. Past the deadline the legs are
-    recorded as not finished, the line is printed, and the process exits 0."""
+    recorded as not finished, the line is printed, and the process exits with
+    bench.WATCHDOG_EXIT (3: a rank hung in RCCL; the driver's rc records it)."""
     import subprocess
     import sys
     script = tmp_path / "stall.py"
@@ -164,7 +182,7 @@ def test_cabi_legs_watchdog_ends_a_stalled_exchange(tmp_path):
         "                torch.device('cpu'), 2.0, lambda: print(json.dumps(out), flush=True))\n"
         "print('not reached')\n")
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stderr
+    assert r.returncode == bench.WATCHDOG_EXIT == 3, r.stderr
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1 and "not reached" not in r.stdout, r.stdout
     ex = json.loads(lines[0])["extra"]
