@@ -102,6 +102,7 @@ SIGNATURES = {
                                  c_size_t, POINTER(DistMove), c_size_t, POINTER(c_size_t),
                                  POINTER(c_int32)]),
     "cec_dist_set_option": (c_int, [c_void_p, c_int, c_int]),
+    "cec_dist_groups": (c_int, [c_void_p, POINTER(c_uint64)]),
     "cec_dist_degraded_read": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint8), c_size_t,
                                        c_size_t, LOCATE_FN, c_void_p, POINTER(c_void_p), c_void_p,
                                        POINTER(c_size_t)]),
@@ -160,6 +161,7 @@ CEC_DIST_SURVIVOR = 0
 CEC_DIST_PARTIAL = 1
 CEC_DIST_OPT_EXCHANGE = 1
 CEC_DIST_OPT_TEST_ABORT = 2
+CEC_DIST_OPT_GROUP_OPS = 3
 
 _libs = {}
 

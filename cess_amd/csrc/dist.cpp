@@ -177,6 +177,8 @@ struct cec_dist {
   int* d_flag = nullptr;
   bool broken = false;  // the communicator was aborted after a failure inside a transfer group
   int test_abort_round = -1;  // CEC_DIST_OPT_TEST_ABORT: fail inside this round's transfer group
+  int group_ops = 1024;       // CEC_DIST_OPT_GROUP_OPS: point-to-point ops per rank per group
+  uint64_t groups = 0;        // transfer groups issued (cec_dist_groups)
   // Device memory is stream-ordered (hipMallocAsync / hipFreeAsync): hipFree performs an implicit
   // hipDeviceSynchronize, which would stall every other codec on the device. `done` is recorded on
   // the caller's stream at the end of every degraded read (its last enqueued work); destruction
@@ -298,7 +300,18 @@ int cec_dist_set_option(cec_dist* d, int option, int value) {
     d->test_abort_round = value < 0 ? -1 : value;
     return CEC_OK;
   }
+  if (option == CEC_DIST_OPT_GROUP_OPS) {
+    if (value < 0) return cec::set_error(CEC_EINVAL, "group ops must be >= 0");
+    d->group_ops = value;
+    return CEC_OK;
+  }
   return cec::set_error(CEC_EINVAL, "unknown dist option");
+}
+
+int cec_dist_groups(const cec_dist* d, uint64_t* groups) {
+  if (!d || !groups) return cec::set_error(CEC_EINVAL, "null dist or output");
+  *groups = d->groups;
+  return CEC_OK;
 }
 
 int cec_dist_plan(int k, int m, int world, const uint64_t* lost_seg, const uint8_t* lost_frag,
@@ -537,9 +550,43 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
       for (const Seg* g : pmine) ragged |= g->decoder == rank && g->holders.size() < H;
       if (ragged && !lrc) hip_ok(hipMemsetAsync(acc + acc_row, 0, H * acc_row, st), "memset");
     }
-    // one group: survivor moves, then partials, each in plan order (pairs every send with its
-    // receive on the peer)
-    NC_TRY(r.group_start());
+    // Transfer groups of at most d->group_ops point-to-point ops on any one rank
+    // (CEC_DIST_OPT_GROUP_OPS; a wide code's round is up to ~7k ops otherwise): the round's
+    // segments are cut at the same plan positions on every rank (each computes every rank's counts
+    // from the shared plan), so a group holds both ends of each of its transfers and no group
+    // waits on another rank's later group. Within a group: survivor moves, then partials, each in
+    // plan order (which pairs every send with its receive on the peer). The groups follow each
+    // other on the stream with no host synchronisation.
+    std::vector<size_t> cuts{r0};
+    if (d->group_ops > 0) {
+      std::vector<size_t> cnt(world, 0), one(world, 0);
+      for (size_t i = r0; i < r1; ++i) {
+        const Seg& g = plan[i];
+        std::fill(one.begin(), one.end(), 0);
+        if (g.partial) {
+          for (int h : g.holders) {
+            one[h] += g.lost.size();
+            one[g.decoder] += g.lost.size();
+          }
+        } else {
+          for (int f : g.surv) {
+            const int o = owner(g.seg, f, world);
+            if (o != g.decoder) {
+              ++one[o];
+              ++one[g.decoder];
+            }
+          }
+        }
+        bool over = false;
+        for (int w = 0; w < world; ++w) over |= cnt[w] + one[w] > (size_t)d->group_ops;
+        if (over && i > cuts.back()) {
+          cuts.push_back(i);
+          std::fill(cnt.begin(), cnt.end(), 0);
+        }
+        for (int w = 0; w < world; ++w) cnt[w] += one[w];
+      }
+    }
+    cuts.push_back(r1);
     size_t rj = 0;
     auto fail = [&](ncclResult_t res, const char* what) {
       // end the half-built group (this thread's group state is then clean; what was enqueued is
@@ -552,42 +599,47 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
       d->broken = true;
       return code;
     };
-    if (d->test_abort_round == (int)(r0 / kRound))
-      return fail(ncclInternalError, "test abort (CEC_DIST_OPT_TEST_ABORT)");
-    for (size_t i = r0; i < r1; ++i) {
-      const Seg& g = plan[i];
-      for (int f : g.surv) {
-        const int src = owner(g.seg, f, world);
-        if (src == rank) {
-          const uint8_t* p = round_src[rj++];
-          if (!g.partial && g.decoder != rank) {
-            ncclResult_t res = r.send(p, F, ncclUint8, g.decoder, d->comm, st);
-            if (res != ncclSuccess) return fail(res, "ncclSend");
-          }
-        } else if (!g.partial && g.decoder == rank) {
-          ncclResult_t res = r.recv(slot(g.seg, f), F, ncclUint8, src, d->comm, st);
-          if (res != ncclSuccess) return fail(res, "ncclRecv");
-        }
-      }
-    }
-    for (const Seg* g : pmine) {
-      if (g->decoder == rank) {
-        for (size_t h = 0; h < g->holders.size(); ++h)
-          for (int f : g->lost) {
-            ncclResult_t res = r.recv(acc + (h + 1) * acc_row + R.pair.at({g->seg, f}) * F, F,
-                                      ncclUint8, g->holders[h], d->comm, st);
+    auto pit = pmine.begin();
+    for (size_t c = 0; c + 1 < cuts.size(); ++c) {
+      const size_t c0 = cuts[c], c1 = cuts[c + 1];
+      NC_TRY(r.group_start());
+      if (c == 0 && d->test_abort_round == (int)(r0 / kRound))
+        return fail(ncclInternalError, "test abort (CEC_DIST_OPT_TEST_ABORT)");
+      for (size_t i = c0; i < c1; ++i) {
+        const Seg& g = plan[i];
+        for (int f : g.surv) {
+          const int src = owner(g.seg, f, world);
+          if (src == rank) {
+            const uint8_t* p = round_src[rj++];
+            if (!g.partial && g.decoder != rank) {
+              ncclResult_t res = r.send(p, F, ncclUint8, g.decoder, d->comm, st);
+              if (res != ncclSuccess) return fail(res, "ncclSend");
+            }
+          } else if (!g.partial && g.decoder == rank) {
+            ncclResult_t res = r.recv(slot(g.seg, f), F, ncclUint8, src, d->comm, st);
             if (res != ncclSuccess) return fail(res, "ncclRecv");
           }
-      } else {
-        for (int f : g->lost) {
-          ncclResult_t res = r.send(pslot(g->seg, f), F, ncclUint8, g->decoder, d->comm, st);
-          if (res != ncclSuccess) return fail(res, "ncclSend");
         }
       }
-    }
-    {
+      for (; pit != pmine.end() && (size_t)(*pit - plan.data()) < c1; ++pit) {
+        const Seg* g = *pit;
+        if (g->decoder == rank) {
+          for (size_t h = 0; h < g->holders.size(); ++h)
+            for (int f : g->lost) {
+              ncclResult_t res = r.recv(acc + (h + 1) * acc_row + R.pair.at({g->seg, f}) * F, F,
+                                        ncclUint8, g->holders[h], d->comm, st);
+              if (res != ncclSuccess) return fail(res, "ncclRecv");
+            }
+        } else {
+          for (int f : g->lost) {
+            ncclResult_t res = r.send(pslot(g->seg, f), F, ncclUint8, g->decoder, d->comm, st);
+            if (res != ncclSuccess) return fail(res, "ncclSend");
+          }
+        }
+      }
       ncclResult_t res = r.group_end();
       if (res != ncclSuccess) return fail(res, "ncclGroupEnd");
+      ++d->groups;
     }
     if (!mine.empty()) {
       // every fragment not lost is flagged present (the codec reads its k survivors, the gathered

@@ -361,6 +361,22 @@ class RcclGroup:
         check(self._lib.cec_dist_set_option(self._h, _lib.CEC_DIST_OPT_TEST_ABORT, round_index),
               "cec_dist_set_option")
 
+    def set_group_ops(self, n: int) -> None:
+        """CEC_DIST_OPT_GROUP_OPS: at most n point-to-point transfers on any rank per RCCL group
+        (default 1024; 0 = one group per round of 256 segments). Same value on every rank."""
+        from . import _lib
+        from .reedsolomon import check
+        check(self._lib.cec_dist_set_option(self._h, _lib.CEC_DIST_OPT_GROUP_OPS, n),
+              "cec_dist_set_option")
+
+    def groups(self) -> int:
+        """Transfer groups this handle has issued (cec_dist_groups)."""
+        from ctypes import byref, c_uint64
+        from .reedsolomon import check
+        g = c_uint64()
+        check(self._lib.cec_dist_groups(self._h, byref(g)), "cec_dist_groups")
+        return g.value
+
     def close(self) -> None:
         if self._h:
             self._lib.cec_dist_destroy(self._h)

@@ -289,7 +289,14 @@ typedef struct cec_dist_move {
  * an RCCL error there would (the group is ended and the communicator aborted, so peers get an
  * error instead of waiting; later calls on the handle return CEC_ENCCL). -1 = off (default). */
 #define CEC_DIST_OPT_TEST_ABORT 2
+/* At most `value` point-to-point transfers on any one rank per RCCL group (default 1024; 0 = one
+ * group per round of 256 segments, up to ~7k transfers for RS(32,32)). A round is cut into groups
+ * at the same plan positions on every rank, so every group holds both ends of its transfers; the
+ * groups are enqueued back to back with no host synchronisation. */
+#define CEC_DIST_OPT_GROUP_OPS 3
 int cec_dist_set_option(cec_dist* d, int option, int value);
+/* Transfer groups this handle has issued (diagnostic: the group split of CEC_DIST_OPT_GROUP_OPS). */
+int cec_dist_groups(const cec_dist* d, uint64_t* groups);
 /* Host only: the plan a degraded read of the lost list runs. The list holds nlost (segment,
  * fragment) erasures, any order, duplicates allowed, at most m distinct per segment
  * (CEC_ETOOFEW otherwise; CEC_EINVAL for an index >= k+m). Writes the moves in issue order

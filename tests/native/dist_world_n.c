@@ -10,10 +10,11 @@
  * restoral (c-pallets/file-bank/src/lib.rs:943-1122). Every rebuilt fragment is compared with the
  * C oracle's codeword (oracle/rs_oracle.c: the checker, test infrastructure only).
  *
- * usage: dist_world_n WORLD K M NSEG F EXCHANGE ABORT_RANK
+ * usage: dist_world_n WORLD K M NSEG F EXCHANGE ABORT_RANK [GROUP_OPS]
  *   EXCHANGE 0 survivors, 1 partials, 2 auto; ABORT_RANK -1 = none, else that rank fails inside
  *   round 0's transfer group (CEC_DIST_OPT_TEST_ABORT), then every rank joins a fresh group;
  *   -2 = host only: print the plan's shape (and whether the stand-in was loaded), no GPU.
+ *   GROUP_OPS: CEC_DIST_OPT_GROUP_OPS (transfers per rank per RCCL group; default: the library's).
  * prints one line "world_n ok ..." on success, "FAIL ..." lines otherwise (exit 1). */
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
@@ -32,7 +33,7 @@ double orc_encode_batch(int k, int m, const uint8_t* data, uint8_t* parity, size
 #define SEED 0xCE550004ull
 #define ROUND 256 /* dist.cpp kRound */
 
-static int W, K, M, N, EXCH, ABORT_RANK;
+static int W, K, M, N, EXCH, ABORT_RANK, GROUP_OPS = -1;
 static size_t NSEG, F, NLOST;
 static uint8_t *h_data, *h_par;   /* the codewords: [seg][k][F], [seg][m][F] */
 static uint64_t* lost_seg;
@@ -52,6 +53,7 @@ typedef struct {
   long long* slot;  /* [seg][n] index into d_store, -1 = not held */
   int rc_first, rc_abort_retry;
   size_t rebuilt, bad;
+  uint64_t groups;
   char why[256];
 } rank_t;
 
@@ -85,6 +87,7 @@ static int one_read(rank_t* r, cec_codec* c, const uint8_t* id, int abort_round,
   RCHECK(cec_dist_create(c, id, W, r->rank, &d) == CEC_OK);
   RCHECK(cec_dist_set_option(d, CEC_DIST_OPT_EXCHANGE, EXCH) == CEC_OK);
   if (abort_round >= 0) RCHECK(cec_dist_set_option(d, CEC_DIST_OPT_TEST_ABORT, abort_round) == 0);
+  if (GROUP_OPS >= 0) RCHECK(cec_dist_set_option(d, CEC_DIST_OPT_GROUP_OPS, GROUP_OPS) == 0);
   uint8_t* d_out = NULL;
   size_t mine = 0;
   for (size_t i = 0; i < NLOST; ++i) mine += decoder[i] == r->rank;
@@ -116,7 +119,10 @@ static int one_read(rank_t* r, cec_codec* c, const uint8_t* id, int abort_round,
         }
       }
       free(got);
-      if (pass == 0) r->rebuilt = nrebuilt;
+      if (pass == 0) {
+        r->rebuilt = nrebuilt;
+        RCHECK(cec_dist_groups(d, &r->groups) == CEC_OK);
+      }
       if (mine) RCHECK(hipMemsetAsync(d_out, 0x5A, mine * F, st) == hipSuccess);
     }
   }
@@ -181,10 +187,11 @@ static void* rank_main(void* arg) {
 }
 
 int main(int argc, char** argv) {
-  if (argc != 8) {
-    fprintf(stderr, "usage: %s WORLD K M NSEG F EXCHANGE ABORT_RANK\n", argv[0]);
+  if (argc != 8 && argc != 9) {
+    fprintf(stderr, "usage: %s WORLD K M NSEG F EXCHANGE ABORT_RANK [GROUP_OPS]\n", argv[0]);
     return 2;
   }
+  if (argc == 9) GROUP_OPS = atoi(argv[8]);
   W = atoi(argv[1]);
   K = atoi(argv[2]);
   M = atoi(argv[3]);
@@ -292,7 +299,7 @@ int main(int argc, char** argv) {
   const int standin = memcmp(id1, "cess-rccl-standin", 17) == 0;
   if (ABORT_RANK == -2) { /* host only: the plan and which librccl libcessec loaded */
     printf("plan world %d RS(%d,%d) nseg %zu lost %zu rounds %zu survivor_moves %zu "
-           "partial_moves %zu max_ops_per_rank_group %zu ragged %d standin %d\n", W, K, M, NSEG,
+           "partial_moves %zu max_ops_per_rank_round %zu ragged %d standin %d\n", W, K, M, NSEG,
            NLOST, rounds, nsurv, npartial, max_ops, ragged, standin);
     return 0;
   }
@@ -318,15 +325,21 @@ int main(int argc, char** argv) {
       fail = 1;
     }
   }
+  for (int i = 1; i < W && ABORT_RANK < 0; ++i)
+    if (rk[i].groups != rk[0].groups) {
+      fprintf(stderr, "FAIL rank %d issued %llu transfer groups, rank 0 %llu\n", i,
+              (unsigned long long)rk[i].groups, (unsigned long long)rk[0].groups);
+      fail = 1;
+    }
   if (ABORT_RANK < 0 && rebuilt != NLOST) {
     fprintf(stderr, "FAIL rebuilt %zu of %zu lost fragments\n", rebuilt, NLOST);
     fail = 1;
   }
   if (fail) return 1;
   printf("world_n ok world %d RS(%d,%d) nseg %zu F %zu exchange %d lost %zu rebuilt %zu rounds %zu "
-         "survivor_moves %zu partial_moves %zu max_ops_per_rank_group %zu ragged %d standin %d",
-         W, K, M, NSEG, F, EXCH, NLOST, rebuilt, rounds, nsurv, npartial, max_ops, ragged,
-         standin);
+         "survivor_moves %zu partial_moves %zu max_ops_per_rank_round %zu ragged %d standin %d "
+         "groups %llu", W, K, M, NSEG, F, EXCH, NLOST, rebuilt, rounds, nsurv, npartial, max_ops,
+         ragged, standin, (unsigned long long)rk[0].groups);
   if (ABORT_RANK >= 0) {
     printf(" abort_rank %d first_rc", ABORT_RANK);
     for (int i = 0; i < W; ++i) printf(" %d", rk[i].rc_first);

@@ -68,21 +68,26 @@ def test_standin_exports_what_dist_resolves(standin):
     assert names <= have, names - have
 
 
-# world, k, m, segments, F, exchange (0 survivors, 1 partials, 2 auto), abort rank (-1 none)
+# world, k, m, segments, F, exchange (0 survivors, 1 partials, 2 auto), abort rank (-1 none),
+# transfers per rank per RCCL group (CEC_DIST_OPT_GROUP_OPS; -1 = the library default, 1024)
 CASES = [
-    (2, 2, 1, 12, (1 << 20) + 64, 0, -1),
-    (3, 2, 1, 12, (1 << 20) + 64, 0, -1),
-    (8, 2, 1, 64, 1 << 16, 0, -1),
-    (4, 4, 2, 40, (1 << 16) + 64, 1, -1),   # ragged holder counts on one decoder
-    (8, 10, 4, 24, 1 << 16, 2, -1),          # auto: survivors and partials in one group
-    (8, 32, 32, 12, 1 << 16, 0, -1),
-    (3, 32, 32, 12, 1 << 16, 1, -1),
-    (2, 32, 32, 300, 4096, 0, -1),           # two rounds, ~4.2k ops in one rank's group
-    (3, 32, 32, 300, 4096, 1, -1),           # two rounds, ~5.6k ops, partials
-    (8, 32, 32, 520, 4096, 2, -1),           # three rounds
-    (3, 4, 2, 12, 1 << 16, 0, 1),            # abort inside round 0's group on rank 1
-    (3, 32, 32, 300, 4096, 1, 2),            # abort with two rounds pending, partials
+    (2, 2, 1, 12, (1 << 20) + 64, 0, -1, -1),
+    (3, 2, 1, 12, (1 << 20) + 64, 0, -1, -1),
+    (8, 2, 1, 64, 1 << 16, 0, -1, -1),
+    (4, 4, 2, 40, (1 << 16) + 64, 1, -1, -1),   # ragged holder counts on one decoder
+    (8, 10, 4, 24, 1 << 16, 2, -1, -1),          # auto: survivors and partials in one group
+    (8, 32, 32, 12, 1 << 16, 0, -1, -1),
+    (3, 32, 32, 12, 1 << 16, 1, -1, -1),
+    (2, 32, 32, 300, 4096, 0, -1, -1),           # two rounds, ~4.2k transfers per rank each
+    (3, 32, 32, 300, 4096, 1, -1, -1),           # two rounds, ~5.6k transfers, partials
+    (8, 32, 32, 520, 4096, 2, -1, -1),           # three rounds
+    (2, 32, 32, 300, 4096, 0, -1, 0),            # unbounded: one group per round
+    (3, 32, 32, 300, 4096, 1, -1, 64),           # many small groups per round
+    (2, 2, 1, 12, (1 << 20) + 64, 0, -1, 1),     # one transfer per group
+    (3, 4, 2, 12, 1 << 16, 0, 1, -1),            # abort inside round 0's group on rank 1
+    (3, 32, 32, 300, 4096, 1, 2, -1),            # abort with two rounds pending, partials
 ]
+DEFAULT_GROUP_OPS = 1024
 
 
 def test_standin_plans(standin):
@@ -90,25 +95,27 @@ def test_standin_plans(standin):
     GPU cases are there for: a ragged partial round, multi-round plans, large groups."""
     seen = {}
     for c in CASES:
-        r = _run(standin, list(c[:6]) + [-2], timeout=60)
+        r = _run(standin, list(c[:6]) + [-2, c[7]], timeout=60)
         assert r.returncode == 0, r.stderr + r.stdout
         f = _fields(r.stdout)
         assert f["standin"] == "1", r.stdout
         seen[c] = f
     assert seen[CASES[3]]["ragged"] == "1"
-    assert int(seen[CASES[7]]["rounds"]) == 2 and int(seen[CASES[7]]["max_ops_per_rank_group"]) > 4000
-    assert int(seen[CASES[8]]["max_ops_per_rank_group"]) > 5000
+    assert int(seen[CASES[7]]["rounds"]) == 2 and int(seen[CASES[7]]["max_ops_per_rank_round"]) > 4000
+    assert int(seen[CASES[8]]["max_ops_per_rank_round"]) > 5000
     assert int(seen[CASES[9]]["rounds"]) == 3
     assert int(seen[CASES[4]]["survivor_moves"]) > 0 and int(seen[CASES[4]]["partial_moves"]) > 0
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", CASES, ids=lambda c: "w{}_rs{}_{}_n{}_F{}_x{}_a{}".format(*c))
+@pytest.mark.parametrize("case", CASES,
+                         ids=lambda c: "w{}_rs{}_{}_n{}_F{}_x{}_a{}_g{}".format(*c))
 def test_c_dist_world_n_standin(standin, case):
     """The degraded read at world > 1 (threads on GPU 0 over the stand-in): every rank's rebuilt
     fragments equal the oracle's codeword, twice on one handle (staging reuse); with an abort the
     aborting rank gets CEC_ENCCL, no rank hangs, and a fresh group on the same codecs then rebuilds
-    bit-exact."""
+    bit-exact. Every rank issues the same number of transfer groups: one per round unbounded, more
+    when a round holds more transfers per rank than the bound."""
     r = _run(standin, case)
     assert r.returncode == 0, r.stderr[-3000:] + r.stdout[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("world_n ok")]
@@ -118,6 +125,14 @@ def test_c_dist_world_n_standin(standin, case):
     assert f["standin"] == "1"
     if case[6] < 0:
         assert f["rebuilt"] == f["lost"]
+        rounds, groups, peak = int(f["rounds"]), int(f["groups"]), int(f["max_ops_per_rank_round"])
+        bound = DEFAULT_GROUP_OPS if case[7] < 0 else case[7]
+        if bound == 0:
+            assert groups == rounds
+        else:
+            # a segment's transfers never split, so a group may exceed a tiny bound; a round
+            # with more transfers on one rank than the bound takes more than one group
+            assert groups >= rounds and (groups > rounds or peak <= bound), (groups, rounds, peak)
     else:
         rcs = [int(x) for x in line[0].split("first_rc")[1].split()]
         assert rcs[case[6]] == -6

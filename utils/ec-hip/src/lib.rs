@@ -97,6 +97,7 @@ pub mod sys {
     pub const CEC_DIST_SURVIVOR: i32 = 0;
     pub const CEC_DIST_PARTIAL: i32 = 1;
     pub const CEC_DIST_OPT_EXCHANGE: c_int = 1;
+    pub const CEC_DIST_OPT_GROUP_OPS: c_int = 3;
     pub type cec_locate_fn = extern "C" fn(user: *mut c_void, seg: u64, frag: c_int) -> *const u8;
 
     extern "C" {
@@ -196,6 +197,7 @@ pub mod sys {
                                 moves: *mut cec_dist_move, moves_cap: usize, nmoves: *mut usize,
                                 decoder: *mut i32) -> c_int;
         pub fn cec_dist_set_option(d: *mut cec_dist, option: c_int, value: c_int) -> c_int;
+        pub fn cec_dist_groups(d: *const cec_dist, groups: *mut u64) -> c_int;
         pub fn cec_dist_degraded_read(d: *mut cec_dist, lost_seg: *const u64,
                                       lost_frag: *const u8, nlost: usize, shard_len: usize,
                                       locate: cec_locate_fn, user: *mut c_void,
