@@ -628,7 +628,13 @@ def config5_leg(dev, local, W: int = 96, warmup: int = 10, sample: int = 48) -> 
     import torch
     import cess_amd
     k, m, F, nseg = CONFIGS[5][0], CONFIGS[5][1], CONFIGS[5][2], CONFIGS[5][3]
-    stream = torch.cuda.Stream(dev)
+    # The encode runs on the current stream, the ticks on a fresh one. A fresh encode stream too
+    # (round 4's leg) can land on the ticks' hardware queue (HIP hands its 4 queues to streams
+    # round robin; this process has made many by now): the two then serialise and the step takes
+    # 1.70-1.71 ms instead of 1.53-1.54 on the same box (profiles/r05/c5_gap2/; CESS_C5_STREAM=new
+    # reproduces it)
+    stream = (torch.cuda.Stream(dev) if os.environ.get("CESS_C5_STREAM") == "new"
+              else torch.cuda.current_stream(dev))
     sha_stream = torch.cuda.Stream(dev)
     enc = cess_amd.New(k, m, device=local)
     d_data = torch.empty((nseg, k, F), dtype=torch.uint8, device=dev)
@@ -1050,6 +1056,10 @@ def main() -> None:
             stream = torch.cuda.Stream(dev, priority=-1)
             sha_stream = torch.cuda.Stream(dev, priority=0)
         else:
+            if os.environ.get("CESS_C5_STREAM") == "new":  # (the queue-collision A/B knob, see
+                # config5_leg; the standalone process has too few streams to collide)
+                torch.cuda.synchronize(dev)
+                stream = torch.cuda.Stream(dev)
             sha_stream = torch.cuda.Stream(dev) if args.hash_stream else stream
         pipe = HashPipeline(enc, d_data, d_par, nseg, F, dev, local, stream, sha_stream, W,
                             args.tick_pf)
