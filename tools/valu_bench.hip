@@ -72,11 +72,27 @@
                " %1, %2\n\t" INS " %3, %4\n\t" INS " %5, %6\n\t" INS " %7, %0\n\t"               \
                : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7));
 
+// 64-bit operand chains (rotates as one 64-bit shift of a doubled word, and their helpers)
+#define CHAINS64(OP)                                                                      \
+  asm volatile(OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) OP(6) OP(7)                            \
+               : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6), \
+                 "+v"(q7)                                                                 \
+               : "v"(kq));
+#define Q_46(i) "v_lshrrev_b64 %" #i ", 7, %" #i "\n\t"
+#define Q_47(i) "v_lshlrev_b64 %" #i ", 7, %" #i "\n\t"
+#define Q_48(i) "v_pk_mov_b32 %" #i ", %" #i ", %" #i " op_sel:[1,0]\n\t"
+#define Q_49(i) "v_mov_b64 %" #i ", %8\n\t"
+#define Q_50(i) "v_lshl_add_u64 %" #i ", %" #i ", 3, %8\n\t"
+#define Q_51(i) "v_pk_add_f32 %" #i ", %" #i ", %8\n\t"
+#define Q_52(i) "v_pk_fma_f32 %" #i ", %" #i ", %8, %8\n\t"
+
 template <int OPI>
 __global__ void k_valu(uint32_t* out, uint64_t* cyc, int iters, uint32_t a, uint32_t b) {
   uint32_t r0 = threadIdx.x, r1 = r0 + 1, r2 = r0 + 2, r3 = r0 + 3, r4 = r0 + 4, r5 = r0 + 5,
            r6 = r0 + 6, r7 = r0 + 7;
   uint32_t k1 = a + threadIdx.x, k2 = b;
+  uint64_t q0 = r0 * 0x100000001ull, q1 = q0 + 1, q2 = q0 + 2, q3 = q0 + 3, q4 = q0 + 4,
+           q5 = q0 + 5, q6 = q0 + 6, q7 = q0 + 7, kq = k1 * 0x100000001ull + b;
   __syncthreads();
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < iters; ++it) {
@@ -127,13 +143,21 @@ __global__ void k_valu(uint32_t* out, uint64_t* cyc, int iters, uint32_t a, uint
     if constexpr (OPI == 43) { REP8(SWAPS("v_permlane16_swap_b32")) }
     if constexpr (OPI == 44) { REP8(CHAINS(O_44)) }
     if constexpr (OPI == 45) { REP8(CHAINS(O_45)) }
+    if constexpr (OPI == 46) { REP8(CHAINS64(Q_46)) }
+    if constexpr (OPI == 47) { REP8(CHAINS64(Q_47)) }
+    if constexpr (OPI == 48) { REP8(CHAINS64(Q_48)) }
+    if constexpr (OPI == 49) { REP8(CHAINS64(Q_49)) }
+    if constexpr (OPI == 50) { REP8(CHAINS64(Q_50)) }
+    if constexpr (OPI == 51) { REP8(CHAINS64(Q_51)) }
+    if constexpr (OPI == 52) { REP8(CHAINS64(Q_52)) }
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
-  out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;
+  out[blockIdx.x * blockDim.x + threadIdx.x] =
+      r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7 ^ (uint32_t)(q0 ^ q1 ^ q2 ^ q3 ^ q4 ^ q5 ^ q6 ^ q7);
   if (threadIdx.x % 64 == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
 }
 
-static const char* kNames[] = {"v_bitop3_b32", "v_perm_b32", "v_lshlrev_b32", "v_alignbit_b32", "v_add3_u32", "v_add_u32", "v_xor_b32", "v_lshl_or_b32", "v_fma_f32", "v_and_b32", "v_mul_u32_u24", "v_mad_u32_u24", "v_pk_add_u16", "v_pk_lshlrev_b16", "v_cndmask_b32", "v_bfi_b32", "v_sub_u32", "v_or3_b32", "v_and_or_b32", "v_xad_u32", "v_lshl_add_u32", "v_bfe_u32", "v_lshrrev_b32", "v_mul_lo_u32", "v_mov_b32_dpp", "v_add_u32_sdwa", "v_lshlrev_b16", "v_lshlrev_b32_by7", "v_lshrrev_b32_by1", "v_lshlrev_b32_vreg", "v_or_b32", "v_not_b32", "v_mov_b32", "v_add_co_u32", "v_ashrrev_i32", "v_bitop3_b16", "v_add_u16", "v_xor_b32_e64_lit", "v_and_b32_lit", "v_bitop3_lit", "v_max_u32", "v_lshlrev_b16_by1_e64", "v_permlane32_swap_b32", "v_permlane16_swap_b32", "v_xor_b32_dpp", "v_and_b32_dpp"};
+static const char* kNames[] = {"v_bitop3_b32", "v_perm_b32", "v_lshlrev_b32", "v_alignbit_b32", "v_add3_u32", "v_add_u32", "v_xor_b32", "v_lshl_or_b32", "v_fma_f32", "v_and_b32", "v_mul_u32_u24", "v_mad_u32_u24", "v_pk_add_u16", "v_pk_lshlrev_b16", "v_cndmask_b32", "v_bfi_b32", "v_sub_u32", "v_or3_b32", "v_and_or_b32", "v_xad_u32", "v_lshl_add_u32", "v_bfe_u32", "v_lshrrev_b32", "v_mul_lo_u32", "v_mov_b32_dpp", "v_add_u32_sdwa", "v_lshlrev_b16", "v_lshlrev_b32_by7", "v_lshrrev_b32_by1", "v_lshlrev_b32_vreg", "v_or_b32", "v_not_b32", "v_mov_b32", "v_add_co_u32", "v_ashrrev_i32", "v_bitop3_b16", "v_add_u16", "v_xor_b32_e64_lit", "v_and_b32_lit", "v_bitop3_lit", "v_max_u32", "v_lshlrev_b16_by1_e64", "v_permlane32_swap_b32", "v_permlane16_swap_b32", "v_xor_b32_dpp", "v_and_b32_dpp", "v_lshrrev_b64", "v_lshlrev_b64", "v_pk_mov_b32_swap", "v_mov_b64", "v_lshl_add_u64", "v_pk_add_f32", "v_pk_fma_f32"};
 
 template <int OPI>
 void run(int waves_per_simd, int cus) {
@@ -182,6 +206,6 @@ template <int... I>
 void run_list(std::integer_sequence<int, I...>, int from) { ((I >= from ? run_all<I>() : void()), ...); }
 
 int main(int argc, char** argv) {
-  run_list(std::make_integer_sequence<int, 46>{}, argc > 1 ? atoi(argv[1]) : 27);
+  run_list(std::make_integer_sequence<int, 53>{}, argc > 1 ? atoi(argv[1]) : 27);
   return 0;
 }
