@@ -1347,11 +1347,14 @@ def main() -> None:
         out.setdefault("extra", {}).update(
             {"reconstruct_GBps_per_gpu": round(bytes_step_gpu / (dms * 1e-3) / GB, 2),
              "reconstruct_ms": round(dms, 4)})
-        # the wide code (BASELINE config 5's RS(32,32), 16 MiB segments: F = 512 KiB) in the same
-        # run, so the driver's own line carries its encode, restoral and multi-erasure rebuild rates
-        out["extra"]["wide_code"] = wide_code_legs(dev, local, stream)
-        # BASELINE config 5 (RS(32,32) encode + SHA-256 of every fragment) as the driver runs it
-        out["extra"]["config5"] = config5_leg(dev, local)
+        if world == 1:
+            # one-GPU legs (at N > 1 every rank would repeat them, and config 5's hash window
+            # holds ~100 GiB of parity per rank: ranks sharing a GPU in the rehearsal do not fit).
+            # The wide code (BASELINE config 5's RS(32,32), 16 MiB segments: F = 512 KiB), so the
+            # driver's own line carries its encode, restoral and multi-erasure rebuild rates
+            out["extra"]["wide_code"] = wide_code_legs(dev, local, stream)
+            # BASELINE config 5 (RS(32,32) encode + SHA-256 of every fragment) as the driver runs
+            out["extra"]["config5"] = config5_leg(dev, local)
         # the measured-copy ceiling beside the spec peak: a device-to-device copy
         # of the same 1 GiB data batch (HIP's blit kernel), read + write bytes per copy
         src = d_data.view(-1)
