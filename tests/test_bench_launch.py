@@ -145,8 +145,9 @@ def test_line_keys_one_gpu():
     assert bench.line_problems(_line(1, extra=cold_less)) == ["wide_code.encode lacks its cold mean"]
 
 
-@pytest.mark.parametrize("name", ["bench_default_b.json", "bench_gpus2_gloo_one_gpu_a.json",
-                                  "bench_gpus4_gloo_one_gpu.json"])
+@pytest.mark.parametrize("name", ["bench_default_b.json",
+                                  "bench_gpus2_gloo_one_gpu_b.json",
+                                  "bench_gpus4_gloo_one_gpu_b.json"])
 def test_recorded_lines_have_every_key(name):
     """The lines this round's GPU runs printed (profiles/r05/): the N = 1 default line and the
     one-GPU rehearsals of the N = 2 and N = 4 lines (gloo ranks sharing GPU 0) carry everything
