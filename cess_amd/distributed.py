@@ -148,13 +148,21 @@ def plan_gather(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
                       moved, partial, decoder, world, survivors)
 
 
+# Transfers per grouped point-to-point batch (one RCCL group each), counted over the whole plan:
+# a batch holds the transfers of a run of the plan, the same run on every rank, so each rank's
+# batch holds both ends of its transfers (the C path's CEC_DIST_OPT_GROUP_OPS, dist.cpp)
+GROUP_TRANSFERS = 1024
+
+
 def _p2p(ops_spec, group, stage: bool):
-    """Issue [(is_send, tensor, peer)] as one grouped point-to-point batch and wait. gloo (CPU
-    tests, rehearsals) needs host buffers: device tensors are staged through host memory."""
+    """Issue [(batch, is_send, tensor, peer)] as grouped point-to-point batches, one per `batch`
+    index in increasing order (all enqueued before any wait), and wait. gloo (CPU tests,
+    rehearsals) needs host buffers: device tensors are staged through host memory."""
     import torch
     import torch.distributed as dist
-    ops, copies = [], []
-    for is_send, t, peer in ops_spec:
+    batches, copies = {}, []
+    for b, is_send, t, peer in ops_spec:
+        ops = batches.setdefault(b, [])
         if is_send:
             ops.append(dist.P2POp(dist.isend, t.cpu() if stage else t, peer, group))
         elif stage:
@@ -163,9 +171,11 @@ def _p2p(ops_spec, group, stage: bool):
             ops.append(dist.P2POp(dist.irecv, h, peer, group))
         else:
             ops.append(dist.P2POp(dist.irecv, t, peer, group))
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+    reqs = []
+    for b in sorted(batches):
+        reqs += dist.batch_isend_irecv(batches[b])
+    for req in reqs:
+        req.wait()
     for t, h in copies:
         t.copy_(h)
 
@@ -197,15 +207,21 @@ def gather_survivors(plan: GatherPlan, store: FragmentStore, k: int, m: int, ran
     def dst_view(s, f):
         return sd[row[s], f] if f < k else sp[row[s], f - k]
 
-    # RCCL/NCCL moves HBM buffers directly (xGMI)
+    # RCCL/NCCL moves HBM buffers directly (xGMI); the plan's cross-rank moves in batches of
+    # GROUP_TRANSFERS, numbered the same on every rank
     ops = []
+    moved = 0
     for (s, f), (src, dst) in sorted(plan.moves.items()):
         if src == dst == rank:
             dst_view(s, f).copy_(store.data[store.slots[(s, f)]])
-        elif src == rank:
-            ops.append((True, store.data[store.slots[(s, f)]], dst))
+        if src == dst:
+            continue
+        b = moved // GROUP_TRANSFERS
+        moved += 1
+        if src == rank:
+            ops.append((b, True, store.data[store.slots[(s, f)]], dst))
         elif dst == rank:
-            ops.append((False, dst_view(s, f), src))
+            ops.append((b, False, dst_view(s, f), src))
     _p2p(ops, group, _staged(dev, group))
     if not mysegs:
         return None, None, None, []
@@ -258,15 +274,21 @@ def partial_exchange(plan: GatherPlan, store: FragmentStore, enc, rank: int, gro
         acc[0, i].copy_(slot(s, f))
     if any(len(plan.partial[s]) < H for s in dsegs):
         acc[1:].zero_()
+    # batch of each partial segment: its first transfer's position in the whole plan's partial
+    # transfers (every rank numbers them alike) // GROUP_TRANSFERS
+    batch, moved = {}, 0
+    for s in sorted(plan.partial):
+        batch[s] = moved // GROUP_TRANSFERS
+        moved += len(plan.lost[s]) * len(plan.partial[s])
     ops = []
     for s in mine:  # the same (segment, fragment) order on both sides of every pair
         if plan.decoder[s] == rank:
             for h, src in enumerate(plan.partial[s]):
                 for f in plan.lost[s]:
-                    ops.append((False, acc[1 + h, pidx[(s, f)]], src))
+                    ops.append((batch[s], False, acc[1 + h, pidx[(s, f)]], src))
         else:
             for f in plan.lost[s]:
-                ops.append((True, slot(s, f), plan.decoder[s]))
+                ops.append((batch[s], True, slot(s, f), plan.decoder[s]))
     _p2p(ops, group, _staged(dev, group))
     if H and pairs:
         # on the current stream, after the received partials and before whoever reads acc[0]

@@ -181,9 +181,11 @@ def _xor_cpu(dst, src, nsrc, stride, length):
         d ^= rows[j]
 
 
-def _exchange_worker(rank, world, port, k, m, nseg, F, exchange, q):
+def _exchange_worker(rank, world, port, k, m, nseg, F, exchange, q, group_transfers=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if group_transfers:
+        D.GROUP_TRANSFERS = group_transfers
     from oracle import rs_oracle as o
     rs = o.ReedSolomon(k, m)
     n = k + m
@@ -227,6 +229,30 @@ def test_degraded_read_partials_gloo(world, k, m, exchange):
     assert all(ok for _, ok, _, _ in res), res
     assert sum(n for _, _, n, _ in res) == sum(1 + (s % m) for s in range(nseg))
     assert all(npart > 0 for _, _, _, npart in res)
+
+
+@pytest.mark.parametrize("world,k,m,exchange,gt", [(2, 2, 1, "survivors", 1),
+                                                   (3, 4, 2, "auto", 2),
+                                                   (3, 10, 4, "partials", 3),
+                                                   (3, 4, 2, "survivors", 5)])
+def test_degraded_read_small_batches_gloo(world, k, m, exchange, gt):
+    """The torch path with its transfers cut into many grouped batches (GROUP_TRANSFERS, the
+    same cuts on every rank): every lost fragment still comes back equal to the oracle's."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    nseg, F = 11, 1024
+    procs = [ctx.Process(target=_exchange_worker,
+                         args=(r, world, port, k, m, nseg, F, exchange, q, gt))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _, _ in res), res
+    assert sum(n for _, _, n, _ in res) == sum(1 + (s % m) for s in range(nseg))
 
 
 @pytest.mark.parametrize("k,m", [(2, 1), (4, 2), (10, 4), (32, 32)])
