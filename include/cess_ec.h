@@ -138,7 +138,8 @@ int cec_sha256_hex(const uint8_t* const* d_bufs, size_t n, size_t len, uint8_t* 
 typedef struct cec_hashq cec_hashq;
 /* capacity: maximum live chains, a power of two (128 B of HBM each). */
 int cec_hashq_create(int device, size_t capacity, void* hip_stream, cec_hashq** out);
-/* Synchronises the queue's stream, then frees the table. */
+/* Frees the table in stream order on the queue's stream (after the launches queued there); does
+ * not wait, and does not stall other streams. */
 void cec_hashq_destroy(cec_hashq* q);
 /* Append n chains: buffer i is d_base + (i / per) * outer_stride + (i % per) * inner_stride, len
  * bytes; its 64 lowercase hex chars go to d_hex + ((i / per) * hex_outer + i % per) * 64
@@ -215,6 +216,10 @@ typedef struct cec_pipeline_stats {
 } cec_pipeline_stats;
 typedef struct cec_pipeline cec_pipeline;
 int cec_pipeline_create(cec_codec* codec, const cec_pipeline_opts* opts, cec_pipeline** out);
+/* Waits for the pipeline's own streams, then frees its pinned host ring and device slots. The HIP
+ * runtime's hipHostFree / hipFree synchronise the whole device, so other codecs' work on this GPU
+ * stalls until it is done: destroy a pipeline while the device is idle, or keep it (a pipeline is
+ * reusable, one run per file). */
 void cec_pipeline_destroy(cec_pipeline* p);
 /* Stream one source through the pipeline (reusable: run again for the next file). */
 int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_fragments,
