@@ -103,6 +103,9 @@ SIGNATURES = {
                                  POINTER(c_int32)]),
     "cec_dist_set_option": (c_int, [c_void_p, c_int, c_int]),
     "cec_dist_groups": (c_int, [c_void_p, POINTER(c_uint64)]),
+    "cec_dist_plan_groups": (c_int, [c_int, c_int, c_int, c_int, c_int, POINTER(c_uint64),
+                                     POINTER(c_uint8), c_size_t, POINTER(c_uint64), c_size_t,
+                                     POINTER(c_size_t)]),
     "cec_dist_degraded_read": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint8), c_size_t,
                                        c_size_t, LOCATE_FN, c_void_p, POINTER(c_void_p), c_void_p,
                                        POINTER(c_size_t)]),

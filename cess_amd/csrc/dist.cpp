@@ -104,6 +104,8 @@ int nccl_err(ncclResult_t res, const char* what) {
     if (_r != ncclSuccess) return nccl_err(_r, #expr); \
   } while (0)
 
+constexpr size_t kRound = 256;  // segments per round of a degraded read (staging bound)
+
 int owner(uint64_t s, int f, int world) { return (int)((s + (uint64_t)f) % (uint64_t)world); }
 
 struct Seg {
@@ -159,6 +161,44 @@ int make_plan(int k, int m, int world, int exchange, const uint64_t* lost_seg,
     out->push_back(std::move(g));
   }
   return CEC_OK;
+}
+
+// Where the transfer groups of plan segments [r0, r1) start (plan positions, ascending, r0 first;
+// r1 appended last): a new group begins before a segment whose transfers would take some rank past
+// `group_ops` transfers in the current group (0: no bound). A segment's transfers never split.
+// Every rank computes every rank's counts from the shared plan, so all cut alike.
+void group_cuts(const std::vector<Seg>& plan, size_t r0, size_t r1, int world, int group_ops,
+                std::vector<size_t>* cuts) {
+  cuts->assign(1, r0);
+  if (group_ops > 0) {
+    std::vector<size_t> cnt(world, 0), one(world, 0);
+    for (size_t i = r0; i < r1; ++i) {
+      const Seg& g = plan[i];
+      std::fill(one.begin(), one.end(), 0);
+      if (g.partial) {
+        for (int h : g.holders) {
+          one[h] += g.lost.size();
+          one[g.decoder] += g.lost.size();
+        }
+      } else {
+        for (int f : g.surv) {
+          const int o = owner(g.seg, f, world);
+          if (o != g.decoder) {
+            ++one[o];
+            ++one[g.decoder];
+          }
+        }
+      }
+      bool over = false;
+      for (int w = 0; w < world; ++w) over |= cnt[w] + one[w] > (size_t)group_ops;
+      if (over && i > cuts->back()) {
+        cuts->push_back(i);
+        std::fill(cnt.begin(), cnt.end(), 0);
+      }
+      for (int w = 0; w < world; ++w) cnt[w] += one[w];
+    }
+  }
+  cuts->push_back(r1);
 }
 
 }  // namespace
@@ -354,6 +394,27 @@ int cec_dist_plan_ex(int k, int m, int world, int exchange, const uint64_t* lost
   return CEC_OK;
 }
 
+int cec_dist_plan_groups(int k, int m, int world, int exchange, int group_ops,
+                         const uint64_t* lost_seg, const uint8_t* lost_frag, size_t nlost,
+                         uint64_t* starts, size_t starts_cap, size_t* ngroups) {
+  if (group_ops < 0) return cec::set_error(CEC_EINVAL, "group ops must be >= 0");
+  std::vector<Seg> plan;
+  int rc = make_plan(k, m, world, exchange, lost_seg, lost_frag, nlost, &plan);
+  if (rc) return rc;
+  size_t n = 0;
+  std::vector<size_t> cuts;
+  for (size_t r0 = 0; r0 < plan.size(); r0 += kRound) {
+    group_cuts(plan, r0, std::min(plan.size(), r0 + kRound), world, group_ops, &cuts);
+    for (size_t c = 0; c + 1 < cuts.size(); ++c) {
+      if (starts && n < starts_cap) starts[n] = cuts[c];
+      ++n;
+    }
+  }
+  if (ngroups) *ngroups = n;
+  if (starts && n > starts_cap) return cec::set_error(CEC_EINVAL, "plan groups: starts_cap too small");
+  return CEC_OK;
+}
+
 int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t* lost_frag,
                            size_t nlost, size_t shard_len, cec_locate_fn locate, void* user,
                            uint8_t* const* d_out, void* hip_stream, size_t* nrebuilt) {
@@ -412,7 +473,6 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
   // Rounds of at most kRound segments of the plan (the same split on every rank) bound the
   // staging; rounds follow each other on the stream, so a round's receives land after the
   // previous round's rebuild has read the staging.
-  constexpr size_t kRound = 256;
   struct Round {
     // survivor segments this rank rebuilds; partial segments it decodes or holds survivors of
     std::vector<const Seg*> mine, pmine;
@@ -557,36 +617,8 @@ int cec_dist_degraded_read(cec_dist* d, const uint64_t* lost_seg, const uint8_t*
     // waits on another rank's later group. Within a group: survivor moves, then partials, each in
     // plan order (which pairs every send with its receive on the peer). The groups follow each
     // other on the stream with no host synchronisation.
-    std::vector<size_t> cuts{r0};
-    if (d->group_ops > 0) {
-      std::vector<size_t> cnt(world, 0), one(world, 0);
-      for (size_t i = r0; i < r1; ++i) {
-        const Seg& g = plan[i];
-        std::fill(one.begin(), one.end(), 0);
-        if (g.partial) {
-          for (int h : g.holders) {
-            one[h] += g.lost.size();
-            one[g.decoder] += g.lost.size();
-          }
-        } else {
-          for (int f : g.surv) {
-            const int o = owner(g.seg, f, world);
-            if (o != g.decoder) {
-              ++one[o];
-              ++one[g.decoder];
-            }
-          }
-        }
-        bool over = false;
-        for (int w = 0; w < world; ++w) over |= cnt[w] + one[w] > (size_t)d->group_ops;
-        if (over && i > cuts.back()) {
-          cuts.push_back(i);
-          std::fill(cnt.begin(), cnt.end(), 0);
-        }
-        for (int w = 0; w < world; ++w) cnt[w] += one[w];
-      }
-    }
-    cuts.push_back(r1);
+    std::vector<size_t> cuts;
+    group_cuts(plan, r0, r1, world, d->group_ops, &cuts);
     size_t rj = 0;
     auto fail = [&](ncclResult_t res, const char* what) {
       // end the half-built group (this thread's group state is then clean; what was enqueued is

@@ -349,6 +349,28 @@ def c_plan(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
             {p: dec[i] for i, p in enumerate(pairs)})
 
 
+def c_plan_groups(lost: Dict[int, Sequence[int]], k: int, m: int, world: int,
+                  exchange: str = "auto", group_ops: int = 1024) -> List[int]:
+    """cec_dist_plan_groups: the plan positions (index of the segment among the lost segments in
+    ascending order) where the RCCL transfer groups of libcessec's degraded read start, with at
+    most `group_ops` transfers on any rank per group (host only)."""
+    from ctypes import byref, c_size_t, c_uint8, c_uint64
+    from . import _lib
+    from .reedsolomon import check
+    pairs = [(s, f) for s in sorted(lost) for f in lost[s]]
+    segs = (c_uint64 * max(1, len(pairs)))(*[s for s, _ in pairs])
+    frags = (c_uint8 * max(1, len(pairs)))(*[f for _, f in pairs])
+    lib = _lib.load()
+    n = c_size_t()
+    ex = EXCHANGES.index(exchange)
+    check(lib.cec_dist_plan_groups(k, m, world, ex, group_ops, segs, frags, len(pairs), None, 0,
+                                   byref(n)), "cec_dist_plan_groups")
+    out = (c_uint64 * max(1, n.value))()
+    check(lib.cec_dist_plan_groups(k, m, world, ex, group_ops, segs, frags, len(pairs), out,
+                                   n.value, byref(n)), "cec_dist_plan_groups")
+    return list(out[:n.value])
+
+
 class RcclGroup:
     """cec_dist_*: libcessec's own RCCL group for the degraded read (one per rank; every rank
     creates it with the same `uid`, made by `RcclGroup.unique_id()` on one rank)."""

@@ -302,6 +302,13 @@ typedef struct cec_dist_move {
 int cec_dist_set_option(cec_dist* d, int option, int value);
 /* Transfer groups this handle has issued (diagnostic: the group split of CEC_DIST_OPT_GROUP_OPS). */
 int cec_dist_groups(const cec_dist* d, uint64_t* groups);
+/* Host only: the transfer groups a degraded read of the lost list issues with `group_ops`
+ * (CEC_DIST_OPT_GROUP_OPS) and `exchange`: *ngroups of them, and the plan position (index of the
+ * segment in ascending segment order) where each starts, written to starts (NULL: count only;
+ * CEC_EINVAL if more than starts_cap). A round of 256 segments always starts a group. */
+int cec_dist_plan_groups(int k, int m, int world, int exchange, int group_ops,
+                         const uint64_t* lost_seg, const uint8_t* lost_frag, size_t nlost,
+                         uint64_t* starts, size_t starts_cap, size_t* ngroups);
 /* Host only: the plan a degraded read of the lost list runs. The list holds nlost (segment,
  * fragment) erasures, any order, duplicates allowed, at most m distinct per segment
  * (CEC_ETOOFEW otherwise; CEC_EINVAL for an index >= k+m). Writes the moves in issue order

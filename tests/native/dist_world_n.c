@@ -292,6 +292,12 @@ int main(int argc, char** argv) {
       ragged |= hi > lo;
     }
 
+  size_t predicted = 0;
+  if (cec_dist_plan_groups(K, M, W, EXCH, GROUP_OPS < 0 ? 1024 : GROUP_OPS, lost_seg, lost_frag,
+                           NLOST, NULL, 0, &predicted)) {
+    fprintf(stderr, "FAIL plan groups: %s\n", cec_last_error());
+    return 1;
+  }
   if (cec_dist_unique_id(id1) || cec_dist_unique_id(id2)) {
     fprintf(stderr, "FAIL unique id: %s\n", cec_last_error());
     return 1;
@@ -299,8 +305,8 @@ int main(int argc, char** argv) {
   const int standin = memcmp(id1, "cess-rccl-standin", 17) == 0;
   if (ABORT_RANK == -2) { /* host only: the plan and which librccl libcessec loaded */
     printf("plan world %d RS(%d,%d) nseg %zu lost %zu rounds %zu survivor_moves %zu "
-           "partial_moves %zu max_ops_per_rank_round %zu ragged %d standin %d\n", W, K, M, NSEG,
-           NLOST, rounds, nsurv, npartial, max_ops, ragged, standin);
+           "partial_moves %zu max_ops_per_rank_round %zu ragged %d standin %d predicted_groups %zu\n",
+           W, K, M, NSEG, NLOST, rounds, nsurv, npartial, max_ops, ragged, standin, predicted);
     return 0;
   }
   pthread_barrier_init(&bar, NULL, (unsigned)W);
@@ -331,6 +337,11 @@ int main(int argc, char** argv) {
               (unsigned long long)rk[i].groups, (unsigned long long)rk[0].groups);
       fail = 1;
     }
+  if (ABORT_RANK < 0 && rk[0].groups != predicted) {
+    fprintf(stderr, "FAIL issued %llu transfer groups, cec_dist_plan_groups predicted %zu\n",
+            (unsigned long long)rk[0].groups, predicted);
+    fail = 1;
+  }
   if (ABORT_RANK < 0 && rebuilt != NLOST) {
     fprintf(stderr, "FAIL rebuilt %zu of %zu lost fragments\n", rebuilt, NLOST);
     fail = 1;
@@ -338,8 +349,8 @@ int main(int argc, char** argv) {
   if (fail) return 1;
   printf("world_n ok world %d RS(%d,%d) nseg %zu F %zu exchange %d lost %zu rebuilt %zu rounds %zu "
          "survivor_moves %zu partial_moves %zu max_ops_per_rank_round %zu ragged %d standin %d "
-         "groups %llu", W, K, M, NSEG, F, EXCH, NLOST, rebuilt, rounds, nsurv, npartial, max_ops,
-         ragged, standin, (unsigned long long)rk[0].groups);
+         "groups %llu predicted_groups %zu", W, K, M, NSEG, F, EXCH, NLOST, rebuilt, rounds, nsurv,
+         npartial, max_ops, ragged, standin, (unsigned long long)rk[0].groups, predicted);
   if (ABORT_RANK >= 0) {
     printf(" abort_rank %d first_rc", ABORT_RANK);
     for (int i = 0; i < W; ++i) printf(" %d", rk[i].rc_first);

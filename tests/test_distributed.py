@@ -318,3 +318,46 @@ def test_survivor_choice():
     import cess_amd
     with pytest.raises(cess_amd.CecError):
         D.survivors_of(4, 2, [True, True, True, False, False, False])
+
+
+@pytest.mark.parametrize("k,m,world,exchange,bound", [(2, 1, 8, "survivors", 64),
+                                                      (32, 32, 8, "survivors", 1024),
+                                                      (32, 32, 3, "partials", 200),
+                                                      (10, 4, 2, "auto", 7),
+                                                      (4, 2, 4, "auto", 1),
+                                                      (32, 32, 8, "auto", 0)])
+def test_c_plan_groups(k, m, world, exchange, bound):
+    """cec_dist_plan_groups (the group cuts libcessec's degraded read issues, CEC_DIST_OPT_GROUP_OPS)
+    equals a restatement from the plan's moves: per round of 256 segments, a new group before a
+    segment whose transfers would take any rank past the bound; rounds always start a group; no
+    group holds more than the bound on any rank unless one segment alone does."""
+    rng = np.random.default_rng(k * 7 + world)
+    n = k + m
+    lost = {}
+    for s in sorted(rng.choice(5000, size=700, replace=False).tolist()):
+        lost[s] = rng.choice(n, size=int(rng.integers(1, m + 1)), replace=False).tolist()
+    moves, _ = D.c_plan(lost, k, m, world, exchange)
+    order = sorted(lost)
+    pos = {s: i for i, s in enumerate(order)}
+    per_seg = [[0] * world for _ in order]
+    for s, f, src, dst, kind in moves:
+        if src != dst:
+            per_seg[pos[s]][src] += 1
+            per_seg[pos[s]][dst] += 1
+    want = []
+    for r0 in range(0, len(order), 256):
+        want.append(r0)
+        cnt = [0] * world
+        for i in range(r0, min(len(order), r0 + 256)):
+            if bound and i > want[-1] and any(c + o > bound for c, o in zip(cnt, per_seg[i])):
+                want.append(i)
+                cnt = [0] * world
+            cnt = [c + o for c, o in zip(cnt, per_seg[i])]
+    got = D.c_plan_groups(lost, k, m, world, exchange, bound)
+    assert got == want
+    ends = got[1:] + [len(order)]
+    for a, b in zip(got, ends):
+        tot = [sum(per_seg[i][w] for i in range(a, b)) for w in range(world)]
+        assert not bound or b - a == 1 or max(tot) <= bound
+    if bound == 0:
+        assert got == list(range(0, len(order), 256))

@@ -198,6 +198,10 @@ pub mod sys {
                                 decoder: *mut i32) -> c_int;
         pub fn cec_dist_set_option(d: *mut cec_dist, option: c_int, value: c_int) -> c_int;
         pub fn cec_dist_groups(d: *const cec_dist, groups: *mut u64) -> c_int;
+        pub fn cec_dist_plan_groups(k: c_int, m: c_int, world: c_int, exchange: c_int,
+                                    group_ops: c_int, lost_seg: *const u64, lost_frag: *const u8,
+                                    nlost: usize, starts: *mut u64, starts_cap: usize,
+                                    ngroups: *mut usize) -> c_int;
         pub fn cec_dist_degraded_read(d: *mut cec_dist, lost_seg: *const u64,
                                       lost_frag: *const u8, nlost: usize, shard_len: usize,
                                       locate: cec_locate_fn, user: *mut c_void,
