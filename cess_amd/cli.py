@@ -11,6 +11,11 @@
       rejected unless --no-segment-limit.
   python -m cess_amd.cli verify <file> <json>
       re-encodes and compares the records.
+  python -m cess_amd.cli decode <json> <fragment dir> <out file> [--k 2 --m 1]
+      retrieves the file from its records and the fragments in DIR (named by hash, as encode
+      --out writes them): every fragment checked against its recorded hash (a wrong one counts
+      as lost), up to m lost fragments per segment rebuilt on the GPU, every segment checked
+      against its recorded hash (cess_amd.retrieve).
 """
 import argparse
 import json
@@ -68,6 +73,21 @@ def _encode(args) -> int:
     return 0
 
 
+def _decode(args) -> int:
+    from .reedsolomon import ErrTooFewShards
+    from .retrieve import ErrSegmentHashMismatch, dir_fetch, record_from_json, retrieve_file
+    with open(args.records) as f:
+        rec = record_from_json(f.read())
+    try:
+        st = retrieve_file(rec, dir_fetch(args.fragments), args.out, args.k, args.m,
+                           args.segment_size, args.device)
+    except (ErrTooFewShards, ErrSegmentHashMismatch) as e:
+        print(json.dumps({"error": str(e)}))
+        return 2
+    print(json.dumps(st))
+    return 0
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="cess-ec")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -88,10 +108,20 @@ def main(argv=None) -> int:
     v = sub.add_parser("verify")
     v.add_argument("file")
     v.add_argument("records")
+    d = sub.add_parser("decode")
+    d.add_argument("records")
+    d.add_argument("fragments")
+    d.add_argument("out")
+    d.add_argument("--k", type=int, default=geometry.DATA_SHARDS)
+    d.add_argument("--m", type=int, default=geometry.PARITY_SHARDS)
+    d.add_argument("--segment-size", type=int, default=geometry.SEGMENT_SIZE)
+    d.add_argument("--device", type=int, default=0)
     args = ap.parse_args(argv)
 
     if args.cmd == "encode":
         return _encode(args)
+    if args.cmd == "decode":
+        return _decode(args)
     from .pipeline import encode_file_records
     with open(args.records) as f:
         want = json.load(f)

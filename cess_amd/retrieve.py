@@ -1,0 +1,211 @@
+"""File retrieval: the download side of the segment -> fragment path.
+
+A file uploaded through `FileBank::upload_declaration` (c-pallets/file-bank/src/lib.rs:423-428)
+is recorded as one `SegmentList { hash, fragment_list }` per segment
+(c-pallets/file-bank/src/types.rs:13-16): the segment's hash and, in index order, the hashes of
+its k data and m parity fragments, which miners store (`FragmentInfo { hash, avail, miner }`,
+types.rs:64-76; `avail = false` is an erasure the restoral flow repairs, lib.rs:943-1122). Getting
+the file back is a degraded read per segment:
+
+  * fetch the data fragments; a fragment whose SHA-256 differs from its recorded hash counts as
+    lost (a miner serving wrong bytes is an erasure, not an error in the file);
+  * while fewer than k fragments check out, fetch parity fragments;
+  * rebuild the lost data fragments of every such segment on the GPU, one
+    `cec_reconstruct_batch` launch per batch (data_only: the parity is not needed);
+  * check each segment against its recorded hash, join the k data fragments of every segment
+    (the contiguous klauspost Split), drop the last segment's zero padding.
+
+The hashes are SHA-256 hex (the ecosystem convention, see segments.py). The GPU is used only for
+the rebuild; a batch whose segments all arrived intact never touches it.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import json
+import os
+import time
+from typing import BinaryIO, Callable, Dict, Optional, Union
+
+import numpy as np
+
+from . import geometry
+from .reedsolomon import ErrTooFewShards
+from .segments import FileRecord, SegmentList, file_hash
+
+# fetch(segment index, fragment index, recorded fragment hash hex) -> the fragment's bytes, or None
+# when no miner serves it
+FetchFn = Callable[[int, int, bytes], Optional[Union[bytes, bytearray, memoryview, np.ndarray]]]
+
+
+class ErrSegmentHashMismatch(ValueError):
+    """A rebuilt or joined segment does not hash to its recorded SegmentList hash."""
+
+
+class ErrRecordsInconsistent(ValueError):
+    """The records' file hash is not the hash of their segment hashes."""
+
+
+def record_from_json(obj: Union[str, dict]) -> FileRecord:
+    """FileRecord from FileRecord.to_json() (the `cess_amd.cli encode` output)."""
+    if isinstance(obj, str):
+        obj = json.loads(obj)
+    segs = [SegmentList(s["hash"].encode(), [f.encode() for f in s["fragment_list"]])
+            for s in obj["segments"]]
+    return FileRecord(obj["file_hash"].encode(), int(obj["size"]), segs)
+
+
+def dir_fetch(directory: str) -> FetchFn:
+    """Fragments stored as files named by their hash (what `cli encode --out DIR` writes)."""
+    def fetch(_seg: int, _frag: int, h: bytes):
+        path = os.path.join(directory, h.decode())
+        try:
+            with open(path, "rb") as f:
+                return f.read()
+        except FileNotFoundError:
+            return None
+    return fetch
+
+
+class Retriever:
+    """Rebuilds files from their records and whatever fragments `fetch` returns. The codec and
+    the device batch are created on the first segment that needs a rebuild."""
+
+    def __init__(self, k: int = geometry.DATA_SHARDS, m: int = geometry.PARITY_SHARDS,
+                 segment_size: int = geometry.SEGMENT_SIZE, device: int = 0,
+                 batch_segments: int = 64, threads: int = 8):
+        if segment_size % k:
+            raise ValueError("segment_size must be a multiple of k")
+        self.k, self.m, self.n = k, m, k + m
+        self.seg = segment_size
+        self.F = segment_size // k
+        self.device = device
+        self.B = max(1, batch_segments)
+        self.pool = cf.ThreadPoolExecutor(max_workers=max(1, threads))
+        self.enc = None
+        self.d_data = self.d_par = None
+
+    def close(self) -> None:
+        self.pool.shutdown(wait=True)
+        if self.enc is not None:
+            self.enc.close()
+            self.enc = None
+        self.d_data = self.d_par = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _gather(self, s: int, sl: SegmentList, fetch: FetchFn):
+        """The fragments of segment s that check out: ({index: uint8 array}, fetched, rejected),
+        data first, parity only while fewer than k are valid (runs on a pool thread)."""
+        if len(sl.fragment_list) != self.n:
+            raise ValueError(f"segment {s}: {len(sl.fragment_list)} fragment hashes, "
+                             f"expected k + m = {self.n} (check_file_spec)")
+        good: Dict[int, np.ndarray] = {}
+        fetched = rejected = 0
+        for f in range(self.n):
+            if f >= self.k and len(good) >= self.k:
+                break
+            raw = fetch(s, f, sl.fragment_list[f])
+            if raw is None:
+                continue
+            fetched += 1
+            a = np.frombuffer(raw, np.uint8) if not isinstance(raw, np.ndarray) else \
+                raw.reshape(-1).view(np.uint8)
+            if a.size != self.F or hashlib.sha256(a).hexdigest().encode() != sl.fragment_list[f]:
+                rejected += 1  # wrong bytes: an erasure like a missing fragment
+                continue
+            good[f] = a
+        if len(good) < self.k:
+            raise ErrTooFewShards(f"segment {s}: {len(good)} of {self.n} fragments valid, "
+                                  f"need {self.k}")
+        return good, fetched, rejected
+
+    def _rebuild(self, todo, stats: dict) -> None:
+        """Rebuild the lost data fragments of [(s, good)] in place (one launch)."""
+        import torch
+        import cess_amd
+        if self.enc is None:
+            self.enc = cess_amd.New(self.k, self.m, device=self.device)
+            dev = torch.device("cuda", self.device)
+            self.d_data = torch.empty((self.B, self.k, self.F), dtype=torch.uint8, device=dev)
+            self.d_par = torch.empty((self.B, self.m, self.F), dtype=torch.uint8, device=dev)
+        nb = len(todo)
+        h_data = np.zeros((nb, self.k, self.F), np.uint8)
+        h_par = np.zeros((nb, self.m, self.F), np.uint8)
+        present = np.zeros((nb, self.n), np.uint8)
+        for i, (_s, good) in enumerate(todo):
+            for f, a in good.items():
+                (h_data[i, f] if f < self.k else h_par[i, f - self.k])[:] = a
+                present[i, f] = 1
+        self.d_data[:nb].copy_(torch.from_numpy(h_data))
+        self.d_par[:nb].copy_(torch.from_numpy(h_par))
+        self.enc.ReconstructBatch(self.d_data[:nb], self.d_par[:nb], nb, self.F, present,
+                                  data_only=True)
+        out = self.d_data[:nb].cpu().numpy()
+        for i, (_s, good) in enumerate(todo):
+            for f in range(self.k):
+                if f not in good:
+                    good[f] = out[i, f]
+        stats["rebuilt_segments"] += nb
+        stats["rebuilt_fragments"] += int(self.k * nb - present[:, :self.k].sum())
+
+    def retrieve(self, rec: FileRecord, fetch: FetchFn, out: Union[str, BinaryIO],
+                 check_segments: bool = True) -> dict:
+        """Write the file `rec` describes to `out` (a path or a binary file object) from the
+        fragments `fetch` returns. Raises ErrTooFewShards when a segment has fewer than k valid
+        fragments, ErrSegmentHashMismatch when a segment does not hash to its record (checked
+        unless check_segments=False), ErrRecordsInconsistent when the file hash does not match
+        the segment hashes. Returns counters (fragments fetched / rejected, segments and
+        fragments rebuilt on the GPU, seconds)."""
+        t0 = time.perf_counter()
+        if file_hash(rec.segments) != rec.file_hash:
+            raise ErrRecordsInconsistent("file hash is not SHA-256 over the segment hashes")
+        nseg = len(rec.segments)
+        if rec.size > nseg * self.seg or rec.size <= (nseg - 1) * self.seg:
+            raise ValueError(f"size {rec.size} does not fit {nseg} segments of {self.seg} bytes")
+        stats = {"segments": nseg, "fetched": 0, "rejected": 0, "rebuilt_segments": 0,
+                 "rebuilt_fragments": 0}
+        own = isinstance(out, str)
+        fo = open(out, "wb") if own else out
+        try:
+            written = 0
+            for b0 in range(0, nseg, self.B):
+                idx = list(range(b0, min(nseg, b0 + self.B)))
+                got = list(self.pool.map(lambda s: self._gather(s, rec.segments[s], fetch), idx))
+                goods = [g for g, _, _ in got]
+                stats["fetched"] += sum(n for _, n, _ in got)
+                stats["rejected"] += sum(r for _, _, r in got)
+                todo = [(s, g) for s, g in zip(idx, goods) if any(f not in g
+                                                                   for f in range(self.k))]
+                if todo:
+                    self._rebuild(todo, stats)
+
+                def check(i):
+                    segm = np.concatenate([goods[i][f] for f in range(self.k)])
+                    if (check_segments and hashlib.sha256(segm).hexdigest().encode()
+                            != rec.segments[idx[i]].hash):
+                        raise ErrSegmentHashMismatch(f"segment {idx[i]} does not match its "
+                                                     f"recorded hash")
+                    return segm
+                for segm in self.pool.map(check, range(len(idx))):
+                    take = min(self.seg, rec.size - written)
+                    fo.write(memoryview(segm[:take]))
+                    written += take
+        finally:
+            if own:
+                fo.close()
+        stats["bytes"] = rec.size
+        stats["seconds"] = round(time.perf_counter() - t0, 4)
+        return stats
+
+
+def retrieve_file(rec: FileRecord, fetch: FetchFn, out: Union[str, BinaryIO],
+                  k: int = geometry.DATA_SHARDS, m: int = geometry.PARITY_SHARDS,
+                  segment_size: int = geometry.SEGMENT_SIZE, device: int = 0, **kw) -> dict:
+    """One-shot Retriever(...).retrieve(rec, fetch, out)."""
+    with Retriever(k, m, segment_size, device, **kw) as r:
+        return r.retrieve(rec, fetch, out)
