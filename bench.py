@@ -231,6 +231,29 @@ def config1_cpu(args) -> dict:
             res["gpu_same_workload"] = {"GBps": round(ops * per_op / (ms * 1e-3) / GB, 2),
                                         "ms_per_step": round(ms, 4),
                                         "note": "one segment per launch: launch-latency bound"}
+            # the same step replayed as one HIP graph (the compile-time RS(2,1) kernels read no
+            # codec-owned memory, so their launches capture safely once warm)
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(st)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                cur = torch.cuda.current_stream(dev)
+                enc.EncodeBatch(d_data, d_par, 1, F, stream=cur)
+                for p in pats:
+                    enc.ReconstructBatch(d_data, d_par, 1, F, p, stream=cur)
+            torch.cuda.synchronize(dev)
+            with torch.cuda.stream(side):
+                for _ in range(5):
+                    g.replay()
+                a.record(side)
+                for _ in range(200):
+                    g.replay()
+                b.record(side)
+            torch.cuda.synchronize(dev)
+            gms = a.elapsed_time(b) / 200
+            res["gpu_same_workload"].update(
+                {"graph_ms_per_step": round(gms, 4),
+                 "graph_GBps": round(ops * per_op / (gms * 1e-3) / GB, 2)})
     except Exception as e:  # noqa: BLE001 - the CPU leg stands on its own
         res["gpu_same_workload"] = {"error": str(e)[:200]}
     return res

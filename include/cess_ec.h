@@ -84,7 +84,14 @@ int cec_verify(cec_codec* codec, uint8_t* const* shards, size_t shard_len, int* 
 
 /* Batched device-resident API. d_data: [nseg][k][shard_len], d_parity: [nseg][m][shard_len],
  * both in HBM. Work is enqueued on `hip_stream` (NULL = the HIP null stream, as in the HIP API)
- * and the call returns without waiting. */
+ * and the call returns without waiting.
+ * HIP graph capture: the calls whose kernels take compile-time coefficients and read no
+ * codec-owned memory may be captured (hipStreamBeginCapture on hip_stream) and replayed, after
+ * one uncaptured call of the same shape: cec_encode_batch of RS(2,1) and RS(32,32), and
+ * cec_reconstruct_batch of RS(2,1) with one pattern (per_segment = 0). Every other rebuild reads
+ * a decode program from the codec's cache, which may evict it while a graph still points at it:
+ * do not capture those. A single 16 MiB RS(2,1) segment's encode + three rebuilds: 29.5 us
+ * eagerly, 24.8 us as one graph (profiles/r05/graph_probe.log). */
 int cec_encode_batch(cec_codec* codec, const uint8_t* d_data, uint8_t* d_parity, size_t nseg,
                      size_t shard_len, void* hip_stream);
 /* Rebuild missing shards in place in the same layout. `present` is a host array of k+m flags

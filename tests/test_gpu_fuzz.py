@@ -76,3 +76,41 @@ def test_random_codes_against_oracle(torch, cess, corc, k, m, ln, nseg, seed):
                 else:  # data_only leaves an erased parity shard as it was
                     assert np.array_equal(got_p[s, j], junk_h[s, k + j]), (s, j)
     enc.close()
+
+
+def test_graph_capture_of_compile_time_calls(torch, cess, corc):
+    """The capturable calls (include/cess_ec.h: RS(2,1) and RS(32,32) encodes, RS(2,1) rebuilds
+    of one pattern) replayed from one HIP graph read the buffers at replay time: new data written
+    between replays comes out with the C oracle's parity, and every erased fragment rebuilt."""
+    from oracle.c_oracle import c_encode
+    for k, m, ln, nseg in ((2, 1, (1 << 16) + 48, 3), (32, 32, 4096, 2)):
+        enc = cess.New(k, m)
+        d_data = torch.empty((nseg, k, ln), dtype=torch.uint8, device="cuda")
+        d_par = torch.empty((nseg, m, ln), dtype=torch.uint8, device="cuda")
+        side = torch.cuda.Stream()
+        pats = ([np.array([int(i != e) for i in range(k + m)], np.uint8) for e in range(k + m)]
+                if k == 2 else [])
+
+        def step(st):
+            enc.EncodeBatch(d_data, d_par, nseg, ln, stream=st)
+            for p in pats:
+                enc.ReconstructBatch(d_data, d_par, nseg, ln, p, stream=st)
+        cess.fill_synthetic(d_data, k * ln, nseg, 0, 77)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            step(side)  # the uncaptured call of the same shape
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            step(torch.cuda.current_stream())
+        for seed in (5, 6):
+            cess.fill_synthetic(d_data, k * ln, nseg, 0, seed)
+            d_par.zero_()
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            data, par = d_data.cpu().numpy(), d_par.cpu().numpy()
+            for s in range(nseg):
+                want = np.stack(c_encode(corc, k, m, [data[s, i] for i in range(k)]))
+                assert np.array_equal(par[s], want), (k, m, seed, s)
+        enc.close()
