@@ -935,6 +935,17 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
     return out
 
 
+def guarded(leg, *a) -> dict:
+    """Run one `extra` leg; an exception becomes {"error": ...} in the line instead of costing
+    the whole line (line_problems still flags the leg)."""
+    try:
+        return leg(*a)
+    except Exception as e:  # noqa: BLE001 - reported in the line
+        import torch
+        torch.cuda.empty_cache()
+        return {"error": f"{type(e).__name__}: {e}"[:400]}
+
+
 def line_problems(out: dict) -> list:
     """What a bench line lacks against the driver's contract and VERDICT's asks (empty = none):
     the contract keys, `roofline` and `cpu_baseline` at every N (at N > 1 on the CPU share of the
@@ -975,6 +986,8 @@ def line_problems(out: dict) -> list:
         c5 = ex.get("config5") or {}
         if not c5.get("digests_match_hashlib") or not c5.get("step_GBps"):
             bad.append("extra.config5 missing or its digests unchecked")
+        if "error" in (ex.get("wide_code") or {}):
+            bad.append(f"extra.wide_code: {ex['wide_code']['error']}")
         for name, leg in (ex.get("wide_code") or {}).items():
             if isinstance(leg, dict) and "ms" in leg and not any(
                     key.startswith("cold_ms") for key in leg):
@@ -1411,10 +1424,11 @@ def main() -> None:
     if not args.no_extra and args.config == 2:
         # BASELINE config 4's strong-scaling encode (64 GiB over the N GPUs, T1 on one GPU beside
         # it) at every N: the driver only ever runs the default command
-        out.setdefault("extra", {})["config4"] = config4_leg(dev, local, world, rank, backend)
+        out.setdefault("extra", {})["config4"] = guarded(config4_leg, dev, local, world, rank,
+                                                         backend)
         # the host-resident path at every N: a file per GPU through the C pipeline
         # (PCIe-inclusive; the north_star's pinned double-buffering, sharded per GPU)
-        out["extra"]["host_e2e"] = host_e2e_leg(dev, local, world, rank, backend)
+        out["extra"]["host_e2e"] = guarded(host_e2e_leg, dev, local, world, rank, backend)
 
     cabi_pending = False
     if args.config == 4:
@@ -1467,9 +1481,9 @@ def main() -> None:
             # holds ~100 GiB of parity per rank: ranks sharing a GPU in the rehearsal do not fit).
             # The wide code (BASELINE config 5's RS(32,32), 16 MiB segments: F = 512 KiB), so the
             # driver's own line carries its encode, restoral and multi-erasure rebuild rates
-            out["extra"]["wide_code"] = wide_code_legs(dev, local, stream)
+            out["extra"]["wide_code"] = guarded(wide_code_legs, dev, local, stream)
             # BASELINE config 5 (RS(32,32) encode + SHA-256 of every fragment) as the driver runs
-            out["extra"]["config5"] = config5_leg(dev, local)
+            out["extra"]["config5"] = guarded(config5_leg, dev, local)
         # the measured-copy ceiling beside the spec peak: a device-to-device copy
         # of the same 1 GiB data batch (HIP's blit kernel), read + write bytes per copy
         src = d_data.view(-1)
