@@ -239,10 +239,24 @@ impl<'c> DistGroup<'c> {
         Ok(DistGroup { d, _codec: std::marker::PhantomData })
     }
 
-    /// Exchange of later degraded reads: 0 survivors (default), 1 partial products, 2 per
-    /// segment whichever moves fewer fragments (the same value on every rank).
+    /// Exchange of later degraded reads: 0 survivors, 1 partial products, 2 per segment
+    /// whichever moves fewer fragments (the default of a new group; the same value on every
+    /// rank).
     pub fn set_exchange(&mut self, exchange: i32) -> Result<(), Error> {
         check(unsafe { sys::cec_dist_set_option(self.d, sys::CEC_DIST_OPT_EXCHANGE, exchange) })
+    }
+
+    /// At most `ops` point-to-point transfers per rank in one RCCL group (default 1024; 0 = one
+    /// group per round of 256 segments; the same value on every rank).
+    pub fn set_group_ops(&mut self, ops: i32) -> Result<(), Error> {
+        check(unsafe { sys::cec_dist_set_option(self.d, sys::CEC_DIST_OPT_GROUP_OPS, ops) })
+    }
+
+    /// Transfer groups this handle has issued so far.
+    pub fn groups(&self) -> Result<u64, Error> {
+        let mut g = 0u64;
+        check(unsafe { sys::cec_dist_groups(self.d, &mut g) })?;
+        Ok(g)
     }
 
     /// Rebuild the `lost` (segment, fragment) list, the same on every rank; `locate(seg, frag)`
