@@ -901,7 +901,7 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
                     "PCIe Gen5 x16 = 63 GB/s per direction per GPU"}
     recs = {}
     for name, hashing in (("no_hash", False), ("segment_lists", True)):
-        with Pipeline(enc, F, batch_segments=64, depth=3, hash=hashing, window=16) as p:
+        with Pipeline(enc, F, batch_segments=64, depth=3, hash=hashing, window=32) as p:
             p.run(buf[:64 * seg_bytes])  # warm-up: pinned ring, device slots, hash queue
             barrier()
             t0 = time.perf_counter()

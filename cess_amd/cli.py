@@ -102,7 +102,7 @@ def main(argv=None) -> int:
     e.add_argument("--k", type=int, default=geometry.DATA_SHARDS)
     e.add_argument("--m", type=int, default=geometry.PARITY_SHARDS)
     e.add_argument("--segment-size", type=int, default=geometry.SEGMENT_SIZE)
-    e.add_argument("--window", type=int, default=16)
+    e.add_argument("--window", type=int, default=32)
     e.add_argument("--device", type=int, default=0)
     e.add_argument("--no-segment-limit", action="store_true")
     v = sub.add_parser("verify")

@@ -107,12 +107,18 @@ struct cec_pipeline {
     depth = o.depth ? o.depth : 3;
     if (depth < 2) return cec::set_error(CEC_EINVAL, "depth must be >= 2");
     hash = o.hash != 0;
-    window = o.window ? o.window : 16;
+    window = o.window ? o.window : 32;
     if (window < 1) return cec::set_error(CEC_EINVAL, "window must be >= 1");
     max_segments = o.max_segments;
     // a slot is reused nd batches later; its hashes are final `window` ticks after its add, and
     // two more slots keep the H2D of a reused slot from waiting on the tick just enqueued
     nd = hash ? window + 3 : 3;
+    // a device slot's events are re-recorded by its next batch: that batch (i + nd) must come
+    // after the slot's previous batch has delivered its fragments, which the host ring guarantees
+    // only for batches `depth` apart (with depth > nd the wait for an old batch's parity copy
+    // became a wait for the newest one, and the ring ran one batch deep: 27-33 GB/s at depth 4
+    // against 49-52 at depth 3, profiles/r05/e2e_sweep.jsonl)
+    nd = std::max(nd, depth);
     PL_TRY(hipSetDevice(device));
     for (hipStream_t* s : {&s_h2d, &s_comp, &s_d2h})
       PL_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));

@@ -85,7 +85,7 @@ class Pipeline:
     segments, GPU SegmentList hashing over a window of `window` batches when hash=True."""
 
     def __init__(self, enc: Encoder, shard_len: int = geometry.FRAGMENT_SIZE,
-                 batch_segments: int = 64, depth: int = 3, hash: bool = True, window: int = 16,
+                 batch_segments: int = 64, depth: int = 3, hash: bool = True, window: int = 32,
                  max_segments: int = 0):
         self.enc = enc
         self.k, self.m = enc.DataShards, enc.ParityShards

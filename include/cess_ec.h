@@ -210,7 +210,8 @@ typedef struct cec_pipeline_opts {
   size_t batch_segments; /* segments per batch (0: 64) */
   int depth;             /* pinned host batches (0: 3; >= 2) */
   int hash;              /* 1: SegmentList hashes on the GPU (on_record); 0: none */
-  int window;            /* batches hashing at once when hash = 1 (0: 16) */
+  int window;            /* batches hashing at once when hash = 1 (0: 32); the pipeline holds
+                            window + 3 device batch slots (1.5 GiB each for CESS batches) */
   uint64_t max_segments; /* 0: no limit; else CEC_ESEGCOUNT when the source has more segments
                             (CEC_SEGMENT_COUNT: what one upload_declaration can carry) */
 } cec_pipeline_opts;

@@ -2,7 +2,8 @@
 """Host-resident pipeline sweep (PCIe-inclusive): an in-memory file through cec_pipeline with
 different batch sizes, ring depths and hash windows; one JSON line per setting.
 
-usage: python tools/e2e_sweep.py [--gib 8]"""
+usage: python tools/e2e_sweep.py [--gib 8] [--batches 8,16,32,64] [--depths 3,4]
+                                 [--windows 16,32,64]"""
 import argparse
 import json
 import os
@@ -22,6 +23,9 @@ MiB = 1 << 20
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=int, default=8)
+    ap.add_argument("--batches", default="8,16,32,64")
+    ap.add_argument("--depths", default="3,4")
+    ap.add_argument("--windows", default="16,32,64")
     args = ap.parse_args()
     k, m, F = 2, 1, 8 * MiB
     seg = k * F
@@ -36,9 +40,9 @@ def main():
     del d
     enc = cess_amd.New(k, m)
     for hashing in (False, True):
-        for batch in (8, 16, 32, 64):
-            for depth in (3, 4):
-                for window in ((16, 32, 64) if hashing else (16,)):
+        for batch in [int(x) for x in args.batches.split(",")]:
+            for depth in [int(x) for x in args.depths.split(",")]:
+                for window in ([int(x) for x in args.windows.split(",")] if hashing else (16,)):
                     with Pipeline(enc, F, batch_segments=batch, depth=depth, hash=hashing,
                                   window=window) as p:
                         p.run(buf[:batch * seg])
