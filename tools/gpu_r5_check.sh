@@ -21,5 +21,5 @@ step() {
 step pytest_gpu 900 python -u -m pytest tests -m gpu --maxfail=5 -v --timeout 200 --timeout-method thread
 step smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()"
 step bench 400 python -u bench.py
-step rocprof_bench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench -- python3 -u bench.py
+step rocprof_bench 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 -u bench.py
 echo done
