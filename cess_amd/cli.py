@@ -1,6 +1,6 @@
 """cess-ec command line.
 
-  python -m cess_amd.cli encode <file> [--out DIR] [--scale FILE] [--k 2 --m 1]
+  python -m cess_amd.cli encode <file> [--out DIR] [--scale FILE] [--k 2 --m 1] [--devices 0,1,..]
       streams the file through the GPU (libcessec host pipeline: pinned multi-buffered copies,
       RS encode, GPU SegmentList hashes) and prints the file's SegmentList records (the
       deal_info of FileBank::upload_declaration, c-pallets/file-bank/src/lib.rs:419-428) as
@@ -40,10 +40,24 @@ def _encode(args) -> int:
                 f.write(memoryview(view))
             tmp[(seg, idx)] = path
     limit = 0 if args.no_segment_limit else geometry.SEGMENT_COUNT
+    if args.devices and args.out:
+        print("--devices (several GPUs) does not write fragments; drop --out", file=sys.stderr)
+        return 2
     try:
-        rec, st = encode_file_records(args.file, args.k, args.m, args.segment_size, args.device,
-                                      on_fragment=writer, max_segments=limit,
-                                      window=args.window)
+        if args.devices:
+            from .pipeline import encode_file_records_multi
+            devs = [int(x) for x in args.devices.split(",")]
+            rec, sts = encode_file_records_multi(args.file, devs, args.k, args.m,
+                                                 args.segment_size, max_segments=limit,
+                                                 window=args.window)
+            st = sts[0]
+            st.seconds = max(x.seconds for x in sts)
+            st.read_seconds = max(x.read_seconds for x in sts)
+            st.bytes_in = sum(x.bytes_in for x in sts)
+        else:
+            rec, st = encode_file_records(args.file, args.k, args.m, args.segment_size,
+                                          args.device, on_fragment=writer, max_segments=limit,
+                                          window=args.window)
     except ErrTooManySegments:
         for p in tmp.values():
             os.unlink(p)
@@ -104,6 +118,9 @@ def main(argv=None) -> int:
     e.add_argument("--segment-size", type=int, default=geometry.SEGMENT_SIZE)
     e.add_argument("--window", type=int, default=32)
     e.add_argument("--device", type=int, default=0)
+    e.add_argument("--devices", default="",
+                   help="comma list of GPUs: the file's segments sharded over them from this "
+                        "process (contiguous ranges, one pipeline per GPU)")
     e.add_argument("--no-segment-limit", action="store_true")
     v = sub.add_parser("verify")
     v.add_argument("file")

@@ -27,7 +27,8 @@ class _Reader:
     """read() callback over a path (parallel os.preadv, GIL released), an in-memory buffer
     (parallel numpy copies) or a binary stream (readinto)."""
 
-    def __init__(self, src: Source, threads: int = 8):
+    def __init__(self, src: Source, threads: int = 8, start: int = 0,
+                 stop: Optional[int] = None):
         self.pool = cf.ThreadPoolExecutor(max_workers=threads)
         self.threads = threads
         self.fd = self.arr = self.stream = None
@@ -35,11 +36,17 @@ class _Reader:
         if isinstance(src, str):
             self.fd = os.open(src, os.O_RDONLY)
             self.size = os.fstat(self.fd).st_size
+            self.pos = start  # absolute offsets in the file: bytes [start, stop)
+            if stop is not None:
+                self.size = min(self.size, stop)
         elif isinstance(src, (bytes, bytearray, memoryview, np.ndarray)):
-            self.arr = (src.reshape(-1).view(np.uint8) if isinstance(src, np.ndarray)
-                        else np.frombuffer(src, np.uint8))
+            arr = (src.reshape(-1).view(np.uint8) if isinstance(src, np.ndarray)
+                   else np.frombuffer(src, np.uint8))
+            self.arr = arr[start:stop]
             self.size = self.arr.size
         else:
+            if start or stop is not None:
+                raise ValueError("a byte range needs a path or an in-memory source")
             self.stream = src
             self.size = None
 
@@ -117,13 +124,15 @@ class Pipeline:
     def run(self, src: Source,
             on_fragments: Optional[Callable[[int, list], None]] = None,
             on_record: Optional[Callable[[int, bytes, list], None]] = None,
-            read_threads: int = 8) -> _lib.PipelineStats:
-        """Stream `src` through the GPU. on_fragments(seg, [k+m uint8 views]) sees every
-        segment's shards (views valid during the call only); on_record(seg, seg_hex,
+            read_threads: int = 8, start: int = 0,
+            stop: Optional[int] = None) -> _lib.PipelineStats:
+        """Stream `src` (bytes [start, stop) of a path or an in-memory buffer) through the GPU.
+        on_fragments(seg, [k+m uint8 views]) sees every segment's shards (views valid during the
+        call only; seg counts from the range's first segment); on_record(seg, seg_hex,
         [k+m fragment hex]) its hashes (hash=True). Returns the run's PipelineStats."""
         n = self.k + self.m
         F = self.F
-        reader = _Reader(src, read_threads)
+        reader = _Reader(src, read_threads, start, stop)
         err = []
 
         def rd(_u, dst, cap):
@@ -204,4 +213,54 @@ def encode_file_records(path_or_buf: Source, k: int = geometry.DATA_SHARDS,
     return out, st
 
 
-__all__ = ["Pipeline", "encode_file_records", "CecError"]
+def encode_file_records_multi(src: Union[str, bytes, bytearray, memoryview, np.ndarray],
+                              devices, k: int = geometry.DATA_SHARDS,
+                              m: int = geometry.PARITY_SHARDS,
+                              segment_size: int = geometry.SEGMENT_SIZE,
+                              max_segments: int = 0, read_threads: int = 8, **kw):
+    """File -> FileRecord with the segments sharded over several GPUs from ONE host process (an
+    uploader on a multi-GPU node): contiguous segment ranges per device
+    (distributed.shard_range; segments are independent, no data exchange), one C pipeline per
+    device on its own host thread (pinned multi-buffered copies per GPU), records merged in
+    segment order. `devices` may repeat a device (several pipelines sharing one GPU).
+    Returns (FileRecord, [PipelineStats per device])."""
+    from .distributed import shard_range
+    from .segments import FileRecord, SegmentList, file_hash
+    size = os.path.getsize(src) if isinstance(src, str) else (
+        src.nbytes if isinstance(src, np.ndarray) else len(src))
+    if size == 0:
+        from .reedsolomon import ErrShortData
+        raise ErrShortData(ErrShortData.__doc__)
+    nseg = -(-size // segment_size)
+    if max_segments and nseg > max_segments:
+        from .records import ErrTooManySegments
+        raise ErrTooManySegments(ErrTooManySegments.__doc__)
+    devices = list(devices)
+    kw.setdefault("batch_segments", max(1, min(64, -(-nseg // len(devices)))))
+
+    def work(i):
+        a, b = shard_range(nseg, len(devices), i)
+        if b <= a:
+            return {}, None
+        recs = {}
+        enc = Encoder(k, m, devices[i])
+        try:
+            with Pipeline(enc, segment_size // k, **kw) as p:
+                st = p.run(src, on_record=lambda s, sh, fl: recs.__setitem__(
+                    a + s, SegmentList(sh, fl)), read_threads=read_threads,
+                    start=a * segment_size, stop=min(size, b * segment_size))
+        finally:
+            enc.close()
+        return recs, st
+
+    with cf.ThreadPoolExecutor(max_workers=len(devices)) as ex:
+        parts = list(ex.map(work, range(len(devices))))
+    recs = {}
+    for r, _ in parts:
+        recs.update(r)
+    out = FileRecord(b"", size, [recs[s] for s in range(nseg)])
+    out.file_hash = file_hash(out.segments)
+    return out, [st for _, st in parts if st is not None]
+
+
+__all__ = ["Pipeline", "encode_file_records", "encode_file_records_multi", "CecError"]

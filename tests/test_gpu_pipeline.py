@@ -127,3 +127,41 @@ def test_pipelines_on_threads(orc):
 
     with cf.ThreadPoolExecutor(len(jobs)) as ex:
         assert all(ex.map(run, jobs))
+
+
+@pytest.mark.parametrize("devices,size,seg,k,m", [([0, 0, 0], 7 * MiB + 5, MiB, 2, 1),
+                                                  ([0, 0], 3 * MiB, MiB // 2, 4, 2),
+                                                  ([0, 0, 0, 0, 0], 2 * MiB, MiB, 2, 1)])
+def test_multi_device_file_records(orc, tmp_path, devices, size, seg, k, m):
+    """One host process sharding a file's segments over several pipelines (here several on GPU 0,
+    as an uploader on an 8-GPU node would use 8 devices): the merged records equal the oracle's,
+    from an in-memory buffer and from a path; more devices than segments leaves some idle."""
+    from cess_amd.pipeline import encode_file_records_multi
+    blob = np.random.default_rng(size).integers(0, 256, size, dtype=np.uint8).tobytes()
+    want = orc.segment_list(blob, k, m, seg)
+    path = tmp_path / "f.bin"
+    path.write_bytes(blob)
+    for src in (blob, str(path)):
+        rec, stats = encode_file_records_multi(src, devices, k, m, seg, window=2)
+        assert [(s.hash, s.fragment_list) for s in rec.segments] == want
+        assert rec.file_hash == orc.file_hash(want) and rec.size == size
+        assert sum(st.segments for st in stats) == len(want)
+
+
+def test_cli_encode_devices(tmp_path):
+    """`cli encode --devices 0,0` (segments sharded over two pipelines) prints the same records
+    as the one-device encode."""
+    import contextlib
+    import io
+    from cess_amd import cli
+    blob = np.random.default_rng(11).integers(0, 256, 3 * MiB + 7, dtype=np.uint8).tobytes()
+    src = tmp_path / "f.bin"
+    src.write_bytes(blob)
+    outs = []
+    for extra in ([], ["--devices", "0,0"]):
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            assert cli.main(["encode", str(src), "--segment-size", str(MiB)] + extra) == 0
+        outs.append(json.loads(buf.getvalue().strip().splitlines()[-1]))
+    assert outs[0]["segments"] == outs[1]["segments"]
+    assert outs[0]["file_hash"] == outs[1]["file_hash"]
