@@ -19,8 +19,14 @@ share device 0.
 Rank 0 prints one JSON line. `roofline` is the dominant kernel's algorithmic bytes per launch /
 its average launch time (HIP events on the launch stream); `cpu_baseline` times the C oracle
 (oracle/rs_oracle.c, kind "port": the reference ships no codec) on a bounded sample on rank 0.
-With N > 1 the default line also carries `extra.degraded_gather`: the RCCL survivor gather of
-BASELINE config 4 (fragment f of segment s on GPU (s + f) mod N) and the rebuild after it.
+The default line also carries, at every N: `extra.config4` (BASELINE config 4's 64 GiB file
+sharded over the N GPUs, T1 on one GPU, efficiency T1 / (N T_N), sampled segments checked against
+the C oracle) and `extra.host_e2e` (an in-memory file per GPU through the C pipeline,
+PCIe-inclusive, with and without SegmentList hashing); at N = 1 the one-GPU legs (reconstruct,
+`extra.wide_code`: RS(32,32) encode / restoral / rebuilds / verify, `extra.config5`: BASELINE
+config 5's encode + SHA-256 step); at N > 1 `extra.degraded_gather` and its wide-code and C-ABI
+forms: the RCCL survivor / partial-product exchange of BASELINE config 4 (fragment f of segment s
+on GPU (s + f) mod N) and the rebuild after it.
 Config 1 is the CPU codec alone (one 16 MiB segment: encode + the 3 single-erasure rebuilds at
 1 thread and at the host's CPU share); config 4 is 64 GiB sharded over the ranks with the
 degraded-read gather inside every step.

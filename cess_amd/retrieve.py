@@ -170,7 +170,11 @@ class Retriever:
         stats = {"segments": nseg, "fetched": 0, "rejected": 0, "rebuilt_segments": 0,
                  "rebuilt_fragments": 0}
         own = isinstance(out, str)
-        fo = open(out, "wb") if own else out
+        # a path is written under a temporary name and renamed once every segment checked out:
+        # a failed retrieval leaves no partial file behind
+        tmp = out + ".part" if own else None
+        fo = open(tmp, "wb") if own else out
+        ok = False
         try:
             written = 0
             for b0 in range(0, nseg, self.B):
@@ -195,9 +199,14 @@ class Retriever:
                     take = min(self.seg, rec.size - written)
                     fo.write(memoryview(segm[:take]))
                     written += take
+            ok = True
         finally:
             if own:
                 fo.close()
+                if ok:
+                    os.replace(tmp, out)
+                else:
+                    os.unlink(tmp)
         stats["bytes"] = rec.size
         stats["seconds"] = round(time.perf_counter() - t0, 4)
         return stats

@@ -81,6 +81,22 @@ def test_too_few_valid_fragments_fail_before_any_rebuild():
     r.close()
 
 
+def test_failed_retrieval_leaves_no_file(tmp_path):
+    """Retrieving to a path: written under a temporary name, renamed only when every segment
+    checked out; a failure removes it."""
+    k, m, seg = 2, 1, 1 << 14
+    blob, rec, frags = _file(3 * seg + 5, k, m, seg)
+    out = tmp_path / "f.bin"
+    retrieve_file(rec, _fetch(frags), str(out), k, m, seg)
+    assert out.read_bytes() == blob and not (tmp_path / "f.bin.part").exists()
+    bad = dict(frags)
+    del bad[(2, 0)], bad[(2, 1)]
+    out2 = tmp_path / "g.bin"
+    with pytest.raises(ErrTooFewShards):
+        retrieve_file(rec, _fetch(bad), str(out2), k, m, seg)
+    assert not out2.exists() and not (tmp_path / "g.bin.part").exists()
+
+
 def test_segment_hash_checked():
     """Fragments that hash right but a segment record that does not match: refused."""
     k, m, seg = 2, 1, 1 << 14
