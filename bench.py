@@ -846,6 +846,12 @@ def config4_leg(dev, local: int, world: int, rank: int, backend: str, reps: int 
                 "segments_checked_per_rank": tn[3],
                 "checker": "C oracle (oracle/rs_oracle.c) on sampled segments of every shard, "
                            "after the timed passes"})
+    # HBM bytes of the whole-file launch from the PMC passes (tools/r05_pmc_c4.sh)
+    tr = load_traffic("c4", total * per_seg, "k_ct<EncCT<2, 1>>")
+    if tr is not None:
+        out["t1_traffic"] = {"bytes_per_launch": tr,
+                             "over_algorithmic": round(tr / (total * per_seg), 6),
+                             "source": traffic_source("c4")}
     if t1 is not None:
         out["efficiency"] = round(t1[0] / (world * tn_ms), 4)
         out["efficiency_basis"] = "T1 / (N x T_N), HIP-event times per pass, T_N max over ranks"
