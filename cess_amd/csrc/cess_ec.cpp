@@ -439,6 +439,7 @@ struct PsPlan {
   std::vector<std::pair<ProgPtr, std::pair<size_t, size_t>>> ct;
   std::vector<PsLaunch> rt;
   size_t mixed_off = 0, mixed_count = 0;  // tagged list (segment | erased << 30), count 0: none
+  std::vector<uint8_t> mixed_e;  // the same erasures per segment in natural order (variant 90)
   struct FdLaunch {
     int side;           // 0, 1: syndrome-row decoder of that side; 2: formal derivative
     bool big;           // cec::fftdec_big of the plans' syndrome slot count
@@ -945,6 +946,8 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
       plan->mixed_off = hl.size();
       plan->mixed_count = tagged.size();
       hl.insert(hl.end(), tagged.begin(), tagged.end());
+      plan->mixed_e.assign(nseg, 2);
+      for (uint32_t w : tagged) plan->mixed_e[w & 0x3FFFFFFFu] = (uint8_t)(w >> 30);
     }
   } else {
     size_t maxchunks = 0;
@@ -1005,6 +1008,10 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
 }
 
 int launch_ps_plan(cec_codec* c, const PsPlan& p, const Layout& L, hipStream_t st) {
+  if (p.mixed_count && c->opts.ct_variant == 90 &&
+      cec::launch_decode1_mixed_kargs(c->k, c->m, L, p.mixed_e.data(),
+                                      (uint32_t)p.mixed_e.size(), st))
+    return check_launch();
   if (p.mixed_count &&
       cec::launch_decode1_mixed(c->opts, c->k, c->m, L, p.list + p.mixed_off,
                                 (uint32_t)p.mixed_count, st))

@@ -63,6 +63,9 @@ bool launch_decode_ct(const KernelOpts& o, int k, int m, int missing, const Layo
                       const uint32_t* seg_list, uint32_t nseg, hipStream_t st);
 // RS(2,1) single erasures, a different one per segment, in one launch: tagged[i] = segment |
 // (erased index << 30) for the nseg segments of the launch. False if not applicable.
+// tuning variant 90 (libcessec_tune.so only; false elsewhere): erasures in the kernel arguments
+bool launch_decode1_mixed_kargs(int k, int m, const Layout& L, const uint8_t* erased,
+                                uint32_t nseg, hipStream_t st);
 bool launch_decode1_mixed(const KernelOpts& o, int k, int m, const Layout& L,
                           const uint32_t* tagged, uint32_t nseg, hipStream_t st);
 

@@ -1394,7 +1394,7 @@ void run_wide_variant(const KernelOpts& o, const Layout& L, const uint32_t* seg_
 }  // namespace
 
 #ifdef CEC_TUNING
-int max_ct_variant() { return 86; }  // 70, 72..78, 83, 85: the derivative decoder forms, 79..82, 84, 86 the syndrome-row decoder's (cess_ec.cpp fdd_form)
+int max_ct_variant() { return 90; }  // 70, 72..78, 83, 85: the derivative decoder forms, 79..82, 84, 86 the syndrome-row decoder's (cess_ec.cpp fdd_form)
 #else
 int max_ct_variant() { return 0; }
 #endif
@@ -1442,6 +1442,43 @@ bool launch_decode1_mixed(const KernelOpts& o, int k, int m, const Layout& L,
                        L, tagged, s0);
   });
   return true;
+}
+
+#ifdef CEC_TUNING
+// Tuning variant 90: the mixed-pattern RS(2,1) rebuild with the per-segment erasure passed in
+// the kernel arguments (2 bits per segment row, 64 rows per launch, segments in natural order)
+// instead of a tagged list each workgroup loads first.
+template <bool NT, int BS>
+__global__ __launch_bounds__(BS) void k_ct_dec1_mixed21_kargs(Layout L, uint32_t seg0,
+                                                              uint64_t t0, uint64_t t1) {
+  const uint32_t y = blockIdx.y;
+  const uint64_t w = y < 32 ? t0 : t1;
+  const uint32_t e = (uint32_t)(w >> (2 * (y & 31))) & 3u;
+  const uint32_t seg = seg0 + y;
+  if (e == 0) ct_tile<Dec1CT<2, 1, 0>, 1, NT, u32x4, 1, false, BS>(L, seg);
+  else if (e == 1) ct_tile<Dec1CT<2, 1, 1>, 1, NT, u32x4, 1, false, BS>(L, seg);
+  else ct_tile<EncCT<2, 1>, 1, NT, u32x4, 1, false, BS>(L, seg);
+}
+#endif
+
+bool launch_decode1_mixed_kargs(int k, int m, const Layout& L, const uint8_t* erased,
+                                uint32_t nseg, hipStream_t st) {
+#ifdef CEC_TUNING
+  if (k != 2 || m != 1 || !layout_vec16_ok(L)) return false;
+  uint64_t gx = (L.len / 16 + 255) / 256;
+  if (gx == 0) gx = 1;
+  for (uint32_t s0 = 0; s0 < nseg; s0 += 64) {
+    const uint32_t ny = nseg - s0 < 64 ? nseg - s0 : 64;
+    uint64_t t[2] = {0, 0};
+    for (uint32_t y = 0; y < ny; ++y) t[y >> 5] |= (uint64_t)(erased[s0 + y] & 3u) << (2 * (y & 31));
+    hipLaunchKernelGGL((k_ct_dec1_mixed21_kargs<true, 256>), dim3((unsigned)gx, ny), dim3(256), 0,
+                       st, L, s0, t[0], t[1]);
+  }
+  return true;
+#else
+  (void)k; (void)m; (void)L; (void)erased; (void)nseg; (void)st;
+  return false;
+#endif
 }
 
 bool launch_decode_ct(const KernelOpts& o, int k, int m, int missing, const Layout& L,
