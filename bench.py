@@ -1524,6 +1524,11 @@ def main() -> None:
         out["cpu_baseline"]["node_GBps_gpu"] = out["value"]
         if args.config == 5:
             out["cpu_baseline"]["sha256"] = cpu_sha256(k, m, F, args.cpu_seconds / 2)
+        elif args.config == 2 and world == 1 and not args.no_extra:
+            # the default line carries config 5's step (extra.config5): its hashing's CPU
+            # baseline beside it (OpenSSL SHA-256, SHA-NI where the host has it)
+            wk, wm, wF = CONFIGS[5][:3]
+            out["cpu_baseline"]["sha256"] = cpu_sha256(wk, wm, wF, args.cpu_seconds / 2)
 
     if cabi_pending:
         cabi_legs(out["extra"], gather_leg, degraded_gather, enc, (k, m, F), world, rank, dev,
