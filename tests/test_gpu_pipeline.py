@@ -165,3 +165,54 @@ def test_cli_encode_devices(tmp_path):
         outs.append(json.loads(buf.getvalue().strip().splitlines()[-1]))
     assert outs[0]["segments"] == outs[1]["segments"]
     assert outs[0]["file_hash"] == outs[1]["file_hash"]
+
+
+def _pipeline_cases(n, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        k, m = [(2, 1), (4, 2), (10, 4), (3, 5)][int(rng.integers(4))]
+        F = int(rng.choice([4096, 4160, 65536, 1000 * 64]))
+        nseg = int(rng.integers(1, 23))
+        tail = int(rng.integers(0, k * F))
+        out.append((k, m, F, nseg, tail, int(rng.choice([1, 2, 3, 5, 8])),
+                    int(rng.choice([2, 3, 4, 6])), int(rng.choice([1, 2, 3, 7])),
+                    bool(rng.integers(2)), int(rng.integers(1 << 30))))
+    return out
+
+
+@pytest.mark.parametrize("k,m,F,nseg,tail,batch,depth,window,hashing,seed",
+                         _pipeline_cases(16, 505))
+def test_pipeline_random_shapes(orc, k, m, F, nseg, tail, batch, depth, window, hashing, seed):
+    """Randomized ring shapes (batch size, ring depth deeper or shallower than the device slots,
+    hash window) over files with ragged tails: every segment's shards equal the oracle's split +
+    encode (zero-padded tail), in segment order, and with hashing every record equals the
+    oracle's SegmentList."""
+    import cess_amd
+    from cess_amd.pipeline import Pipeline
+    seg = k * F
+    size = max(1, (nseg - 1) * seg + tail)
+    blob = np.random.default_rng(seed).integers(0, 256, size, dtype=np.uint8).tobytes()
+    want = orc.segment_list(blob, k, m, seg) if hashing else None
+    rs = orc.ReedSolomon(k, m)
+    seen, recs = [], {}
+
+    def frags(s, views):
+        padded = np.zeros(seg, np.uint8)
+        chunk = np.frombuffer(blob[s * seg:(s + 1) * seg], np.uint8)
+        padded[:len(chunk)] = chunk
+        shards = rs.split(padded.tobytes())
+        shards[k:] = rs.encode(shards[:k])
+        assert all(np.array_equal(v, np.asarray(x, np.uint8)) for v, x in zip(views, shards)), s
+        seen.append(s)
+
+    enc = cess_amd.New(k, m)
+    with Pipeline(enc, F, batch_segments=batch, depth=depth, hash=hashing, window=window) as p:
+        st = p.run(blob, on_fragments=frags,
+                   on_record=(lambda s, sh, fl: recs.__setitem__(s, (sh, list(fl))))
+                   if hashing else None)
+    enc.close()
+    nsegs = -(-size // seg)
+    assert seen == list(range(nsegs)) and st.segments == nsegs
+    if hashing:
+        assert [recs[s] for s in range(nsegs)] == [(h, list(fl)) for h, fl in want]
