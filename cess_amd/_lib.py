@@ -179,6 +179,15 @@ def load(tuning: bool = False) -> ctypes.CDLL:
             raise OSError(f"libcessec not found at {path}: build it with "
                           "`python -c 'import __graft_entry__ as g; g.build()'` "
                           "or `make -C cess_amd/csrc`")
+        # One HIP runtime per process: torch's wheel carries its own libamdhip64 (SONAME
+        # libamdhip64.so.7, but its libraries NEED it as "libamdhip64.so"). Loaded after torch,
+        # libcessec binds to torch's copy by SONAME; loaded first, it maps /opt/rocm's, torch
+        # later maps a second runtime beside it and its device init fails ("No HIP GPUs are
+        # available"). So torch, when present, goes first.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)

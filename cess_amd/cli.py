@@ -1,8 +1,11 @@
 """cess-ec command line.
 
   python -m cess_amd.cli encode <file> [--out DIR] [--scale FILE] [--k 2 --m 1] [--devices 0,1,..]
-      streams the file through the GPU (libcessec host pipeline: pinned multi-buffered copies,
-      RS encode, GPU SegmentList hashes) and prints the file's SegmentList records (the
+                                   [--hash-on auto|gpu|host]
+      streams the file through the GPU (RS encode; SegmentList hashes by --hash-on: "gpu" =
+      libcessec host pipeline with pinned multi-buffered copies and GPU hashing, "host" = SHA-NI
+      threads beside the GPU encode, "auto" = the host below 20 GiB, where it finishes sooner,
+      pipeline.AUTO_GPU_RECORD_BYTES) and prints the file's SegmentList records (the
       deal_info of FileBank::upload_declaration, c-pallets/file-bank/src/lib.rs:419-428) as
       JSON. --out writes every fragment as DIR/<fragment hash> while the file streams (host
       memory holds the pipeline's pinned batches, not the file). --scale writes the SCALE bytes
@@ -57,7 +60,7 @@ def _encode(args) -> int:
         else:
             rec, st = encode_file_records(args.file, args.k, args.m, args.segment_size,
                                           args.device, on_fragment=writer, max_segments=limit,
-                                          window=args.window)
+                                          hash_on=args.hash_on, window=args.window)
     except ErrTooManySegments:
         for p in tmp.values():
             os.unlink(p)
@@ -117,6 +120,7 @@ def main(argv=None) -> int:
     e.add_argument("--m", type=int, default=geometry.PARITY_SHARDS)
     e.add_argument("--segment-size", type=int, default=geometry.SEGMENT_SIZE)
     e.add_argument("--window", type=int, default=32)
+    e.add_argument("--hash-on", choices=("auto", "gpu", "host"), default="auto")
     e.add_argument("--device", type=int, default=0)
     e.add_argument("--devices", default="",
                    help="comma list of GPUs: the file's segments sharded over them from this "
@@ -142,7 +146,7 @@ def main(argv=None) -> int:
     from .pipeline import encode_file_records
     with open(args.records) as f:
         want = json.load(f)
-    got = encode_file_records(args.file)[0].to_json()
+    got = encode_file_records(args.file, hash_on="auto")[0].to_json()
     ok = got["segments"] == want["segments"] and got["file_hash"] == want["file_hash"]
     print(json.dumps({"ok": ok}))
     return 0 if ok else 1

@@ -179,21 +179,57 @@ class Pipeline:
         return stats
 
 
+def _source_size(src: Source) -> Optional[int]:
+    if isinstance(src, str):
+        return os.path.getsize(src)
+    if isinstance(src, (np.ndarray, memoryview)):
+        return src.nbytes
+    if isinstance(src, (bytes, bytearray)):
+        return len(src)
+    return None  # a stream
+
+
+# encode_file_records(hash_on="auto") hashes on the GPU from this size up. Measured fresh per
+# call, RS(2,1), 16 host threads (profiles/r05/records_crossover.jsonl): the GPU path pays
+# ~0.3 s pinning + ~0.3 s unpinning its 4.5 GiB ring and the last segment chain (0.5 s when the
+# chip is busy, 1.15 s for a lone one-segment file), so the host wins up to 16 GiB (1.26 s
+# against 1.43) and the GPU from 32 GiB (1.75 s against 2.28; 30 GB/s against 15.6 at 64 GiB).
+# CESS's SegmentCount = 1000 segments (15.6 GiB) keeps every declarable file on the host.
+AUTO_GPU_RECORD_BYTES = 20 << 30
+
+
 def encode_file_records(path_or_buf: Source, k: int = geometry.DATA_SHARDS,
                         m: int = geometry.PARITY_SHARDS,
                         segment_size: int = geometry.SEGMENT_SIZE, device: int = 0,
                         on_fragment: Optional[Callable[[int, int, np.ndarray], None]] = None,
-                        max_segments: int = 0, **kw):
-    """File -> FileRecord (SegmentLists + two-level file hash) through the C pipeline.
-    on_fragment(seg, idx, view) sees each fragment before its hash is known."""
+                        max_segments: int = 0, hash_on: str = "gpu", hash_threads: int = 16,
+                        **kw):
+    """File -> FileRecord (SegmentLists + two-level file hash), encoded on the GPU.
+    on_fragment(seg, idx, view) sees each fragment (before its hash is known on the GPU path).
+
+    hash_on "gpu": the C pipeline (pinned multi-buffered copies, SegmentList hashes through the
+    GPU hash queue); a file's records land one 16 MiB segment chain (~0.47 s) after its last
+    batch. "host": SegmentEncoder with SHA-256 (OpenSSL SHA-NI) on `hash_threads` host threads
+    beside the GPU encode. "auto": the host below AUTO_GPU_RECORD_BYTES for codes whose batch
+    holds < 2048 fragments, the GPU otherwise and for streams of unknown size. The records are
+    the same either way."""
     from .segments import FileRecord, SegmentList, file_hash
     if segment_size % k:
         raise ValueError("segment_size must be a multiple of k")
+    if hash_on not in ("gpu", "host", "auto"):
+        raise ValueError("hash_on must be 'gpu', 'host' or 'auto'")
+    size = _source_size(path_or_buf)
+    if hash_on == "auto":
+        hash_on = "host" if (size is not None and size < AUTO_GPU_RECORD_BYTES
+                             and 64 * (k + m) < 2048) else "gpu"
+    if hash_on == "host":
+        return _encode_file_records_host(path_or_buf, size, k, m, segment_size, device,
+                                         on_fragment, max_segments, hash_threads)
     recs = {}
-    if "batch_segments" not in kw:  # a small file does not need 1 GiB pinned batches
-        size = (os.path.getsize(path_or_buf) if isinstance(path_or_buf, str)
-                else len(path_or_buf) if isinstance(path_or_buf, (bytes, bytearray)) else None)
-        kw["batch_segments"] = 64 if size is None else max(1, min(64, -(-size // segment_size)))
+    if size is not None:  # a small file does not need 1 GiB pinned batches
+        # (the window stays: a chain finishes after `window` ticks of blocks/window each, so a
+        # narrower window only makes each tick coarser; measured 1.52 s against 1.11 at 8 GiB)
+        kw.setdefault("batch_segments", max(1, min(64, -(-size // segment_size))))
     enc = Encoder(k, m, device)
     try:
         with Pipeline(enc, segment_size // k, max_segments=max_segments, **kw) as p:
@@ -211,6 +247,33 @@ def encode_file_records(path_or_buf: Source, k: int = geometry.DATA_SHARDS,
     out = FileRecord(b"", int(st.bytes_in), [recs[s] for s in range(len(recs))])
     out.file_hash = file_hash(out.segments)
     return out, st
+
+
+def _encode_file_records_host(src, size, k, m, segment_size, device, on_fragment, max_segments,
+                              hash_threads):
+    """encode_file_records' host-hash path: SegmentEncoder (GPU encode, pinned double-buffered
+    batches sized to the file, SHA-256 on host threads). Returns (FileRecord, PipelineStats)."""
+    import time
+
+    from .segments import SegmentEncoder
+    if size is None:
+        raise ValueError("hash_on='host' needs a path or an in-memory source (known size)")
+    nseg = -(-size // segment_size)
+    if size == 0:
+        from .reedsolomon import ErrShortData
+        raise ErrShortData(ErrShortData.__doc__)
+    if max_segments and nseg > max_segments:
+        from .records import ErrTooManySegments
+        raise ErrTooManySegments(ErrTooManySegments.__doc__)
+    t0 = time.perf_counter()
+    se = SegmentEncoder(k, m, segment_size, batch_segments=min(64, nseg), device=device,
+                        hash_on="host", hash_threads=hash_threads)
+    try:
+        rec = se.encode_file(src, on_fragment=on_fragment)
+    finally:
+        se.close()
+    st = _lib.PipelineStats(len(rec.segments), rec.size, time.perf_counter() - t0, 0.0, 0.0)
+    return rec, st
 
 
 def encode_file_records_multi(src: Union[str, bytes, bytearray, memoryview, np.ndarray],
@@ -263,4 +326,5 @@ def encode_file_records_multi(src: Union[str, bytes, bytearray, memoryview, np.n
     return out, [st for _, st in parts if st is not None]
 
 
-__all__ = ["Pipeline", "encode_file_records", "encode_file_records_multi", "CecError"]
+__all__ = ["Pipeline", "encode_file_records", "encode_file_records_multi", "CecError",
+           "AUTO_GPU_RECORD_BYTES"]

@@ -41,21 +41,37 @@ def test_pipeline_from_c(e2e_exe, args):
     assert out["pipeline"] == "ok" and out["bad"] == 0 and out["checked"] == args[3]
 
 
-def test_pipeline_python_records(orc):
+@pytest.mark.parametrize("hash_on", ["gpu", "host", "auto"])
+def test_pipeline_python_records(orc, hash_on):
+    """encode_file_records on either hash placement (the C pipeline's GPU hash queue, or
+    SegmentEncoder's host SHA-256 beside the GPU encode): the oracle's SegmentLists, file hash
+    and fragments, from bytes, a numpy array and a memoryview."""
     from cess_amd.pipeline import encode_file_records
-    for size, seg, k, m in [(5 * MiB + 7, MiB, 2, 1), (3 * MiB, MiB // 2, 4, 2),
-                            (MiB - 3, MiB // 4, 32, 32)]:
+    as_array = lambda b: np.frombuffer(b, np.uint8)  # noqa: E731
+    for size, seg, k, m, wrap in [(5 * MiB + 7, MiB, 2, 1, bytes),
+                                  (3 * MiB, MiB // 2, 4, 2, as_array),
+                                  (MiB - 3, MiB // 4, 32, 32, memoryview)]:
         blob = np.random.default_rng(size).integers(0, 256, size, dtype=np.uint8).tobytes()
         frags = {}
         rec, st = encode_file_records(
-            blob, k, m, seg, batch_segments=2, window=2,
+            wrap(blob), k, m, seg, batch_segments=2, window=2, hash_on=hash_on,
             on_fragment=lambda s, i, v: frags.__setitem__((s, i), hashlib.sha256(v).hexdigest()))
         want = orc.segment_list(blob, k, m, seg)
         assert [(s.hash, s.fragment_list) for s in rec.segments] == want
         assert rec.file_hash == orc.file_hash(want) and rec.size == size
-        assert st.segments == len(want)
+        assert st.segments == len(want) and st.bytes_in == size
+        assert len(frags) == len(want) * (k + m)
         for (s, i), h in frags.items():
             assert h.encode() == want[s][1][i]
+
+
+def test_records_host_path_limits():
+    import cess_amd
+    from cess_amd.pipeline import encode_file_records
+    with pytest.raises(cess_amd.ErrTooManySegments):
+        encode_file_records(bytes(5 * 8192), 2, 1, 8192, max_segments=4, hash_on="host")
+    with pytest.raises(cess_amd.ErrShortData):
+        encode_file_records(b"", 2, 1, 8192, hash_on="host")
 
 
 def test_pipeline_segment_limit_and_callback_errors():
@@ -76,7 +92,8 @@ def test_pipeline_segment_limit_and_callback_errors():
         assert st.segments == 5
 
 
-def test_cli_encode_streams_fragments_and_scale(tmp_path, orc):
+@pytest.mark.parametrize("hash_on", ["auto", "gpu"])
+def test_cli_encode_streams_fragments_and_scale(tmp_path, orc, hash_on):
     import sys
     from cess_amd import records
     from cess_amd.segments import SegmentList
@@ -87,8 +104,8 @@ def test_cli_encode_streams_fragments_and_scale(tmp_path, orc):
     outdir = tmp_path / "frags"
     r = subprocess.run([sys.executable, "-m", "cess_amd.cli", "encode", str(src), "--out",
                         str(outdir), "--segment-size", str(1 << 20), "--scale",
-                        str(tmp_path / "deal.scale")], capture_output=True, text=True,
-                       timeout=300, check=True, cwd=ROOT)
+                        str(tmp_path / "deal.scale"), "--hash-on", hash_on],
+                       capture_output=True, text=True, timeout=300, check=True, cwd=ROOT)
     rec = json.loads(r.stdout)
     want = orc.segment_list(blob, 2, 1, 1 << 20)
     assert [(s["hash"].encode(), [f.encode() for f in s["fragment_list"]])
@@ -104,8 +121,8 @@ def test_cli_encode_streams_fragments_and_scale(tmp_path, orc):
     big = tmp_path / "big.bin"
     big.write_bytes(bytes(1001 * 16384))
     r = subprocess.run([sys.executable, "-m", "cess_amd.cli", "encode", str(big),
-                        "--segment-size", "16384"], capture_output=True, text=True, timeout=300,
-                       cwd=ROOT)
+                        "--segment-size", "16384", "--hash-on", hash_on], capture_output=True,
+                       text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 2 and "SegmentCount" in r.stdout
 
 

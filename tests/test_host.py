@@ -84,6 +84,21 @@ def test_python_api_errors_without_gpu():
         enc.Encode([np.ones(4, np.uint8), np.ones(5, np.uint8), np.ones(4, np.uint8)])
 
 
+def test_records_hash_placement_arguments():
+    """encode_file_records' hash_on is checked before any device work; the host path needs a
+    source of known size (a stream goes through the C pipeline)."""
+    import io
+    from cess_amd import pipeline
+    with pytest.raises(ValueError, match="hash_on"):
+        pipeline.encode_file_records(b"x", hash_on="cpu")
+    with pytest.raises(ValueError, match="known size|in-memory"):
+        pipeline.encode_file_records(io.BytesIO(b"x"), hash_on="host")
+    assert pipeline._source_size(np.zeros((3, 5), np.uint16)) == 30
+    assert pipeline._source_size(memoryview(bytes(7))) == 7
+    assert pipeline._source_size(io.BytesIO(b"x")) is None
+    assert pipeline.AUTO_GPU_RECORD_BYTES > 1000 * (16 << 20)  # SegmentCount files: host
+
+
 def test_join(tmp_path):
     import io
     import cess_amd
