@@ -146,6 +146,24 @@ def test_pipelines_on_threads(orc):
         assert all(ex.map(run, jobs))
 
 
+def test_library_first_then_torch():
+    """A fresh process that touches libcessec before torch (the C pipeline path needs no torch)
+    and then uses torch on the GPU: one HIP runtime in the process (cess_amd._lib.load)."""
+    import sys
+    code = ("import numpy as np\n"
+            "from cess_amd.pipeline import encode_file_records\n"
+            "rec, _ = encode_file_records(bytes(3 * 65536), 2, 1, 65536, batch_segments=2, "
+            "window=2)\n"
+            "import torch\n"
+            "x = torch.ones(4, device='cuda')\n"
+            "rec2, _ = encode_file_records(bytes(3 * 65536), 2, 1, 65536, hash_on='host')\n"
+            "assert rec2.file_hash == rec.file_hash\n"
+            "print('ok', int(x.sum().item()))\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
+                       cwd=ROOT)
+    assert r.returncode == 0 and "ok 4" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("devices,size,seg,k,m", [([0, 0, 0], 7 * MiB + 5, MiB, 2, 1),
                                                   ([0, 0], 3 * MiB, MiB // 2, 4, 2),
                                                   ([0, 0, 0, 0, 0], 2 * MiB, MiB, 2, 1)])
