@@ -22,7 +22,8 @@ its average launch time (HIP events on the launch stream); `cpu_baseline` times 
 The default line also carries, at every N: `extra.config4` (BASELINE config 4's 64 GiB file
 sharded over the N GPUs, T1 on one GPU, efficiency T1 / (N T_N), sampled segments checked against
 the C oracle) and `extra.host_e2e` (an in-memory file per GPU through the C pipeline,
-PCIe-inclusive, with and without SegmentList hashing); at N = 1 the one-GPU legs (reconstruct,
+PCIe-inclusive, with and without SegmentList hashing, the hashes on the GPU or on host
+threads); at N = 1 the one-GPU legs (reconstruct,
 `extra.wide_code`: RS(32,32) encode / restoral / rebuilds / verify, `extra.config5`: BASELINE
 config 5's encode + SHA-256 step); at N > 1 `extra.degraded_gather` and its wide-code and C-ABI
 forms: the RCCL survivor / partial-product exchange of BASELINE config 4 (fragment f of segment s
@@ -868,9 +869,12 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
     libcessec's C pipeline (cec_pipeline_*: pinned host ring, H2D / encode / D2H on three HIP
     streams, the north_star's pinned hipMemcpyAsync multi-buffering), once without hashing and
     once emitting every SegmentList record (segment + fragment SHA-256 on the GPU through the hash
-    queue, c-pallets/file-bank/src/types.rs:13-16). Segments are sharded per GPU with no
-    collective. Whole-node rate = all ranks' file bytes / the max over ranks of the run time
-    (barrier to barrier). Sampled records are checked afterwards with hashlib and the C oracle."""
+    queue, c-pallets/file-bank/src/types.rs:13-16), then once more with the same records hashed on
+    16 host SHA-NI threads beside the GPU encode (SegmentEncoder; the placement
+    encode_file_records picks below 20 GiB). Segments are sharded per GPU with no collective.
+    Whole-node rate = all ranks' file bytes / the max over ranks of the run time (barrier to
+    barrier). Sampled records are checked afterwards with hashlib and the C oracle, and the
+    host-hashed records against the GPU-hashed ones."""
     import hashlib
     import torch
     import torch.distributed as dist
@@ -926,6 +930,29 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
                      "node_GBps": round(world * nseg * seg_bytes / t / GB, 2),
                      "per_gpu_GBps": round(nseg * seg_bytes / t / GB, 2)}
     enc.close()
+    # the same records with the hashes on host SHA-NI threads beside the GPU encode (SegmentEncoder,
+    # what encode_file_records(hash_on="auto") picks below 20 GiB); records must equal the GPU's
+    from cess_amd.segments import SegmentEncoder
+    se = SegmentEncoder(k, m, seg_bytes, batch_segments=64, device=local, hash_on="host",
+                        hash_threads=16)
+    try:
+        se.encode_file(buf[:64 * seg_bytes])  # warm-up: pinned batches, thread pools
+        barrier()
+        t0 = time.perf_counter()
+        hrec = se.encode_file(buf)
+        t = time.perf_counter() - t0
+        barrier()
+    finally:
+        se.close()
+    t = reduce_max(t)
+    host_same = len(hrec.segments) == nseg and all(
+        (hrec.segments[s].hash, list(hrec.segments[s].fragment_list)) ==
+        (recs[s][0], list(recs[s][1])) for s in range(nseg) if s in recs)
+    out["segment_lists_host_sha"] = {
+        "seconds": round(t, 4), "segments": len(hrec.segments), "hash_threads": 16,
+        "node_GBps": round(world * nseg * seg_bytes / t / GB, 2),
+        "per_gpu_GBps": round(nseg * seg_bytes / t / GB, 2),
+        "records_equal_gpu_hashed": bool(not reduce_max(0.0 if host_same else 1.0))}
     # checker: sampled records against hashlib over the file bytes and the C oracle's parity
     from oracle.c_oracle import load_c_oracle
     orc = load_c_oracle()
@@ -994,6 +1021,9 @@ def line_problems(out: dict) -> list:
     e2e = ex.get("host_e2e")
     if e2e is not None and not e2e.get("records_match_hashlib_and_oracle"):
         bad.append("extra.host_e2e records unchecked or wrong")
+    if e2e is not None and "segment_lists_host_sha" in e2e and not e2e[
+            "segment_lists_host_sha"].get("records_equal_gpu_hashed"):
+        bad.append("extra.host_e2e host-hashed records differ from the GPU-hashed ones")
     if n == 1:
         c5 = ex.get("config5") or {}
         if not c5.get("digests_match_hashlib") or not c5.get("step_GBps"):

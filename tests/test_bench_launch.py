@@ -106,6 +106,21 @@ def test_line_keys_config4():
             _line(n, extra={"config4": no_t1}))
 
 
+def test_line_keys_host_e2e():
+    """The host-resident leg's records: the GPU-hashed ones checked against hashlib and the C
+    oracle, the host-hashed ones equal to the GPU-hashed ones."""
+    ok = {"records_match_hashlib_and_oracle": True,
+          "segment_lists_host_sha": {"records_equal_gpu_hashed": True}}
+    assert not any("host_e2e" in p for p in bench.line_problems(
+        _line(1, extra={"config4": C4, "host_e2e": ok})))
+    differ = dict(ok, segment_lists_host_sha={"records_equal_gpu_hashed": False})
+    assert "extra.host_e2e host-hashed records differ from the GPU-hashed ones" in \
+        bench.line_problems(_line(1, extra={"config4": C4, "host_e2e": differ}))
+    unchecked = dict(ok, records_match_hashlib_and_oracle=False)
+    assert "extra.host_e2e records unchecked or wrong" in bench.line_problems(
+        _line(1, extra={"config4": C4, "host_e2e": unchecked}))
+
+
 def test_line_keys_multi_gpu():
     """The N > 1 default line must carry cpu_baseline at the node's CPU share and both
     degraded-read transports (torch group, libcessec's own RCCL communicator) bit-exact."""
@@ -147,6 +162,7 @@ def test_line_keys_one_gpu():
 
 @pytest.mark.parametrize("name", ["bench_default_b.json", "bench_default_c.json",
                                   "bench_default_e.json", "bench_default_g.json",
+                                  "bench_default_h.json", "bench_gpus2_gloo_one_gpu_c.json",
                                   "bench_gpus2_gloo_one_gpu_b.json",
                                   "bench_gpus4_gloo_one_gpu_b.json"])
 def test_recorded_lines_have_every_key(name):
