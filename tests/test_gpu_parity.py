@@ -516,6 +516,36 @@ def test_max_shards_256(cess, corc):
         cess.New(200, 57)
 
 
+@pytest.mark.parametrize("k,m", [(1, 255), (255, 1), (128, 128), (3, 253), (253, 3)])
+def test_extreme_codes_batched(torch, cess, corc, k, m):
+    """Codes at the GF(2^8) limit k + m = 256 with one data shard, one parity shard or an even
+    split: batched encode equal to the C oracle, and a rebuild of m random erasures (every one
+    of the erasable count) per segment restoring the oracle's codeword."""
+    ln, nseg = 1000 + 3, 2
+    rng = np.random.default_rng(k * 1000 + m)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    want = np.stack([np.stack(c_encode(corc, k, m, [data[s, i] for i in range(k)]))
+                     for s in range(nseg)])
+    enc = cess.New(k, m)
+    d_data = to_dev(torch, data)
+    d_par = torch.zeros((nseg, m, ln), dtype=torch.uint8, device="cuda")
+    enc.EncodeBatch(d_data, d_par, nseg, ln)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_par.cpu().numpy(), want)
+    present = np.ones((nseg, k + m), np.uint8)
+    for s in range(nseg):
+        present[s, rng.choice(k + m, size=m, replace=False)] = 0
+    dd, dp = d_data.clone(), d_par.clone()
+    for s in range(nseg):
+        for f in np.flatnonzero(present[s] == 0):
+            (dd[s, f] if f < k else dp[s, f - k]).fill_(0xA5)
+    enc.ReconstructBatch(dd, dp, nseg, ln, present)
+    torch.cuda.synchronize()
+    assert np.array_equal(dd.cpu().numpy(), data)
+    assert np.array_equal(dp.cpu().numpy(), want)
+    enc.close()
+
+
 def test_more_segments_than_grid_y(torch, cess, corc):
     """nseg > 65535 splits the launch over grid.y chunks (encode, verify, per-segment decode)."""
     k, m, ln, nseg = 2, 1, 32, 70000
