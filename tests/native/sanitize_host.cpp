@@ -2,10 +2,12 @@
 // build of the CPU codec; GPU sanitizers are not available on this pool). Built and run by
 // tests/test_host.py::test_host_code_under_sanitizers with g++ -fsanitize=address,undefined:
 //   * libcessec's host-only code: SCALE records (records.cpp), the degraded-read plan of every
-//     exchange (dist.cpp, no GPU call on that path), the GF(2^8) matrix builder and decode plans
+//     exchange and its RCCL group cuts at several bounds, plans of up to three rounds (dist.cpp,
+//     no GPU call on that path), the GF(2^8) matrix builder and decode plans
 //     (gf256.h) for every erasure pattern of small codes;
 //   * the CPU codec (oracle/rs_oracle.c, the CPU baseline) in its scalar, AVX2 and GFNI forms,
 //     encode + reconstruct round trips with ragged lengths.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -112,6 +114,44 @@ static void records(std::mt19937& g) {
   CHECK(cec_shard_id(reinterpret_cast<const uint8_t*>(h.data()), 1000, id) != CEC_OK);
 }
 
+// the RCCL group cuts of a plan (dist.cpp group_cuts via cec_dist_plan_groups): count-only and
+// filled calls agree, starts ascend from 0, every round of 256 segments starts a group, a smaller
+// bound never gives fewer groups, an undersized starts buffer is refused
+static void group_cuts(int k, int m, int world, int ex, const std::vector<uint64_t>& seg,
+                       const std::vector<uint8_t>& frag) {
+  size_t nsegs = 0;
+  {
+    std::vector<uint64_t> u(seg);
+    std::sort(u.begin(), u.end());
+    nsegs = (size_t)(std::unique(u.begin(), u.end()) - u.begin());
+  }
+  size_t prev = 0;
+  for (int bound : {4096, 1024, 64, 7, 1, 0}) {
+    size_t ng = 0;
+    CHECK(cec_dist_plan_groups(k, m, world, ex, bound, seg.data(), frag.data(), seg.size(),
+                               nullptr, 0, &ng) == CEC_OK);
+    std::vector<uint64_t> st(ng + 1, ~0ull);
+    size_t ng2 = 0;
+    CHECK(cec_dist_plan_groups(k, m, world, ex, bound, seg.data(), frag.data(), seg.size(),
+                               st.data(), ng, &ng2) == CEC_OK && ng2 == ng);
+    CHECK(st[ng] == ~0ull);  // nothing past starts_cap
+    if (ng > 1)
+      CHECK(cec_dist_plan_groups(k, m, world, ex, bound, seg.data(), frag.data(), seg.size(),
+                                 st.data(), ng - 1, &ng2) == CEC_EINVAL);
+    if (nsegs == 0) continue;
+    CHECK(ng >= (nsegs + 255) / 256 && st[0] == 0);
+    for (size_t i = 1; i < ng; ++i) CHECK(st[i] > st[i - 1] && st[i] < nsegs);
+    for (size_t r = 256; r < nsegs; r += 256)
+      CHECK(std::find(st.begin(), st.begin() + ng, (uint64_t)r) != st.begin() + ng);
+    if (bound > 0) {
+      CHECK(ng >= prev);
+      prev = ng;
+    } else {
+      CHECK(ng == (nsegs + 255) / 256);
+    }
+  }
+}
+
 static void plans(std::mt19937& g) {
   const int codes[][2] = {{2, 1}, {4, 2}, {10, 4}, {32, 32}, {200, 56}};
   for (auto& km : codes) {
@@ -157,7 +197,24 @@ static void plans(std::mt19937& g) {
         for (size_t i = 0; i < nm; ++i)
           CHECK(mv[i].src >= 0 && mv[i].src < world && mv[i].dst >= 0 && mv[i].dst < world &&
                 mv[i].frag >= 0 && mv[i].frag < k + m && (mv[i].kind == 0 || mv[i].kind == 1));
+        group_cuts(k, m, world, ex, s2, f2);
       }
+    if (k + m <= 64) {  // plans of several rounds (700 segments), ragged erasure counts
+      for (int world : {2, 3, 8})
+        for (int ex = 0; ex <= 2; ++ex) {
+          std::vector<uint64_t> seg;
+          std::vector<uint8_t> frag;
+          for (uint64_t s = 0; s < 700; ++s) {
+            const int e = 1 + (int)(g() % m);
+            const int f0 = (int)(g() % (k + m));
+            for (int q = 0; q < e; ++q) {
+              seg.push_back(s * 3 + 1);
+              frag.push_back((uint8_t)((f0 + q) % (k + m)));
+            }
+          }
+          group_cuts(k, m, world, ex, seg, frag);
+        }
+    }
     if (k + m < 256) {  // an index past the code (uint8 holds every index of a 256-shard code)
       uint64_t s0 = 3;
       uint8_t bad = (uint8_t)(k + m);
