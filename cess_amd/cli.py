@@ -28,6 +28,12 @@ import sys
 from . import geometry
 
 
+def _placement(args, size: int) -> str:
+    """Where the record hashes ran: "gpu" (hash queue) or "host" (SHA-NI threads)."""
+    from .pipeline import record_hash_placement
+    return "gpu" if args.devices else record_hash_placement(args.hash_on, size, args.k, args.m)
+
+
 def _encode(args) -> int:
     from .pipeline import encode_file_records
     from .records import ErrTooManySegments
@@ -74,7 +80,8 @@ def _encode(args) -> int:
     out["check_file_spec"] = check_file_spec(rec.segments, args.k + args.m)
     out["needed_space"] = needed_space(rec.segments, args.segment_size)
     out["pipeline"] = {"seconds": round(st.seconds, 4), "read_seconds": round(st.read_seconds, 4),
-                       "GBps": round(st.bytes_in / max(st.seconds, 1e-9) / 1e9, 3)}
+                       "GBps": round(st.bytes_in / max(st.seconds, 1e-9) / 1e9, 3),
+                       "hash_on": _placement(args, rec.size)}
     if args.scale:
         with open(args.scale, "wb") as f:
             f.write(rec.deal_info_scale())

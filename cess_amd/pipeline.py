@@ -198,6 +198,15 @@ def _source_size(src: Source) -> Optional[int]:
 AUTO_GPU_RECORD_BYTES = 20 << 30
 
 
+def record_hash_placement(hash_on: str, size: Optional[int], k: int, m: int) -> str:
+    """"gpu" or "host" for encode_file_records' hash_on ("auto" resolved by source size and
+    code width: a batch of >= 2048 fragments keeps the GPU's hash lanes busy)."""
+    if hash_on != "auto":
+        return hash_on
+    return "host" if (size is not None and size < AUTO_GPU_RECORD_BYTES
+                      and 64 * (k + m) < 2048) else "gpu"
+
+
 def encode_file_records(path_or_buf: Source, k: int = geometry.DATA_SHARDS,
                         m: int = geometry.PARITY_SHARDS,
                         segment_size: int = geometry.SEGMENT_SIZE, device: int = 0,
@@ -219,9 +228,7 @@ def encode_file_records(path_or_buf: Source, k: int = geometry.DATA_SHARDS,
     if hash_on not in ("gpu", "host", "auto"):
         raise ValueError("hash_on must be 'gpu', 'host' or 'auto'")
     size = _source_size(path_or_buf)
-    if hash_on == "auto":
-        hash_on = "host" if (size is not None and size < AUTO_GPU_RECORD_BYTES
-                             and 64 * (k + m) < 2048) else "gpu"
+    hash_on = record_hash_placement(hash_on, size, k, m)
     if hash_on == "host":
         return _encode_file_records_host(path_or_buf, size, k, m, segment_size, device,
                                          on_fragment, max_segments, hash_threads)
@@ -327,4 +334,4 @@ def encode_file_records_multi(src: Union[str, bytes, bytearray, memoryview, np.n
 
 
 __all__ = ["Pipeline", "encode_file_records", "encode_file_records_multi", "CecError",
-           "AUTO_GPU_RECORD_BYTES"]
+           "AUTO_GPU_RECORD_BYTES", "record_hash_placement"]

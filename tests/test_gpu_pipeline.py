@@ -107,6 +107,7 @@ def test_cli_encode_streams_fragments_and_scale(tmp_path, orc, hash_on):
                         str(tmp_path / "deal.scale"), "--hash-on", hash_on],
                        capture_output=True, text=True, timeout=300, check=True, cwd=ROOT)
     rec = json.loads(r.stdout)
+    assert rec["pipeline"]["hash_on"] == ("host" if hash_on == "auto" else "gpu")
     want = orc.segment_list(blob, 2, 1, 1 << 20)
     assert [(s["hash"].encode(), [f.encode() for f in s["fragment_list"]])
             for s in rec["segments"]] == want

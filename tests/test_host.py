@@ -97,6 +97,11 @@ def test_records_hash_placement_arguments():
     assert pipeline._source_size(memoryview(bytes(7))) == 7
     assert pipeline._source_size(io.BytesIO(b"x")) is None
     assert pipeline.AUTO_GPU_RECORD_BYTES > 1000 * (16 << 20)  # SegmentCount files: host
+    place = pipeline.record_hash_placement
+    assert place("auto", 1 << 30, 2, 1) == "host" and place("auto", 64 << 30, 2, 1) == "gpu"
+    assert place("auto", None, 2, 1) == "gpu"  # a stream of unknown size
+    assert place("auto", 1 << 20, 32, 32) == "gpu"  # 4096 fragments per batch
+    assert place("host", 64 << 30, 2, 1) == "host" and place("gpu", 1, 2, 1) == "gpu"
 
 
 def test_join(tmp_path):
