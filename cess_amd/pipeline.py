@@ -231,7 +231,8 @@ def encode_file_records(path_or_buf: Source, k: int = geometry.DATA_SHARDS,
     hash_on = record_hash_placement(hash_on, size, k, m)
     if hash_on == "host":
         return _encode_file_records_host(path_or_buf, size, k, m, segment_size, device,
-                                         on_fragment, max_segments, hash_threads)
+                                         on_fragment, max_segments, hash_threads,
+                                         kw.get("batch_segments"))
     recs = {}
     if size is not None:  # a small file does not need 1 GiB pinned batches
         # (the window stays: a chain finishes after `window` ticks of blocks/window each, so a
@@ -257,9 +258,10 @@ def encode_file_records(path_or_buf: Source, k: int = geometry.DATA_SHARDS,
 
 
 def _encode_file_records_host(src, size, k, m, segment_size, device, on_fragment, max_segments,
-                              hash_threads):
+                              hash_threads, batch_segments=None):
     """encode_file_records' host-hash path: SegmentEncoder (GPU encode, pinned double-buffered
-    batches sized to the file, SHA-256 on host threads). Returns (FileRecord, PipelineStats)."""
+    batches sized to the file unless batch_segments is given, SHA-256 on host threads; the C
+    pipeline's other options do not apply). Returns (FileRecord, PipelineStats)."""
     import time
 
     from .segments import SegmentEncoder
@@ -273,8 +275,8 @@ def _encode_file_records_host(src, size, k, m, segment_size, device, on_fragment
         from .records import ErrTooManySegments
         raise ErrTooManySegments(ErrTooManySegments.__doc__)
     t0 = time.perf_counter()
-    se = SegmentEncoder(k, m, segment_size, batch_segments=min(64, nseg), device=device,
-                        hash_on="host", hash_threads=hash_threads)
+    se = SegmentEncoder(k, m, segment_size, batch_segments=batch_segments or min(64, nseg),
+                        device=device, hash_on="host", hash_threads=hash_threads)
     try:
         rec = se.encode_file(src, on_fragment=on_fragment)
     finally:
