@@ -83,14 +83,14 @@ class Retriever:
         self.B = max(1, batch_segments)
         self.pool = cf.ThreadPoolExecutor(max_workers=max(1, threads))
         self.enc = None
-        self.d_data = self.d_par = None
+        self.d_data = self.d_par = self.h_data = self.h_par = None
 
     def close(self) -> None:
         self.pool.shutdown(wait=True)
         if self.enc is not None:
             self.enc.close()
             self.enc = None
-        self.d_data = self.d_par = None
+        self.d_data = self.d_par = self.h_data = self.h_par = None
 
     def __enter__(self):
         return self
@@ -125,33 +125,44 @@ class Retriever:
         return good, fetched, rejected
 
     def _rebuild(self, todo, stats: dict) -> None:
-        """Rebuild the lost data fragments of [(s, good)] in place (one launch)."""
+        """Rebuild the lost data fragments of [(s, good)] (one launch). The valid fragments go
+        through a pinned staging batch (copied in on the pool's threads); only the rebuilt
+        fragments come back, into the same staging rows, which `good` then refers to (valid until
+        the next batch's rebuild)."""
         import torch
         import cess_amd
+        k, m, F = self.k, self.m, self.F
         if self.enc is None:
-            self.enc = cess_amd.New(self.k, self.m, device=self.device)
+            self.enc = cess_amd.New(k, m, device=self.device)
             dev = torch.device("cuda", self.device)
-            self.d_data = torch.empty((self.B, self.k, self.F), dtype=torch.uint8, device=dev)
-            self.d_par = torch.empty((self.B, self.m, self.F), dtype=torch.uint8, device=dev)
+            self.d_data = torch.empty((self.B, k, F), dtype=torch.uint8, device=dev)
+            self.d_par = torch.empty((self.B, m, F), dtype=torch.uint8, device=dev)
+            self.h_data = torch.empty((self.B, k, F), dtype=torch.uint8, pin_memory=True)
+            self.h_par = torch.empty((self.B, m, F), dtype=torch.uint8, pin_memory=True)
         nb = len(todo)
-        h_data = np.zeros((nb, self.k, self.F), np.uint8)
-        h_par = np.zeros((nb, self.m, self.F), np.uint8)
+        hd, hp = self.h_data.numpy(), self.h_par.numpy()
         present = np.zeros((nb, self.n), np.uint8)
+        copies = []
         for i, (_s, good) in enumerate(todo):
             for f, a in good.items():
-                (h_data[i, f] if f < self.k else h_par[i, f - self.k])[:] = a
                 present[i, f] = 1
-        self.d_data[:nb].copy_(torch.from_numpy(h_data))
-        self.d_par[:nb].copy_(torch.from_numpy(h_par))
-        self.enc.ReconstructBatch(self.d_data[:nb], self.d_par[:nb], nb, self.F, present,
-                                  data_only=True)
-        out = self.d_data[:nb].cpu().numpy()
-        for i, (_s, good) in enumerate(todo):
-            for f in range(self.k):
-                if f not in good:
-                    good[f] = out[i, f]
+                copies.append((hd[i, f] if f < k else hp[i, f - k], a))
+        list(self.pool.map(lambda c: np.copyto(c[0], c[1]), copies))
+        # whole rows over PCIe (the rows of lost fragments carry stale bytes the codec never
+        # reads: it reads exactly its survivors)
+        self.d_data[:nb].copy_(self.h_data[:nb], non_blocking=True)
+        self.d_par[:nb].copy_(self.h_par[:nb], non_blocking=True)
+        st = torch.cuda.current_stream(self.d_data.device)  # the copies' stream
+        self.enc.ReconstructBatch(self.d_data[:nb], self.d_par[:nb], nb, F, present,
+                                  data_only=True, stream=st)
+        lost = [(i, f) for i in range(nb) for f in range(k) if not present[i, f]]
+        for i, f in lost:
+            self.h_data[i, f].copy_(self.d_data[i, f], non_blocking=True)
+        st.synchronize()
+        for i, f in lost:
+            todo[i][1][f] = hd[i, f]
         stats["rebuilt_segments"] += nb
-        stats["rebuilt_fragments"] += int(self.k * nb - present[:, :self.k].sum())
+        stats["rebuilt_fragments"] += len(lost)
 
     def retrieve(self, rec: FileRecord, fetch: FetchFn, out: Union[str, BinaryIO],
                  check_segments: bool = True) -> dict:
@@ -188,17 +199,22 @@ class Retriever:
                 if todo:
                     self._rebuild(todo, stats)
 
-                def check(i):
-                    segm = np.concatenate([goods[i][f] for f in range(self.k)])
-                    if (check_segments and hashlib.sha256(segm).hexdigest().encode()
-                            != rec.segments[idx[i]].hash):
-                        raise ErrSegmentHashMismatch(f"segment {idx[i]} does not match its "
-                                                     f"recorded hash")
-                    return segm
-                for segm in self.pool.map(check, range(len(idx))):
-                    take = min(self.seg, rec.size - written)
-                    fo.write(memoryview(segm[:take]))
-                    written += take
+                def check(i):  # the segment's hash over its k data fragments, no joined copy
+                    if check_segments:
+                        h = hashlib.sha256()
+                        for f in range(self.k):
+                            h.update(goods[i][f])
+                        if h.hexdigest().encode() != rec.segments[idx[i]].hash:
+                            raise ErrSegmentHashMismatch(f"segment {idx[i]} does not match "
+                                                         f"its recorded hash")
+                    return goods[i]
+                for g in self.pool.map(check, range(len(idx))):
+                    for f in range(self.k):  # the data fragments in order, the padding dropped
+                        take = min(self.F, rec.size - written)
+                        if take <= 0:
+                            break
+                        fo.write(memoryview(g[f][:take]))
+                        written += take
             ok = True
         finally:
             if own:
