@@ -99,30 +99,48 @@ class Retriever:
         self.close()
 
     def _gather(self, s: int, sl: SegmentList, fetch: FetchFn):
-        """The fragments of segment s that check out: ({index: uint8 array}, fetched, rejected),
-        data first, parity only while fewer than k are valid (runs on a pool thread)."""
+        """The fragments of segment s that check out: ({index: uint8 array}, fetched, rejected,
+        the segment's hex digest when all k data fragments checked out, else None), data first,
+        parity only while fewer than k are valid (runs on a pool thread)."""
         if len(sl.fragment_list) != self.n:
             raise ValueError(f"segment {s}: {len(sl.fragment_list)} fragment hashes, "
                              f"expected k + m = {self.n} (check_file_spec)")
         good: Dict[int, np.ndarray] = {}
         fetched = rejected = 0
+        # the segment's hash streams over the valid data fragments in order: fragment 0's digest
+        # is that stream's prefix digest (one pass serves both, as on upload), and when every
+        # data fragment checks out the segment digest needs no second pass
+        seg_h = hashlib.sha256()
+        seg_ok = True
         for f in range(self.n):
             if f >= self.k and len(good) >= self.k:
                 break
             raw = fetch(s, f, sl.fragment_list[f])
             if raw is None:
+                seg_ok &= f >= self.k
                 continue
             fetched += 1
             a = np.frombuffer(raw, np.uint8) if not isinstance(raw, np.ndarray) else \
                 raw.reshape(-1).view(np.uint8)
-            if a.size != self.F or hashlib.sha256(a).hexdigest().encode() != sl.fragment_list[f]:
+            if a.size != self.F:
+                valid = False
+            elif f == 0:
+                seg_h.update(a)
+                valid = seg_h.copy().hexdigest().encode() == sl.fragment_list[0]
+            else:
+                valid = hashlib.sha256(a).hexdigest().encode() == sl.fragment_list[f]
+                if valid and f < self.k and seg_ok:
+                    seg_h.update(a)
+            if not valid:
                 rejected += 1  # wrong bytes: an erasure like a missing fragment
+                seg_ok &= f >= self.k
                 continue
             good[f] = a
         if len(good) < self.k:
             raise ErrTooFewShards(f"segment {s}: {len(good)} of {self.n} fragments valid, "
                                   f"need {self.k}")
-        return good, fetched, rejected
+        seg_hex = seg_h.hexdigest().encode() if seg_ok else None
+        return good, fetched, rejected, seg_hex
 
     def _rebuild(self, todo, stats: dict) -> None:
         """Rebuild the lost data fragments of [(s, good)] (one launch). The valid fragments go
@@ -191,9 +209,10 @@ class Retriever:
             for b0 in range(0, nseg, self.B):
                 idx = list(range(b0, min(nseg, b0 + self.B)))
                 got = list(self.pool.map(lambda s: self._gather(s, rec.segments[s], fetch), idx))
-                goods = [g for g, _, _ in got]
-                stats["fetched"] += sum(n for _, n, _ in got)
-                stats["rejected"] += sum(r for _, _, r in got)
+                goods = [g for g, _, _, _ in got]
+                seg_hex = [h for _, _, _, h in got]  # None: a data fragment is rebuilt
+                stats["fetched"] += sum(n for _, n, _, _ in got)
+                stats["rejected"] += sum(r for _, _, r, _ in got)
                 todo = [(s, g) for s, g in zip(idx, goods) if any(f not in g
                                                                    for f in range(self.k))]
                 if todo:
@@ -201,10 +220,13 @@ class Retriever:
 
                 def check(i):  # the segment's hash over its k data fragments, no joined copy
                     if check_segments:
-                        h = hashlib.sha256()
-                        for f in range(self.k):
-                            h.update(goods[i][f])
-                        if h.hexdigest().encode() != rec.segments[idx[i]].hash:
+                        got_hex = seg_hex[i]
+                        if got_hex is None:
+                            h = hashlib.sha256()
+                            for f in range(self.k):
+                                h.update(goods[i][f])
+                            got_hex = h.hexdigest().encode()
+                        if got_hex != rec.segments[idx[i]].hash:
                             raise ErrSegmentHashMismatch(f"segment {idx[i]} does not match "
                                                          f"its recorded hash")
                     return goods[i]

@@ -6,7 +6,7 @@ retrieved: fetch, fragment hashes checked on host threads, lost data fragments r
 GPU (one ReconstructBatch launch per batch), segment hashes checked, joined. Output written to a
 sink that compares every byte with the source. One JSON line.
 
-usage: python tools/retrieve_bench.py [--gib 4] [--threads 16]"""
+usage: python tools/retrieve_bench.py [--gib 4] [--threads 16] [--intact]"""
 import argparse
 import json
 import os
@@ -44,6 +44,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=int, default=4)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--intact", action="store_true", help="lose no fragment")
+    ap.add_argument("--separate-segment-pass", action="store_true",
+                    help="A/B: drop the streamed segment digest, hash every segment again")
     args = ap.parse_args()
     seg = 16 * MiB
     nseg = args.gib * 1024 // 16
@@ -63,11 +66,14 @@ def main():
         src, hash_on="host",
         on_fragment=lambda s, i, v: store.__setitem__((s, i), np.array(v, copy=True)))
     t_enc = time.perf_counter() - t0
-    lost = {(s, s % 3) for s in range(nseg)}
+    lost = set() if args.intact else {(s, s % 3) for s in range(nseg)}
 
     def fetch(s, f, _h):
         return None if (s, f) in lost else store[(s, f)]
 
+    if args.separate_segment_pass:
+        gather = Retriever._gather
+        Retriever._gather = lambda self, *a: gather(self, *a)[:3] + (None,)
     with Retriever(threads=args.threads) as r:
         r.retrieve(rec, fetch, CompareSink(src))  # warm-up (codec, device batch)
         sink = CompareSink(src)
@@ -78,7 +84,8 @@ def main():
                       "rebuilt_segments": st["rebuilt_segments"],
                       "rebuilt_fragments": st["rebuilt_fragments"], "seconds": round(t, 4),
                       "GBps": round(size / t / 1e9, 2), "threads": args.threads,
-                      "output_equal_source": sink.same and sink.n == size,
+                      "output_equal_source": sink.same and sink.n == size, "intact": args.intact,
+                      "separate_segment_pass": args.separate_segment_pass,
                       "encode_records_seconds": round(t_enc, 4)}), flush=True)
 
 
