@@ -164,12 +164,19 @@ class Retriever:
         for i, (_s, good) in enumerate(todo):
             for f, a in good.items():
                 present[i, f] = 1
-                copies.append((hd[i, f] if f < k else hp[i, f - k], a))
-        list(self.pool.map(lambda c: np.copyto(c[0], c[1]), copies))
-        # whole rows over PCIe (the rows of lost fragments carry stale bytes the codec never
-        # reads: it reads exactly its survivors)
-        self.d_data[:nb].copy_(self.h_data[:nb], non_blocking=True)
-        self.d_par[:nb].copy_(self.h_par[:nb], non_blocking=True)
+                copies.append((i, f, a))
+
+        def stage(c):
+            i, f, a = c
+            np.copyto(hd[i, f] if f < k else hp[i, f - k], a)
+        list(self.pool.map(stage, copies))
+        # only the valid fragments cross PCIe: the gather stops at k of them, so they are exactly
+        # the survivors the rebuild reads (the slots of lost fragments are never read)
+        for i, f, _a in copies:
+            if f < k:
+                self.d_data[i, f].copy_(self.h_data[i, f], non_blocking=True)
+            else:
+                self.d_par[i, f - k].copy_(self.h_par[i, f - k], non_blocking=True)
         st = torch.cuda.current_stream(self.d_data.device)  # the copies' stream
         self.enc.ReconstructBatch(self.d_data[:nb], self.d_par[:nb], nb, F, present,
                                   data_only=True, stream=st)
