@@ -211,11 +211,19 @@ class Retriever:
         tmp = out + ".part" if own else None
         fo = open(tmp, "wb") if own else out
         ok = False
+
+        def gather(b0):  # the batch's fetch + fragment checks, queued on the pool
+            return [self.pool.submit(self._gather, s, rec.segments[s], fetch)
+                    for s in range(b0, min(nseg, b0 + self.B))]
+        pending = gather(0) if nseg else []
         try:
             written = 0
             for b0 in range(0, nseg, self.B):
                 idx = list(range(b0, min(nseg, b0 + self.B)))
-                got = list(self.pool.map(lambda s: self._gather(s, rec.segments[s], fetch), idx))
+                got = [f.result() for f in pending]
+                # the next batch's fetches and checks run on the pool while this one is rebuilt
+                # on the GPU (the pool is otherwise idle then) and checked
+                pending = gather(b0 + self.B) if b0 + self.B < nseg else []
                 goods = [g for g, _, _, _ in got]
                 seg_hex = [h for _, _, _, h in got]  # None: a data fragment is rebuilt
                 stats["fetched"] += sum(n for _, n, _, _ in got)
@@ -246,6 +254,8 @@ class Retriever:
                         written += take
             ok = True
         finally:
+            for f in pending:  # after a failure: drop the next batch's queued work
+                f.cancel()
             if own:
                 fo.close()
                 if ok:
