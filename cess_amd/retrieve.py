@@ -100,24 +100,24 @@ class Retriever:
 
     def _gather(self, s: int, sl: SegmentList, fetch: FetchFn):
         """The fragments of segment s that check out: ({index: uint8 array}, fetched, rejected,
-        the segment's hex digest when all k data fragments checked out, else None), data first,
+        (segment hasher, p): the hasher has streamed the first p data fragments), data first,
         parity only while fewer than k are valid (runs on a pool thread)."""
         if len(sl.fragment_list) != self.n:
             raise ValueError(f"segment {s}: {len(sl.fragment_list)} fragment hashes, "
                              f"expected k + m = {self.n} (check_file_spec)")
         good: Dict[int, np.ndarray] = {}
         fetched = rejected = 0
-        # the segment's hash streams over the valid data fragments in order: fragment 0's digest
-        # is that stream's prefix digest (one pass serves both, as on upload), and when every
-        # data fragment checks out the segment digest needs no second pass
+        # the segment's hash streams over the leading valid data fragments in order: fragment 0's
+        # digest is that stream's prefix digest (one pass serves both, as on upload); the segment
+        # check later streams only the data fragments after the valid prefix (all rebuilt or
+        # after a gap), so a segment whose data fragments all check out is hashed once
         seg_h = hashlib.sha256()
-        seg_ok = True
+        prefix = 0
         for f in range(self.n):
             if f >= self.k and len(good) >= self.k:
                 break
             raw = fetch(s, f, sl.fragment_list[f])
             if raw is None:
-                seg_ok &= f >= self.k
                 continue
             fetched += 1
             a = np.frombuffer(raw, np.uint8) if not isinstance(raw, np.ndarray) else \
@@ -127,20 +127,23 @@ class Retriever:
             elif f == 0:
                 seg_h.update(a)
                 valid = seg_h.copy().hexdigest().encode() == sl.fragment_list[0]
+                if valid:
+                    prefix = 1
+                else:
+                    seg_h = hashlib.sha256()  # the wrong bytes leave the stream
             else:
                 valid = hashlib.sha256(a).hexdigest().encode() == sl.fragment_list[f]
-                if valid and f < self.k and seg_ok:
+                if valid and f == prefix and f < self.k:
                     seg_h.update(a)
+                    prefix += 1
             if not valid:
                 rejected += 1  # wrong bytes: an erasure like a missing fragment
-                seg_ok &= f >= self.k
                 continue
             good[f] = a
         if len(good) < self.k:
             raise ErrTooFewShards(f"segment {s}: {len(good)} of {self.n} fragments valid, "
                                   f"need {self.k}")
-        seg_hex = seg_h.hexdigest().encode() if seg_ok else None
-        return good, fetched, rejected, seg_hex
+        return good, fetched, rejected, (seg_h, prefix)
 
     def _rebuild(self, todo, stats: dict) -> None:
         """Rebuild the lost data fragments of [(s, good)] (one launch). The valid fragments go
@@ -225,7 +228,7 @@ class Retriever:
                 # on the GPU (the pool is otherwise idle then) and checked
                 pending = gather(b0 + self.B) if b0 + self.B < nseg else []
                 goods = [g for g, _, _, _ in got]
-                seg_hex = [h for _, _, _, h in got]  # None: a data fragment is rebuilt
+                streams = [h for _, _, _, h in got]  # (hasher, data fragments streamed)
                 stats["fetched"] += sum(n for _, n, _, _ in got)
                 stats["rejected"] += sum(r for _, _, r, _ in got)
                 todo = [(s, g) for s, g in zip(idx, goods) if any(f not in g
@@ -235,13 +238,10 @@ class Retriever:
 
                 def check(i):  # the segment's hash over its k data fragments, no joined copy
                     if check_segments:
-                        got_hex = seg_hex[i]
-                        if got_hex is None:
-                            h = hashlib.sha256()
-                            for f in range(self.k):
-                                h.update(goods[i][f])
-                            got_hex = h.hexdigest().encode()
-                        if got_hex != rec.segments[idx[i]].hash:
+                        h, p = streams[i]
+                        for f in range(p, self.k):  # the rebuilt ones and any after them
+                            h.update(goods[i][f])
+                        if h.hexdigest().encode() != rec.segments[idx[i]].hash:
                             raise ErrSegmentHashMismatch(f"segment {idx[i]} does not match "
                                                          f"its recorded hash")
                     return goods[i]

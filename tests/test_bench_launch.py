@@ -163,7 +163,7 @@ def test_line_keys_one_gpu():
 @pytest.mark.parametrize("name", ["bench_default_b.json", "bench_default_c.json",
                                   "bench_default_e.json", "bench_default_g.json",
                                   "bench_default_h.json", "bench_default_i.json", "bench_default_j.json",
-                                  "bench_default_k.json",
+                                  "bench_default_k.json", "bench_default_l.json",
                                   "bench_gpus2_gloo_one_gpu_c.json", "bench_gpus4_gloo_one_gpu_c.json",
                                   "bench_gpus2_gloo_one_gpu_b.json",
                                   "bench_gpus4_gloo_one_gpu_b.json"])
