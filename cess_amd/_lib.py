@@ -17,13 +17,21 @@ TUNE_LIB_PATH = os.path.join(_HERE, "libcessec_tune.so")
 READ_FN = CFUNCTYPE(c_longlong, c_void_p, c_void_p, c_size_t)
 FRAGMENTS_FN = CFUNCTYPE(c_int, c_void_p, c_uint64, POINTER(c_void_p), c_size_t)
 RECORD_FN = CFUNCTYPE(c_int, c_void_p, c_uint64, c_void_p, c_void_p)
+# cec_pipeline_run_files callbacks: (user, file, ...)
+FILE_FRAGMENTS_FN = CFUNCTYPE(c_int, c_void_p, c_size_t, c_uint64, POINTER(c_void_p), c_size_t)
+FILE_RECORD_FN = CFUNCTYPE(c_int, c_void_p, c_size_t, c_uint64, c_void_p, c_void_p)
 # cec_dist_degraded_read locate callback
 LOCATE_FN = CFUNCTYPE(c_void_p, c_void_p, c_uint64, c_int)
 
 
 class PipelineOpts(Structure):
     _fields_ = [("shard_len", c_size_t), ("batch_segments", c_size_t), ("depth", c_int),
-                ("hash", c_int), ("window", c_int), ("max_segments", c_uint64)]
+                ("hash", c_int), ("window", c_int), ("max_segments", c_uint64),
+                ("host_threads", c_int), ("tail_batches", c_int)]
+
+
+class Source(Structure):
+    _fields_ = [("read", READ_FN), ("user", c_void_p), ("size", c_uint64)]
 
 
 class DistMove(Structure):
@@ -34,6 +42,9 @@ class DistMove(Structure):
 class PipelineStats(Structure):
     _fields_ = [("segments", c_uint64), ("bytes_in", c_uint64), ("seconds", c_double),
                 ("read_seconds", c_double), ("wait_seconds", c_double)]
+
+
+FILE_DONE_FN = CFUNCTYPE(c_int, c_void_p, c_size_t, POINTER(PipelineStats))
 
 
 # exported symbols and their (restype, argtypes); tests check this against include/cess_ec.h
@@ -62,6 +73,11 @@ SIGNATURES = {
                                  c_void_p]),
     "cec_sha256_hex": (c_int, [POINTER(c_void_p), c_size_t, c_size_t, POINTER(c_uint8),
                                c_void_p]),
+    "cec_sha256_host": (c_int, [POINTER(c_void_p), c_size_t, c_size_t, c_void_p, c_size_t,
+                                c_void_p, c_int]),
+    "cec_host_sha_set_form": (c_int, [c_int]),
+    "cec_host_sha_form": (c_int, []),
+    "cec_host_sha_probe": (c_double, [c_int, c_size_t, c_int]),
     "cec_split_segment": (c_int, [c_void_p, c_size_t, c_int, POINTER(c_void_p), c_size_t]),
     "cec_fill_synthetic": (c_int, [c_void_p, c_size_t, c_size_t, c_uint64, c_uint64, c_void_p]),
     "cec_set_option": (c_int, [c_void_p, c_int, c_int]),
@@ -82,6 +98,10 @@ SIGNATURES = {
     "cec_pipeline_destroy": (None, [c_void_p]),
     "cec_pipeline_run": (c_int, [c_void_p, READ_FN, FRAGMENTS_FN, RECORD_FN, c_void_p,
                                  POINTER(PipelineStats)]),
+    "cec_pipeline_info": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
+    "cec_pipeline_run_files": (c_int, [c_void_p, POINTER(Source), c_size_t, FILE_FRAGMENTS_FN,
+                                       FILE_RECORD_FN, FILE_DONE_FN, c_void_p,
+                                       POINTER(PipelineStats)]),
     "cec_challenge_indices": (c_int, [POINTER(c_uint64), c_size_t, c_uint32, c_uint32,
                                       POINTER(c_uint32), POINTER(c_size_t)]),
     "cec_audit_chunks": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_uint32,
@@ -159,6 +179,15 @@ CEC_STAT_POOL_BYTES = 3
 CEC_STAT_FFTDEC_SEGMENTS = 4
 CEC_STAT_FFTDEC_D_SEGMENTS = 5
 CEC_HQOPT_TICK = 1
+CEC_PIPE_HASH_NONE = 0
+CEC_PIPE_HASH_GPU = 1
+CEC_PIPE_HASH_HOST = 2
+CEC_PIPE_HASH_HYBRID = 3
+CEC_HSHA_SCALAR = 0
+CEC_HSHA_NI1 = 1
+CEC_HSHA_NI2 = 2
+CEC_HSHA_NI4 = 3
+CEC_HSHA_X16 = 4
 CEC_DIST_ID_BYTES = 128
 CEC_DIST_SURVIVOR = 0
 CEC_DIST_PARTIAL = 1

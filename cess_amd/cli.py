@@ -1,17 +1,19 @@
 """cess-ec command line.
 
-  python -m cess_amd.cli encode <file> [--out DIR] [--scale FILE] [--k 2 --m 1] [--devices 0,1,..]
-                                   [--hash-on auto|gpu|host]
-      streams the file through the GPU (RS encode; SegmentList hashes by --hash-on: "gpu" =
-      libcessec host pipeline with pinned multi-buffered copies and GPU hashing, "host" = SHA-NI
-      threads beside the GPU encode, "auto" = the host below 20 GiB, where it finishes sooner,
-      pipeline.AUTO_GPU_RECORD_BYTES) and prints the file's SegmentList records (the
-      deal_info of FileBank::upload_declaration, c-pallets/file-bank/src/lib.rs:419-428) as
-      JSON. --out writes every fragment as DIR/<fragment hash> while the file streams (host
-      memory holds the pipeline's pinned batches, not the file). --scale writes the SCALE bytes
-      of deal_info; --call also writes the whole upload_declaration call data (needs --account,
-      --name, --bucket). A file over SegmentCount = 1000 segments (runtime/src/lib.rs:1026) is
-      rejected unless --no-segment-limit.
+  python -m cess_amd.cli encode <file> [<file> ...] [--out DIR] [--scale FILE] [--k 2 --m 1]
+                                   [--devices 0,1,..] [--hash-on auto|hybrid|host|gpu]
+      streams the files through one GPU pipeline (RS encode; SegmentList hashes by --hash-on:
+      "hybrid" / "auto" = segment chains on host SHA-256 threads, the other fragments on the GPU
+      hash queue, the last batches on the host; "host" = every hash on host threads; "gpu" =
+      every hash on the GPU hash queue) and prints each file's SegmentList records (the
+      deal_info of FileBank::upload_declaration, c-pallets/file-bank/src/lib.rs:419-428) as JSON:
+      one object for one file, one line per file for several, which share one pipeline (pinned
+      once) and stream back to back. --out writes every fragment as DIR/<fragment hash> while the
+      files stream (host memory holds the pipeline's pinned batches, not the files). --scale
+      writes the SCALE bytes of deal_info; --call also writes the whole upload_declaration call
+      data (needs --account, --name, --bucket); both for a single file. A file over
+      SegmentCount = 1000 segments (runtime/src/lib.rs:1026) is rejected unless
+      --no-segment-limit.
   python -m cess_amd.cli verify <file> <json>
       re-encodes and compares the records.
   python -m cess_amd.cli decode <json> <fragment dir> <out file> [--k 2 --m 1]
@@ -28,60 +30,78 @@ import sys
 from . import geometry
 
 
-def _placement(args, size: int) -> str:
-    """Where the record hashes ran: "gpu" (hash queue) or "host" (SHA-NI threads)."""
+def _placement(args) -> str:
+    """Where the record hashes ran: "gpu", "host" or "hybrid"."""
     from .pipeline import record_hash_placement
-    return "gpu" if args.devices else record_hash_placement(args.hash_on, size, args.k, args.m)
+    return "gpu" if args.devices else record_hash_placement(args.hash_on)
+
+
+def _report(args, rec, st) -> dict:
+    from .segments import check_file_spec, needed_space
+    out = rec.to_json()
+    out["check_file_spec"] = check_file_spec(rec.segments, args.k + args.m)
+    out["needed_space"] = needed_space(rec.segments, args.segment_size)
+    out["pipeline"] = {"seconds": round(st.seconds, 4), "read_seconds": round(st.read_seconds, 4),
+                       "GBps": round(st.bytes_in / max(st.seconds, 1e-9) / 1e9, 3),
+                       "hash_on": _placement(args)}
+    return out
 
 
 def _encode(args) -> int:
-    from .pipeline import encode_file_records
     from .records import ErrTooManySegments
-    from .segments import check_file_spec, needed_space
-    writer = None
-    tmp = {}
-    if args.out:
-        os.makedirs(args.out, exist_ok=True)
-
-        def writer(seg, idx, view):  # hash not known yet: temporary name, renamed on its record
-            path = os.path.join(args.out, f".part-{seg}-{idx}")
-            with open(path, "wb") as f:
-                f.write(memoryview(view))
-            tmp[(seg, idx)] = path
+    from .reedsolomon import ErrShortData
     limit = 0 if args.no_segment_limit else geometry.SEGMENT_COUNT
     if args.devices and args.out:
         print("--devices (several GPUs) does not write fragments; drop --out", file=sys.stderr)
         return 2
+    if len(args.file) > 1 and (args.devices or args.scale or args.call):
+        print("--devices, --scale and --call take a single file", file=sys.stderr)
+        return 2
+    tmp = {}
+    writer = None
+    if args.out:
+        os.makedirs(args.out, exist_ok=True)
+
+        def writer(f, seg, idx, view):  # hash not known yet: temporary name, renamed on its record
+            path = os.path.join(args.out, f".part-{f}-{seg}-{idx}")
+            with open(path, "wb") as fh:
+                fh.write(memoryview(view))
+            tmp[(f, seg, idx)] = path
     try:
         if args.devices:
             from .pipeline import encode_file_records_multi
             devs = [int(x) for x in args.devices.split(",")]
-            rec, sts = encode_file_records_multi(args.file, devs, args.k, args.m,
+            rec, sts = encode_file_records_multi(args.file[0], devs, args.k, args.m,
                                                  args.segment_size, max_segments=limit,
                                                  window=args.window)
             st = sts[0]
             st.seconds = max(x.seconds for x in sts)
             st.read_seconds = max(x.read_seconds for x in sts)
             st.bytes_in = sum(x.bytes_in for x in sts)
+            results = [(rec, st)]
         else:
-            rec, st = encode_file_records(args.file, args.k, args.m, args.segment_size,
-                                          args.device, on_fragment=writer, max_segments=limit,
-                                          hash_on=args.hash_on, window=args.window)
-    except ErrTooManySegments:
+            from .pipeline import RecordsSession, _source_size, record_hash_placement
+            nseg = max(-(-_source_size(p) // args.segment_size) for p in args.file)
+            results = []
+            with RecordsSession(args.k, args.m, args.segment_size, args.device,
+                                record_hash_placement(args.hash_on),
+                                batch_segments=max(1, min(64, nseg)), window=args.window,
+                                max_segments=limit) as ses:
+                recs, _ = ses.encode_many(args.file, on_fragment=writer,
+                                          on_file=lambda f, r, fst: results.append((r, fst)))
+    except (ErrTooManySegments, ErrShortData) as e:
         for p in tmp.values():
             os.unlink(p)
-        print(json.dumps({"error": f"file exceeds SegmentCount = {geometry.SEGMENT_COUNT} "
-                                   f"segments of {args.segment_size} bytes"}))
+        msg = (f"file exceeds SegmentCount = {geometry.SEGMENT_COUNT} segments of "
+               f"{args.segment_size} bytes") if isinstance(e, ErrTooManySegments) else \
+            "empty file"
+        print(json.dumps({"error": msg}))
         return 2
     if args.out:
-        for (s, i), p in tmp.items():
-            os.replace(p, os.path.join(args.out, rec.segments[s].fragment_list[i].decode()))
-    out = rec.to_json()
-    out["check_file_spec"] = check_file_spec(rec.segments, args.k + args.m)
-    out["needed_space"] = needed_space(rec.segments, args.segment_size)
-    out["pipeline"] = {"seconds": round(st.seconds, 4), "read_seconds": round(st.read_seconds, 4),
-                       "GBps": round(st.bytes_in / max(st.seconds, 1e-9) / 1e9, 3),
-                       "hash_on": _placement(args, rec.size)}
+        for (f, s, i), p in tmp.items():
+            os.replace(p, os.path.join(args.out,
+                                       results[f][0].segments[s].fragment_list[i].decode()))
+    rec, st = results[0]
     if args.scale:
         with open(args.scale, "wb") as f:
             f.write(rec.deal_info_scale())
@@ -92,21 +112,34 @@ def _encode(args) -> int:
         with open(args.call, "wb") as f:
             f.write(rec.upload_declaration(bytes.fromhex(args.account), args.name.encode(),
                                            args.bucket.encode()))
-    json.dump(out, sys.stdout)
-    print()
+    if len(results) == 1:
+        json.dump(_report(args, rec, st), sys.stdout)
+        print()
+    else:
+        for path, (r, s) in zip(args.file, results):
+            out = _report(args, r, s)
+            out["file"] = path
+            print(json.dumps(out))
     return 0
 
 
 def _decode(args) -> int:
     from .reedsolomon import ErrTooFewShards
-    from .retrieve import ErrSegmentHashMismatch, dir_fetch, record_from_json, retrieve_file
-    with open(args.records) as f:
-        rec = record_from_json(f.read())
+    from .retrieve import (ErrRecordsInconsistent, ErrSegmentHashMismatch, dir_fetch,
+                           record_from_json, retrieve_file)
+    try:
+        with open(args.records) as f:
+            rec = record_from_json(f.read())
+    except (ValueError, KeyError, TypeError) as e:
+        print(json.dumps({"error": f"records: {type(e).__name__}: {e}"}))
+        return 2
     try:
         st = retrieve_file(rec, dir_fetch(args.fragments), args.out, args.k, args.m,
                            args.segment_size, args.device)
-    except (ErrTooFewShards, ErrSegmentHashMismatch) as e:
-        print(json.dumps({"error": str(e)}))
+    except (ErrTooFewShards, ErrSegmentHashMismatch, ErrRecordsInconsistent, ValueError) as e:
+        # ValueError: a size / segment count the records cannot hold, a fragment count other
+        # than k + m (ErrSegmentHashMismatch and ErrRecordsInconsistent are ValueErrors too)
+        print(json.dumps({"error": f"{type(e).__name__}: {e}"}))
         return 2
     print(json.dumps(st))
     return 0
@@ -116,7 +149,7 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="cess-ec")
     sub = ap.add_subparsers(dest="cmd", required=True)
     e = sub.add_parser("encode")
-    e.add_argument("file")
+    e.add_argument("file", nargs="+")
     e.add_argument("--out", default=None)
     e.add_argument("--scale", default=None, help="write deal_info's SCALE bytes here")
     e.add_argument("--call", default=None, help="write upload_declaration call data here")
@@ -126,8 +159,9 @@ def main(argv=None) -> int:
     e.add_argument("--k", type=int, default=geometry.DATA_SHARDS)
     e.add_argument("--m", type=int, default=geometry.PARITY_SHARDS)
     e.add_argument("--segment-size", type=int, default=geometry.SEGMENT_SIZE)
-    e.add_argument("--window", type=int, default=32)
-    e.add_argument("--hash-on", choices=("auto", "gpu", "host"), default="auto")
+    e.add_argument("--window", type=int, default=0, help="GPU hash-queue window in batches "
+                   "(0: the pipeline's default, 32 GPU / 16 hybrid)")
+    e.add_argument("--hash-on", choices=("auto", "hybrid", "gpu", "host"), default="auto")
     e.add_argument("--device", type=int, default=0)
     e.add_argument("--devices", default="",
                    help="comma list of GPUs: the file's segments sharded over them from this "

@@ -946,7 +946,9 @@ int build_ps_plan(cec_codec* c, const std::string& pkey, size_t nseg, bool data_
       plan->mixed_off = hl.size();
       plan->mixed_count = tagged.size();
       hl.insert(hl.end(), tagged.begin(), tagged.end());
-      plan->mixed_e.assign(nseg, 2);
+      // tuning variant 90's per-row codes: the lost shard of a tagged segment, 3 = untouched (an
+      // intact segment, or one another launch handles: nothing is written to it)
+      plan->mixed_e.assign(nseg, 3);
       for (uint32_t w : tagged) plan->mixed_e[w & 0x3FFFFFFFu] = (uint8_t)(w >> 30);
     }
   } else {

@@ -1,0 +1,45 @@
+// Internal interface of the host SHA-256 (sha256_host.cpp) for the pipeline and the C ABI.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+
+#include "../../include/cess_ec.h"
+
+namespace hsha {
+
+// n chains of `len` bytes: chain i reads bufs[i]; its hex goes to
+// hex + ((i / per) * hex_outer + i % per) * 64, and with prefix_len (a multiple of 64) the hex of
+// its first prefix_len bytes to prefix_hex + ((i / per) * prefix_outer + i % per) * 64.
+struct Job {
+  const uint8_t* const* bufs = nullptr;
+  size_t n = 0, len = 0;
+  uint8_t* hex = nullptr;
+  size_t per = 1, hex_outer = 1;
+  size_t prefix_len = 0;
+  uint8_t* prefix_hex = nullptr;
+  size_t prefix_outer = 1;
+};
+
+struct JobState {
+  Job job;
+  int form = 0;
+  std::atomic<int> left{0};
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+};
+
+void hash_range(const Job& j, size_t c0, size_t n, int form);
+// Queue a job on the process-wide pool (grown to `threads` workers). The job's pointers must stay
+// valid until it is ready.
+std::shared_ptr<JobState> submit(const Job& job, int threads);
+bool ready(const std::shared_ptr<JobState>& js);
+// Block until the job is done; with help, the caller runs queued tasks meanwhile.
+void wait(const std::shared_ptr<JobState>& js, bool help);
+
+}  // namespace hsha

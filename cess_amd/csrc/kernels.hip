@@ -660,7 +660,8 @@ __global__ __launch_bounds__(BS) void k_ct_dec1_mixed21(Layout L,
   const uint32_t seg = w & 0x3FFFFFFFu, e = w >> 30;
   if (e == 0) ct_tile<Dec1CT<2, 1, 0>, 1, NT, u32x4, 1, false, BS>(L, seg);
   else if (e == 1) ct_tile<Dec1CT<2, 1, 1>, 1, NT, u32x4, 1, false, BS>(L, seg);
-  else ct_tile<EncCT<2, 1>, 1, NT, u32x4, 1, false, BS>(L, seg);
+  else if (e == 2) ct_tile<EncCT<2, 1>, 1, NT, u32x4, 1, false, BS>(L, seg);
+  // e == 3: a segment with nothing to rebuild in this launch, left untouched
 }
 
 // Persistent grid-stride variant: a fixed grid walks the flattened (segment, tile) space.
@@ -1457,7 +1458,8 @@ __global__ __launch_bounds__(BS) void k_ct_dec1_mixed21_kargs(Layout L, uint32_t
   const uint32_t seg = seg0 + y;
   if (e == 0) ct_tile<Dec1CT<2, 1, 0>, 1, NT, u32x4, 1, false, BS>(L, seg);
   else if (e == 1) ct_tile<Dec1CT<2, 1, 1>, 1, NT, u32x4, 1, false, BS>(L, seg);
-  else ct_tile<EncCT<2, 1>, 1, NT, u32x4, 1, false, BS>(L, seg);
+  else if (e == 2) ct_tile<EncCT<2, 1>, 1, NT, u32x4, 1, false, BS>(L, seg);
+  // e == 3: a segment with nothing to rebuild in this launch, left untouched
 }
 #endif
 

@@ -1,21 +1,36 @@
-// libcessec host pipeline: a file in host memory -> segments -> fragments (+ SegmentList hashes)
-// through one GPU, with the pinned hipMemcpyAsync multi-buffering of the north_star.
+// libcessec host pipeline: files in host memory -> segments -> fragments (+ SegmentList hashes)
+// through one GPU, with the pinned hipMemcpyAsync multi-buffering of the north_star. The records
+// are `SegmentList { hash, fragment_list }` (c-pallets/file-bank/src/types.rs:13-16) for
+// FileBank::upload_declaration (c-pallets/file-bank/src/lib.rs:423-499).
 //
-// Per batch of up to B segments (segment = k * F bytes, the contiguous klauspost Split):
-//   host:    read() fills pinned input slot hs = i % depth (zero-pads the last segment)
+// Per batch of up to B segments of one file (segment = k * F bytes, the contiguous klauspost
+// Split):
+//   host:    read() fills pinned input slot hs = i % depth (zero-pads the file's last segment)
 //   s_h2d:   waits until device slot ds = i % nd is free, copies the batch in
 //   s_comp:  cec_encode_batch into the slot's parity
 //   s_d2h:   copies parity into pinned parity slot hs
-//   s_comp:  (hash = 1) then adds the batch's segment and fragment chains to the GPU hash queue
-//            and ticks it once: `window` batches hash together and a batch's hex is final
-//            `window` ticks after its add (cec_hashq_*); the hex is copied to pinned memory
-//            there too. Ticks share the compute stream with the encodes on purpose: three
-//            streams fit the device's hardware queues (GPU_MAX_HW_QUEUES = 4, one taken by the
-//            codec), and a fourth stream shared a queue with the parity copies, which held every
-//            tick behind a 11 ms D2H (rocprof timeline, profiles/r02/).
-// and the host delivers on_fragments (shards straight from the pinned slots) and on_record (hex)
-// in segment order. Reading batch i+1 on the host overlaps the copies and kernels of batch i,
-// H2D overlaps D2H (PCIe is full duplex), and the hash queue overlaps everything.
+// and the hashes of the batch's records go where the pipeline's hash mode puts them:
+//   GPU     every chain on the GPU hash queue (segment chain with data fragment 0 as its prefix
+//           digest, the other fragments), added after the encode on s_comp and ticked once per
+//           batch: `window` batches hash together and a batch's hex is final `window` ticks
+//           after its add. Ticks share the compute stream with the encodes on purpose: three
+//           streams fit the device's hardware queues (GPU_MAX_HW_QUEUES = 4, one taken by the
+//           codec), and a fourth stream shared a queue with the parity copies, which held every
+//           tick behind a 11 ms D2H (rocprof timeline, profiles/r02/).
+//   HOST    every chain on host threads (sha256_host.cpp) straight from the pinned slots: the
+//           segment chains (fragment 0 as prefix) and data fragments as soon as the batch is
+//           read, the parity once its D2H is back.
+//   HYBRID  the host takes the 16 MiB segment chains (one pass over the file's bytes, fragment
+//           0's digest on the way); the GPU queue takes the 8 MiB chains of the other fragments
+//           and parity, except for the last batches of the run's last source, whose chains the
+//           host takes too: a GPU chain finishes ~blocks x 1.9 us after its batch lands (one
+//           wave per chain), so chains added near the end would outlast the host's work.
+// Reading batch i+1 on the host overlaps the copies and kernels of batch i, H2D overlaps D2H
+// (PCIe is full duplex), and the hashing overlaps everything.
+//
+// A run takes a list of sources (files) and keeps the pipeline full across them: batches never
+// mix files, the records of each file are delivered in segment order, and a file's on_done
+// comes once its last record is out, while later files are already streaming.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -23,10 +38,12 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "../../include/cess_ec.h"
+#include "host_sha.h"
 #include "kernels.h"
 
 namespace cec {
@@ -54,6 +71,10 @@ double now_s() {
       .count();
 }
 
+// GPU time of one 64-byte block of a lone chain (the latency-form tick, DESIGN.md §4: ~1.8 us
+// measured; a little slack for the ticks' launch gaps). Used only to place a batch's chains.
+constexpr double kGpuChainSecondsPerBlock = 1.9e-6;
+
 }  // namespace
 
 struct cec_pipeline {
@@ -61,7 +82,8 @@ struct cec_pipeline {
   int k = 0, m = 0, device = 0;
   size_t F = 0, SB = 0, B = 0;  // shard bytes, segment bytes, segments per batch
   int depth = 0, nd = 0, window = 0;
-  bool hash = false;
+  int mode = CEC_PIPE_HASH_NONE;
+  int host_threads = 16, tail_batches = -1;
   uint64_t max_segments = 0;
   // pinned host ring
   std::vector<uint8_t*> h_in, h_par;
@@ -72,18 +94,39 @@ struct cec_pipeline {
   std::vector<hipEvent_t> ev_h2d, ev_enc, ev_d2h, ev_hex;  // per device slot
   cec_hashq* hq = nullptr;
   uint32_t tick_blocks = 0;
+  // host hash jobs not yet known to be finished (they read the pinned ring)
+  std::vector<std::shared_ptr<hsha::JobState>> host_jobs;
+
+  bool gpu_hash() const { return mode == CEC_PIPE_HASH_GPU || mode == CEC_PIPE_HASH_HYBRID; }
+  bool host_hash() const { return mode == CEC_PIPE_HASH_HOST || mode == CEC_PIPE_HASH_HYBRID; }
+  // first fragment index a hybrid batch leaves to the GPU: the host's segment chain yields
+  // fragment 0 as its prefix digest when F is a multiple of 64; otherwise the host hashes the
+  // data fragments and the GPU only the parity
+  int hybrid_gpu_first() const { return F % 64 == 0 ? 1 : k; }
 
   struct Batch {
-    uint64_t idx, seg_base, ticket = 0;
-    size_t nseg;
-    int hs, ds;
+    uint64_t idx = 0, seg_base = 0, ticket = 0;
+    size_t file = 0, nseg = 0;
+    int hs = 0, ds = 0;
     bool frags_done = false, hex_copied = false;
+    bool gpu = false;         // some chains on the GPU hash queue (hex copied out of slot ds)
+    bool gpu_seg = false;     // the segment chain too (GPU mode)
+    bool host_frags = false;  // the host hashes every fragment chain of the batch
+    std::shared_ptr<hsha::JobState> j_seg, j_data, j_par;
+    std::vector<const uint8_t*> p_seg, p_data, p_par;
+    std::vector<uint8_t> shex, fhex;  // host-hashed records [nseg][64], [nseg][k+m][64]
   };
+
+  void wait_host_jobs() {
+    for (auto& j : host_jobs) hsha::wait(j, false);
+    host_jobs.clear();
+  }
 
   ~cec_pipeline() {
     (void)hipSetDevice(device);
     for (hipStream_t s : {s_h2d, s_comp, s_d2h})
       if (s) (void)hipStreamSynchronize(s);
+    wait_host_jobs();
     if (hq) cec_hashq_destroy(hq);
     for (auto* v : {&h_in, &h_par, &h_shex, &h_fhex})
       for (uint8_t* p : *v)
@@ -101,25 +144,43 @@ struct cec_pipeline {
   int init(const cec_pipeline_opts& o) {
     PL_RC(cec_codec_info(codec, &k, &m, &device));
     if (o.shard_len == 0) return cec::set_error(CEC_ESHARDLEN, "zero shard length");
+    if (o.hash < CEC_PIPE_HASH_NONE || o.hash > CEC_PIPE_HASH_HYBRID)
+      return cec::set_error(CEC_EINVAL, "hash must be 0 (none), 1 (GPU), 2 (host), 3 (hybrid)");
     F = o.shard_len;
     SB = (size_t)k * F;
     B = o.batch_segments ? o.batch_segments : 64;
+    mode = o.hash;
     depth = o.depth ? o.depth : 3;
     if (depth < 2) return cec::set_error(CEC_EINVAL, "depth must be >= 2");
-    hash = o.hash != 0;
-    window = o.window ? o.window : 32;
+    window = o.window ? o.window : (mode == CEC_PIPE_HASH_HYBRID ? 16 : 32);
     if (window < 1) return cec::set_error(CEC_EINVAL, "window must be >= 1");
+    host_threads = o.host_threads > 0 ? o.host_threads : 16;
+    tail_batches = o.tail_batches;
     max_segments = o.max_segments;
-    // a slot is reused nd batches later; its hashes are final `window` ticks after its add, and
-    // two more slots keep the H2D of a reused slot from waiting on the tick just enqueued
-    nd = hash ? window + 3 : 3;
+    PL_TRY(hipSetDevice(device));
+    // a slot is reused nd batches later; with GPU hashing its hashes are final `window` ticks
+    // after its add, and two more slots keep the H2D of a reused slot from waiting on the tick
+    // just enqueued. The window shrinks to what free HBM holds (one CESS slot is
+    // ~1.5 GiB, so 35 slots are ~52 GiB, and several pipelines may share a GPU).
+    const size_t slot_bytes = B * SB + B * (size_t)m * F + (gpu_hash() ? B * (k + m + 1) * 64 : 0);
+    size_t free_b = 0, total_b = 0;
+    PL_TRY(hipMemGetInfo(&free_b, &total_b));
+    const size_t budget = (size_t)(0.85 * (double)free_b);
+    if (gpu_hash()) {
+      const size_t fit = slot_bytes ? budget / slot_bytes : 0;
+      if (fit < 4)
+        return cec::set_error(CEC_ENOMEM, "pipeline: free HBM holds fewer than 4 batch slots");
+      window = std::min<int>(window, (int)std::min<size_t>(fit - 3, 1 << 20));
+    }
+    nd = gpu_hash() ? window + 3 : 3;
     // a device slot's events are re-recorded by its next batch: that batch (i + nd) must come
     // after the slot's previous batch has delivered its fragments, which the host ring guarantees
     // only for batches `depth` apart (with depth > nd the wait for an old batch's parity copy
     // became a wait for the newest one, and the ring ran one batch deep: 27-33 GB/s at depth 4
     // against 49-52 at depth 3, profiles/r05/e2e_sweep.jsonl)
     nd = std::max(nd, depth);
-    PL_TRY(hipSetDevice(device));
+    if ((size_t)nd * slot_bytes > budget)
+      return cec::set_error(CEC_ENOMEM, "pipeline: the device slots do not fit in free HBM");
     for (hipStream_t* s : {&s_h2d, &s_comp, &s_d2h})
       PL_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
     h_in.assign(depth, nullptr);
@@ -137,7 +198,7 @@ struct cec_pipeline {
       for (auto* v : {&ev_h2d, &ev_enc, &ev_d2h, &ev_hex})
         PL_TRY(hipEventCreateWithFlags(&(*v)[i], hipEventDisableTiming));
     }
-    if (hash) {
+    if (gpu_hash()) {
       d_shex.assign(nd, nullptr);
       d_fhex.assign(nd, nullptr);
       h_shex.assign(nd, nullptr);
@@ -151,29 +212,42 @@ struct cec_pipeline {
       size_t chains = (size_t)(window + 1) * B * (k + m + 1), cap = 1024;
       while (cap < chains) cap <<= 1;
       PL_RC(cec_hashq_create(device, cap, s_comp, &hq));
-      const uint64_t blocks = cec::sha256_blocks(SB);
+      // GPU mode's longest chain is the segment's, hybrid's a fragment's
+      const uint64_t blocks = cec::sha256_blocks(mode == CEC_PIPE_HASH_GPU ? SB : F);
       tick_blocks = (uint32_t)((blocks + window - 1) / window);
     }
     return CEC_OK;
   }
 
-  // Enqueue the batch's hash chains (segment chain with fragment 0 as its prefix digest when F
-  // is a multiple of 64, the other data fragments, the parity fragments) and one tick.
-  int add_hashes(Batch& b) {
+  // GPU chains of a batch and one tick. GPU mode: the segment chain with fragment 0 as its
+  // prefix digest when F is a multiple of 64, the other data fragments, the parity. Hybrid: the
+  // fragments from hybrid_gpu_first() on (the host has the segment chain).
+  int add_gpu_hashes(Batch& b) {
     const int n = k + m;
     uint8_t* dd = d_data[b.ds];
     uint8_t* fh = d_fhex[b.ds];
     uint64_t t = 0;
-    if (F % 64 == 0) {
-      PL_RC(cec_hashq_add_prefix(hq, dd, b.nseg, 1, SB, SB, SB, d_shex[b.ds], 1, F, fh, n, &t));
-      if (k > 1)
-        PL_RC(cec_hashq_add(hq, dd + F, b.nseg * (k - 1), k - 1, SB, F, F, fh + 64, n, nullptr));
+    if (mode == CEC_PIPE_HASH_GPU) {
+      if (F % 64 == 0) {
+        PL_RC(cec_hashq_add_prefix(hq, dd, b.nseg, 1, SB, SB, SB, d_shex[b.ds], 1, F, fh, n, &t));
+        if (k > 1)
+          PL_RC(cec_hashq_add(hq, dd + F, b.nseg * (k - 1), k - 1, SB, F, F, fh + 64, n,
+                              nullptr));
+      } else {
+        PL_RC(cec_hashq_add(hq, dd, b.nseg, 1, SB, SB, SB, d_shex[b.ds], 1, &t));
+        PL_RC(cec_hashq_add(hq, dd, b.nseg * k, k, SB, F, F, fh, n, nullptr));
+      }
+      PL_RC(cec_hashq_add(hq, d_par[b.ds], b.nseg * m, m, (size_t)m * F, F, F, fh + 64 * k, n,
+                          nullptr));
     } else {
-      PL_RC(cec_hashq_add(hq, dd, b.nseg, 1, SB, SB, SB, d_shex[b.ds], 1, &t));
-      PL_RC(cec_hashq_add(hq, dd, b.nseg * k, k, SB, F, F, fh, n, nullptr));
+      const int g0 = hybrid_gpu_first();
+      if (g0 < k)
+        PL_RC(cec_hashq_add(hq, dd + (size_t)g0 * F, b.nseg * (k - g0), k - g0, SB, F, F,
+                            fh + 64 * g0, n, nullptr));
+      // equal lengths: the last add completes last
+      PL_RC(cec_hashq_add(hq, d_par[b.ds], b.nseg * m, m, (size_t)m * F, F, F, fh + 64 * k, n,
+                          &t));
     }
-    PL_RC(cec_hashq_add(hq, d_par[b.ds], b.nseg * m, m, (size_t)m * F, F, F, fh + 64 * k, n,
-                        nullptr));
     b.ticket = t;
     return cec_hashq_tick(hq, tick_blocks);
   }
@@ -184,18 +258,100 @@ struct cec_pipeline {
     return done != 0;
   }
 
-  // Tick until the batch's chains are complete, then copy its hex out (on the hash stream).
+  // Tick until the batch's chains are complete, then copy its hex out (on the compute stream).
   int copy_hex(Batch& b) {
     while (!hashed(b)) PL_RC(cec_hashq_tick(hq, tick_blocks));
-    PL_TRY(hipMemcpyAsync(h_shex[b.ds], d_shex[b.ds], b.nseg * 64, hipMemcpyDeviceToHost,
-                          s_comp));
+    if (b.gpu_seg)
+      PL_TRY(hipMemcpyAsync(h_shex[b.ds], d_shex[b.ds], b.nseg * 64, hipMemcpyDeviceToHost,
+                            s_comp));
     PL_TRY(hipMemcpyAsync(h_fhex[b.ds], d_fhex[b.ds], b.nseg * (k + m) * 64,
                           hipMemcpyDeviceToHost, s_comp));
     PL_TRY(hipEventRecord(ev_hex[b.ds], s_comp));
     b.hex_copied = true;
     return CEC_OK;
   }
+
+  std::shared_ptr<hsha::JobState> host_job(std::vector<const uint8_t*>& ptrs, size_t len,
+                                           uint8_t* hex, size_t per, size_t hex_outer,
+                                           size_t prefix_len, uint8_t* prefix_hex,
+                                           size_t prefix_outer) {
+    hsha::Job j;
+    j.bufs = ptrs.data();
+    j.n = ptrs.size();
+    j.len = len;
+    j.hex = hex;
+    j.per = per;
+    j.hex_outer = hex_outer;
+    j.prefix_len = prefix_len;
+    j.prefix_hex = prefix_hex;
+    j.prefix_outer = prefix_outer;
+    auto js = hsha::submit(j, host_threads);
+    host_jobs.push_back(js);
+    return js;
+  }
+
+  // Host chains of a freshly read batch: the segment chains (fragment 0 as prefix when F is a
+  // multiple of 64) and, when the host takes the batch's fragments, the data fragments.
+  void submit_host_data(Batch& b) {
+    const int n = k + m;
+    const uint8_t* base = h_in[b.hs];
+    b.shex.assign(b.nseg * 64, 0);
+    b.fhex.assign(b.nseg * n * 64, 0);
+    const bool prefix = F % 64 == 0;
+    b.p_seg.resize(b.nseg);
+    for (size_t s = 0; s < b.nseg; ++s) b.p_seg[s] = base + s * SB;
+    b.j_seg = host_job(b.p_seg, SB, b.shex.data(), 1, 1, prefix ? F : 0,
+                       prefix ? b.fhex.data() : nullptr, n);
+    // data fragments the host hashes on their own chains: 1..k-1 with the prefix trick (0..k-1
+    // without), for batches whose fragments are all on the host or, without the prefix trick,
+    // hybrid batches too (their GPU part is the parity alone)
+    const int d0 = prefix ? 1 : 0;
+    if (d0 < k && (b.host_frags || (!prefix && mode == CEC_PIPE_HASH_HYBRID))) {
+      b.p_data.resize(b.nseg * (k - d0));
+      for (size_t s = 0; s < b.nseg; ++s)
+        for (int j = d0; j < k; ++j) b.p_data[s * (k - d0) + (j - d0)] = base + s * SB + j * F;
+      b.j_data = host_job(b.p_data, F, b.fhex.data() + 64 * d0, (size_t)(k - d0), n, 0,
+                          nullptr, 1);
+    }
+  }
+
+  // Host chains of the parity (its D2H complete).
+  void submit_host_parity(Batch& b) {
+    if (!b.host_frags || b.j_par) return;
+    const int n = k + m;
+    b.p_par.resize(b.nseg * m);
+    for (size_t s = 0; s < b.nseg; ++s)
+      for (int j = 0; j < m; ++j) b.p_par[s * m + j] = h_par[b.hs] + (s * m + j) * F;
+    b.j_par = host_job(b.p_par, F, b.fhex.data() + 64 * k, (size_t)m, n, 0, nullptr, 1);
+  }
+
+  static bool job_ready(const std::shared_ptr<hsha::JobState>& j) { return !j || hsha::ready(j); }
+  bool host_ready(const Batch& b) const {
+    return job_ready(b.j_seg) && job_ready(b.j_data) && job_ready(b.j_par);
+  }
+  void host_wait(Batch& b) {
+    for (auto* j : {&b.j_seg, &b.j_data, &b.j_par})
+      if (*j) hsha::wait(*j, true);
+  }
+  // forget finished jobs (the list only guards the pinned ring at teardown)
+  void prune_jobs() {
+    host_jobs.erase(std::remove_if(host_jobs.begin(), host_jobs.end(),
+                                   [](const std::shared_ptr<hsha::JobState>& j) {
+                                     return hsha::ready(j);
+                                   }),
+                    host_jobs.end());
+  }
 };
+
+namespace {
+
+struct FileState {
+  uint64_t segments = 0, bytes = 0, batches_open = 0;
+  bool ended = false;
+  double t0 = 0, t_read = 0;
+};
+
+}  // namespace
 
 extern "C" {
 
@@ -216,33 +372,78 @@ int cec_pipeline_create(cec_codec* codec, const cec_pipeline_opts* opts, cec_pip
 
 void cec_pipeline_destroy(cec_pipeline* p) { delete p; }
 
-int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_fragments,
-                     cec_record_fn on_record, void* user, cec_pipeline_stats* stats) {
-  if (!p || !read) return cec::set_error(CEC_EINVAL, "null pipeline or read callback");
-  if (on_record && !p->hash) return cec::set_error(CEC_EINVAL, "on_record needs hash = 1");
+int cec_pipeline_info(const cec_pipeline* p, int* window, int* device_slots, int* depth) {
+  if (!p) return cec::set_error(CEC_EINVAL, "null pipeline");
+  if (window) *window = p->window;
+  if (device_slots) *device_slots = p->nd;
+  if (depth) *depth = p->depth;
+  return CEC_OK;
+}
+
+int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
+                           cec_file_fragments_fn on_fragments, cec_file_record_fn on_record,
+                           cec_file_done_fn on_done, void* user, cec_pipeline_stats* stats) {
+  if (!p || (nsrc && !srcs)) return cec::set_error(CEC_EINVAL, "null pipeline or sources");
+  for (size_t f = 0; f < nsrc; ++f)
+    if (!srcs[f].read) return cec::set_error(CEC_EINVAL, "null read callback");
+  if (on_record && p->mode == CEC_PIPE_HASH_NONE)
+    return cec::set_error(CEC_EINVAL, "on_record needs hashing (hash != 0)");
   PL_TRY(hipSetDevice(p->device));
-  // start clean after an aborted run: no queued copies, no live chains of the old batches
-  if (p->hash) PL_RC(cec_hashq_finish(p->hq));
+  // start clean after an aborted run: no queued copies, no live chains of the old batches, no
+  // host jobs reading the ring
+  if (p->hq) PL_RC(cec_hashq_finish(p->hq));
   for (hipStream_t s : {p->s_h2d, p->s_comp, p->s_d2h})
     if (s) PL_TRY(hipStreamSynchronize(s));
+  p->wait_host_jobs();
   const double t0 = now_s();
   double t_read = 0, t_wait = 0;
   const int n = p->k + p->m;
-  std::deque<cec_pipeline::Batch> inflight;  // batch order; popped once fully delivered
-  uint64_t seg_base = 0, bytes_in = 0, i = 0;
+  using Batch = cec_pipeline::Batch;
+  std::deque<Batch> inflight;  // batch order; popped once fully delivered
+  // Host jobs read the batches' pointer arrays and write their hex vectors: however the run
+  // ends (an error or a callback's abort returns early), they finish before `inflight` goes.
+  struct JobsGuard {
+    cec_pipeline* p;
+    ~JobsGuard() { p->wait_host_jobs(); }
+  } jobs_guard{p};
+  std::vector<FileState> files(nsrc);
+  uint64_t bytes_in = 0, segs_total = 0, i = 0;
+  size_t cur = 0;  // source being read
+  if (nsrc) files[0].t0 = t0;
+  // per-batch wall time of the source reads so far (hybrid placement of the last batches)
+  double interval = (double)(p->B * p->SB) / 45e9, last_batch_t = t0;
+  const double gpu_chain_s =
+      (double)cec::sha256_blocks(p->F) * kGpuChainSecondsPerBlock;
+  std::vector<uint8_t> rec(64 * (size_t)n);
 
+  // on_done of every finished file, in file order (an empty file ends before the one in front
+  // of it has delivered its records)
+  size_t next_done = 0;
+  auto files_done = [&]() -> int {
+    while (next_done < nsrc && files[next_done].ended && !files[next_done].batches_open) {
+      const FileState& fs = files[next_done];
+      if (on_done) {
+        cec_pipeline_stats st{fs.segments, fs.bytes, now_s() - fs.t0, fs.t_read, 0.0};
+        if (on_done(user, next_done, &st))
+          return cec::set_error(CEC_ECALLBACK, "on_done returned an error");
+      }
+      ++next_done;
+    }
+    return CEC_OK;
+  };
   // on_fragments of batch b (its parity D2H complete); shards straight from the pinned slots
-  auto deliver_frags = [&](cec_pipeline::Batch& b) -> int {
+  auto deliver_frags = [&](Batch& b) -> int {
     const double w = now_s();
     PL_TRY(hipEventSynchronize(p->ev_d2h[b.ds]));  // (a later reuse of the slot only waits more)
     t_wait += now_s() - w;
+    p->submit_host_parity(b);
     if (on_fragments) {
       const uint8_t* sh[256];
       for (size_t s = 0; s < b.nseg; ++s) {
         for (int j = 0; j < p->k; ++j) sh[j] = p->h_in[b.hs] + s * p->SB + (size_t)j * p->F;
         for (int j = 0; j < p->m; ++j)
           sh[p->k + j] = p->h_par[b.hs] + (s * p->m + j) * p->F;
-        if (on_fragments(user, b.seg_base + s, sh, p->F))
+        if (on_fragments(user, b.file, b.seg_base + s, sh, p->F))
           return cec::set_error(CEC_ECALLBACK, "on_fragments returned an error");
       }
     }
@@ -254,13 +455,25 @@ int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_frag
       if (o.idx <= idx && !o.frags_done) PL_RC(deliver_frags(o));
     return CEC_OK;
   };
+  // host slot of batch idx + depth: every reader of the slot (fragment delivery, host chains)
+  // of the batches up to idx is finished
+  auto host_through = [&](uint64_t idx) -> int {
+    PL_RC(frags_through(idx));
+    for (auto& o : inflight)
+      if (o.idx <= idx && !p->host_ready(o)) {
+        const double w = now_s();
+        p->host_wait(o);
+        t_wait += now_s() - w;
+      }
+    return CEC_OK;
+  };
   // Pop (delivering on_record) every batch up to idx; the hex copies of those are enqueued.
   std::function<int(uint64_t)> records_through;
-  // Enqueue hex copies of every batch up to idx. A copy lands in its device slot's pinned hex
-  // buffer, so the slot's previous batch (idx - nd) must have delivered its records first.
+  // Enqueue hex copies of every GPU-hashed batch up to idx. A copy lands in its device slot's
+  // pinned hex buffer, so the slot's previous batch (idx - nd) must have delivered its records.
   auto hex_through = [&](uint64_t idx) -> int {
     while (true) {
-      cec_pipeline::Batch* o = nullptr;
+      Batch* o = nullptr;
       for (auto& x : inflight)
         if (!x.hex_copied) {
           o = &x;
@@ -276,57 +489,103 @@ int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_frag
     while (!inflight.empty() && inflight.front().idx <= idx) {
       auto& b = inflight.front();
       if (!b.frags_done) PL_RC(deliver_frags(b));
-      if (p->hash) {
+      const double w = now_s();
+      if (b.gpu) {
         if (!b.hex_copied) PL_RC(p->copy_hex(b));  // its slot's previous batch is popped
-        const double w = now_s();
         PL_TRY(hipEventSynchronize(p->ev_hex[b.ds]));
-        t_wait += now_s() - w;
-        if (on_record)
-          for (size_t s = 0; s < b.nseg; ++s)
-            if (on_record(user, b.seg_base + s, p->h_shex[b.ds] + s * 64,
-                          p->h_fhex[b.ds] + s * n * 64))
-              return cec::set_error(CEC_ECALLBACK, "on_record returned an error");
       }
+      p->host_wait(b);
+      t_wait += now_s() - w;
+      if (on_record && p->mode != CEC_PIPE_HASH_NONE) {
+        const int g0 = b.gpu ? (b.gpu_seg ? 0 : p->hybrid_gpu_first()) : n;
+        for (size_t s = 0; s < b.nseg; ++s) {
+          const uint8_t* sh = b.gpu_seg ? p->h_shex[b.ds] + s * 64 : b.shex.data() + s * 64;
+          for (int f = 0; f < n; ++f) {
+            const uint8_t* src = f >= g0 ? p->h_fhex[b.ds] + (s * n + f) * 64
+                                         : b.fhex.data() + (s * n + f) * 64;
+            std::memcpy(rec.data() + 64 * f, src, 64);
+          }
+          if (on_record(user, b.file, b.seg_base + s, sh, rec.data()))
+            return cec::set_error(CEC_ECALLBACK, "on_record returned an error");
+        }
+      }
+      const size_t f = b.file;
       inflight.pop_front();
+      files[f].batches_open--;
+      PL_RC(files_done());
     }
     return CEC_OK;
   };
+  auto record_ready = [&](const Batch& b) -> bool {
+    if (!b.frags_done) return false;
+    if (b.gpu && (!b.hex_copied || hipEventQuery(p->ev_hex[b.ds]) != hipSuccess)) return false;
+    return p->host_ready(b);
+  };
 
-  while (true) {
+  while (cur < nsrc) {
     const int hs = (int)(i % p->depth);
     const int ds = (int)(i % p->nd);
-    // host slot hs: the batch that used it must have delivered its fragments
-    if (i >= (uint64_t)p->depth) PL_RC(frags_through(i - p->depth));
-    // read the next batch into pinned memory (overlaps the GPU work of earlier batches)
+    // host slot hs: the batch that used it must be done with it
+    if (i >= (uint64_t)p->depth) PL_RC(host_through(i - p->depth));
+    // read the next batch of the current source into pinned memory (overlaps the GPU work)
     uint8_t* dst = p->h_in[hs];
     const size_t cap = p->B * p->SB;
     size_t got = 0;
     const double r0 = now_s();
     while (got < cap) {
-      const long long r = read(user, dst + got, cap - got);
+      const long long r = srcs[cur].read(srcs[cur].user, dst + got, cap - got);
       if (r < 0) return cec::set_error(CEC_ECALLBACK, "read returned an error");
       if (r == 0) break;
       got += (size_t)r;
     }
-    t_read += now_s() - r0;
-    if (got == 0) break;
+    const double dr = now_s() - r0;
+    t_read += dr;
+    files[cur].t_read += dr;
+    if (got == 0) {  // source `cur` has ended: the next batch belongs to the next one
+      files[cur].ended = true;
+      PL_RC(files_done());
+      if (++cur < nsrc) files[cur].t0 = now_s();
+      continue;
+    }
+    FileState& fs = files[cur];
     bytes_in += got;
     const size_t nseg = (got + p->SB - 1) / p->SB;
     if (got < nseg * p->SB) std::memset(dst + got, 0, nseg * p->SB - got);  // zero-pad (Split)
-    if (p->max_segments && seg_base + nseg > p->max_segments)
+    if (p->max_segments && fs.segments + nseg > p->max_segments)
       return cec::set_error(CEC_ESEGCOUNT, "source exceeds max_segments segments");
+    // where this batch's fragment chains go
+    bool host_frags = p->mode == CEC_PIPE_HASH_HOST;
+    if (p->mode == CEC_PIPE_HASH_HYBRID && cur + 1 == nsrc && srcs[cur].size) {
+      const uint64_t size = srcs[cur].size, after = fs.bytes + got;
+      const uint64_t left = size > after ? (size - after + cap - 1) / cap : 0;  // batches after
+      if (p->tail_batches >= 0)
+        host_frags = left < (uint64_t)p->tail_batches;
+      else  // auto: the GPU's chains would finish after the source's remaining batches land
+        host_frags = (double)(left + 1) * interval < gpu_chain_s;
+    }
     if (i >= (uint64_t)p->nd) {
       // device slot ds: its previous batch's parity read out and (hashing) its hex copied out
-      if (p->hash) PL_RC(hex_through(i - p->nd));
+      if (p->gpu_hash()) PL_RC(hex_through(i - p->nd));
       PL_TRY(hipStreamWaitEvent(p->s_h2d, p->ev_d2h[ds], 0));
-      if (p->hash) PL_TRY(hipStreamWaitEvent(p->s_h2d, p->ev_hex[ds], 0));
+      if (p->gpu_hash()) PL_TRY(hipStreamWaitEvent(p->s_h2d, p->ev_hex[ds], 0));
     }
-    cec_pipeline::Batch b;
+    inflight.emplace_back();
+    Batch& b = inflight.back();
     b.idx = i;
-    b.seg_base = seg_base;
+    b.file = cur;
+    b.seg_base = fs.segments;
     b.nseg = nseg;
     b.hs = hs;
     b.ds = ds;
+    b.host_frags = host_frags;
+    b.gpu = p->mode == CEC_PIPE_HASH_GPU || (p->mode == CEC_PIPE_HASH_HYBRID && !host_frags);
+    b.gpu_seg = p->mode == CEC_PIPE_HASH_GPU;
+    b.hex_copied = !b.gpu;
+    fs.segments += nseg;
+    fs.bytes += got;
+    fs.batches_open++;
+    segs_total += nseg;
+    if (p->host_hash()) p->submit_host_data(b);
     PL_TRY(hipMemcpyAsync(p->d_data[ds], dst, nseg * p->SB, hipMemcpyHostToDevice, p->s_h2d));
     PL_TRY(hipEventRecord(p->ev_h2d[ds], p->s_h2d));
     PL_TRY(hipStreamWaitEvent(p->s_comp, p->ev_h2d[ds], 0));
@@ -336,8 +595,17 @@ int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_frag
     PL_TRY(hipMemcpyAsync(p->h_par[hs], p->d_par[ds], nseg * p->m * p->F, hipMemcpyDeviceToHost,
                           p->s_d2h));
     PL_TRY(hipEventRecord(p->ev_d2h[ds], p->s_d2h));
-    if (p->hash) PL_RC(p->add_hashes(b));  // on s_comp, after the encode
-    inflight.push_back(b);
+    if (b.gpu) {
+      PL_RC(p->add_gpu_hashes(b));  // on s_comp, after the encode
+    } else if (p->gpu_hash()) {
+      // nothing of this batch on the queue: its slot is free for reuse after the encode, and
+      // the queue still ticks for the chains of earlier batches
+      PL_TRY(hipEventRecord(p->ev_hex[ds], p->s_comp));
+      PL_RC(cec_hashq_tick(p->hq, p->tick_blocks));
+    }
+    const double tb = now_s();
+    interval = 0.5 * interval + 0.5 * (tb - last_batch_t);
+    last_batch_t = tb;
     // deliver whatever has completed, without blocking (a slot's event re-recorded by a newer
     // batch completes later on the same stream, so a query of it is conservative)
     for (auto& o : inflight) {
@@ -345,7 +613,7 @@ int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_frag
       if (hipEventQuery(p->ev_d2h[o.ds]) != hipSuccess) break;
       PL_RC(deliver_frags(o));
     }
-    if (p->hash) {
+    if (p->gpu_hash()) {
       uint64_t ready = 0;
       bool any = false;
       for (auto& o : inflight) {
@@ -356,28 +624,52 @@ int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_frag
       }
       if (any) PL_RC(hex_through(ready));
     }
-    while (!inflight.empty()) {
-      auto& f = inflight.front();
-      if (!f.frags_done) break;
-      if (p->hash && (!f.hex_copied || hipEventQuery(p->ev_hex[f.ds]) != hipSuccess)) break;
-      PL_RC(records_through(f.idx));
-    }
-    seg_base += nseg;
+    while (!inflight.empty() && record_ready(inflight.front()))
+      PL_RC(records_through(inflight.front().idx));
+    p->prune_jobs();
     ++i;
   }
   // drain
-  if (p->hash) PL_RC(cec_hashq_finish(p->hq));
+  if (p->hq) PL_RC(cec_hashq_finish(p->hq));
   if (i) PL_RC(records_through(i - 1));
   for (hipStream_t s : {p->s_h2d, p->s_comp, p->s_d2h})
     if (s) PL_TRY(hipStreamSynchronize(s));
+  p->wait_host_jobs();
+  PL_RC(files_done());
   if (stats) {
-    stats->segments = seg_base;
+    stats->segments = segs_total;
     stats->bytes_in = bytes_in;
     stats->seconds = now_s() - t0;
     stats->read_seconds = t_read;
     stats->wait_seconds = t_wait;
   }
   return CEC_OK;
+}
+
+namespace {
+// cec_pipeline_run's callbacks over cec_pipeline_run_files with one source
+struct OneSource {
+  cec_fragments_fn fr;
+  cec_record_fn rc;
+  void* user;
+};
+int one_frag(void* u, size_t, uint64_t seg, const uint8_t* const* shards, size_t len) {
+  auto* o = static_cast<OneSource*>(u);
+  return o->fr(o->user, seg, shards, len);
+}
+int one_record(void* u, size_t, uint64_t seg, const uint8_t* seg_hex, const uint8_t* frag_hex) {
+  auto* o = static_cast<OneSource*>(u);
+  return o->rc(o->user, seg, seg_hex, frag_hex);
+}
+}  // namespace
+
+int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_fragments,
+                     cec_record_fn on_record, void* user, cec_pipeline_stats* stats) {
+  if (!p || !read) return cec::set_error(CEC_EINVAL, "null pipeline or read callback");
+  OneSource o{on_fragments, on_record, user};
+  cec_source s{read, user, 0};
+  return cec_pipeline_run_files(p, &s, 1, on_fragments ? one_frag : nullptr,
+                                on_record ? one_record : nullptr, nullptr, &o, stats);
 }
 
 }  // extern "C"

@@ -28,8 +28,9 @@ class _Reader:
     (parallel numpy copies) or a binary stream (readinto)."""
 
     def __init__(self, src: Source, threads: int = 8, start: int = 0,
-                 stop: Optional[int] = None):
-        self.pool = cf.ThreadPoolExecutor(max_workers=threads)
+                 stop: Optional[int] = None, pool: Optional[cf.ThreadPoolExecutor] = None):
+        self.own_pool = pool is None
+        self.pool = pool or cf.ThreadPoolExecutor(max_workers=threads)
         self.threads = threads
         self.fd = self.arr = self.stream = None
         self.pos = 0
@@ -49,6 +50,8 @@ class _Reader:
                 raise ValueError("a byte range needs a path or an in-memory source")
             self.stream = src
             self.size = None
+        # bytes this reader yields in all (None for a stream)
+        self.nbytes = None if self.size is None else max(0, self.size - self.pos)
 
     def _pread(self, mv: memoryview, off: int) -> None:
         got = 0
@@ -81,28 +84,47 @@ class _Reader:
         return n
 
     def close(self) -> None:
-        self.pool.shutdown(wait=True)
+        if self.own_pool:
+            self.pool.shutdown(wait=True)
         if self.fd is not None:
             os.close(self.fd)
             self.fd = None
 
 
+HASH_MODES = {False: _lib.CEC_PIPE_HASH_NONE, True: _lib.CEC_PIPE_HASH_GPU,
+              "none": _lib.CEC_PIPE_HASH_NONE, "gpu": _lib.CEC_PIPE_HASH_GPU,
+              "host": _lib.CEC_PIPE_HASH_HOST, "hybrid": _lib.CEC_PIPE_HASH_HYBRID}
+
+
 class Pipeline:
     """cec_pipeline bound to one codec: `depth` pinned host batches of `batch_segments`
-    segments, GPU SegmentList hashing over a window of `window` batches when hash=True."""
+    segments; SegmentList hashes where `hash` says: "gpu" (True; the GPU hash queue over a window
+    of `window` batches), "host" (`host_threads` host threads, cec_sha256_host), "hybrid" (the
+    segment chains on the host, the other fragments on the GPU queue, the last `tail_batches`
+    batches of a run's last source wholly on the host; -1 = auto) or "none" (False)."""
 
     def __init__(self, enc: Encoder, shard_len: int = geometry.FRAGMENT_SIZE,
-                 batch_segments: int = 64, depth: int = 3, hash: bool = True, window: int = 32,
-                 max_segments: int = 0):
+                 batch_segments: int = 64, depth: int = 3, hash=True, window: int = 0,
+                 max_segments: int = 0, host_threads: int = 16, tail_batches: int = -1):
         self.enc = enc
         self.k, self.m = enc.DataShards, enc.ParityShards
         self.F = shard_len
-        self.opts = _lib.PipelineOpts(shard_len, batch_segments, depth, 1 if hash else 0, window,
-                                      max_segments)
+        if hash not in HASH_MODES:
+            raise ValueError("hash must be one of " + ", ".join(map(repr, HASH_MODES)))
+        self.mode = HASH_MODES[hash]
+        self.opts = _lib.PipelineOpts(shard_len, batch_segments, depth, self.mode, window,
+                                      max_segments, host_threads, tail_batches)
         self._lib = enc._lib
         self._h = c_void_p()
         check(self._lib.cec_pipeline_create(enc._h, byref(self.opts), byref(self._h)),
               "Pipeline")
+
+    def info(self) -> dict:
+        """The window the pipeline settled on (fitted to free HBM), device slots, host batches."""
+        w, nd, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(self._lib.cec_pipeline_info(self._h, byref(w), byref(nd), byref(d)),
+              "Pipeline.info")
+        return {"window": w.value, "device_slots": nd.value, "depth": d.value}
 
     def close(self) -> None:
         if self._h:
@@ -129,54 +151,175 @@ class Pipeline:
         """Stream `src` (bytes [start, stop) of a path or an in-memory buffer) through the GPU.
         on_fragments(seg, [k+m uint8 views]) sees every segment's shards (views valid during the
         call only; seg counts from the range's first segment); on_record(seg, seg_hex,
-        [k+m fragment hex]) its hashes (hash=True). Returns the run's PipelineStats."""
+        [k+m fragment hex]) its hashes. Returns the run's PipelineStats."""
+        fr = (lambda _f, seg, views: on_fragments(seg, views)) if on_fragments else None
+        rc_ = (lambda _f, seg, sh, fl: on_record(seg, sh, fl)) if on_record else None
+        return self.run_files([src], fr, rc_, None, read_threads, [(start, stop)])
+
+    def run_files(self, srcs, on_fragments: Optional[Callable[[int, int, list], None]] = None,
+                  on_record: Optional[Callable[[int, int, bytes, list], None]] = None,
+                  on_done: Optional[Callable[[int, _lib.PipelineStats], None]] = None,
+                  read_threads: int = 8, ranges=None) -> _lib.PipelineStats:
+        """Several sources in one run (cec_pipeline_run_files): the pipeline stays full across
+        files, each file's records come in segment order and on_done(file, stats) once its last
+        record is out (in file order) while later files already stream. Callbacks take the file's
+        index first: on_fragments(file, seg, views), on_record(file, seg, seg_hex, [hex]).
+        `ranges`: optional (start, stop) byte range per source. Returns the run's stats."""
         n = self.k + self.m
         F = self.F
-        reader = _Reader(src, read_threads, start, stop)
+        readers = []
         err = []
+        pool = cf.ThreadPoolExecutor(max_workers=read_threads)  # shared by the sources' readers
+        try:
+            for i, src in enumerate(srcs):
+                a, b = ranges[i] if ranges else (0, None)
+                readers.append(_Reader(src, read_threads, a, b, pool))
+        except BaseException:
+            for r in readers:
+                r.close()
+            pool.shutdown(wait=True)
+            raise
 
-        def rd(_u, dst, cap):
-            try:
-                return reader(dst, cap)
-            except BaseException as e:  # noqa: BLE001 - re-raised after the C call returns
-                err.append(e)
-                return -1
+        def make_read(reader):
+            def rd(_u, dst, cap):
+                try:
+                    return reader(dst, cap)
+                except BaseException as e:  # noqa: BLE001 - re-raised after the C call returns
+                    err.append(e)
+                    return -1
+            return _lib.READ_FN(rd)
 
-        def fr(_u, seg, shards, _len):
+        def fr(_u, f, seg, shards, _len):
             try:
                 views = [np.ctypeslib.as_array((ctypes.c_uint8 * F).from_address(shards[i]))
                          for i in range(n)]
-                on_fragments(seg, views)
+                on_fragments(f, seg, views)
                 return 0
             except BaseException as e:  # noqa: BLE001
                 err.append(e)
                 return -1
 
-        def rc_(_u, seg, seg_hex, frag_hex):
+        def rc_(_u, f, seg, seg_hex, frag_hex):
             try:
                 fh = ctypes.string_at(frag_hex, 64 * n)
-                on_record(seg, ctypes.string_at(seg_hex, 64),
+                on_record(f, seg, ctypes.string_at(seg_hex, 64),
                           [fh[64 * i:64 * (i + 1)] for i in range(n)])
                 return 0
             except BaseException as e:  # noqa: BLE001
                 err.append(e)
                 return -1
 
-        cb_read = _lib.READ_FN(rd)
-        cb_frag = _lib.FRAGMENTS_FN(fr) if on_fragments else _lib.FRAGMENTS_FN()
-        cb_rec = _lib.RECORD_FN(rc_) if on_record else _lib.RECORD_FN()
+        def dn(_u, f, st):
+            try:
+                on_done(f, st.contents)
+                return 0
+            except BaseException as e:  # noqa: BLE001
+                err.append(e)
+                return -1
+
+        cbs = [make_read(r) for r in readers]
+        arr = (_lib.Source * max(1, len(readers)))()
+        for i, r in enumerate(readers):
+            arr[i].read = cbs[i]
+            arr[i].user = None
+            arr[i].size = r.nbytes or 0
+        cb_frag = _lib.FILE_FRAGMENTS_FN(fr) if on_fragments else _lib.FILE_FRAGMENTS_FN()
+        cb_rec = _lib.FILE_RECORD_FN(rc_) if on_record else _lib.FILE_RECORD_FN()
+        cb_done = _lib.FILE_DONE_FN(dn) if on_done else _lib.FILE_DONE_FN()
         stats = _lib.PipelineStats()
         try:
-            rc = self._lib.cec_pipeline_run(self._h, cb_read, cb_frag, cb_rec, None, byref(stats))
+            rc = self._lib.cec_pipeline_run_files(self._h, arr, len(readers), cb_frag, cb_rec,
+                                                  cb_done, None, byref(stats))
         finally:
-            reader.close()
+            for r in readers:
+                r.close()
+            pool.shutdown(wait=True)
         if err:
             raise err[0]
         if rc == _lib.CEC_ESEGCOUNT:
             from .records import ErrTooManySegments
             raise ErrTooManySegments(ErrTooManySegments.__doc__)
-        check(rc, "Pipeline.run")
+        check(rc, "Pipeline.run_files")
         return stats
+
+
+class RecordsSession:
+    """A long-lived uploader: one codec and one pipeline (pinned ring pinned once, device slots
+    allocated once) for many files, each turned into its FileRecord (SegmentLists + file hash).
+    `hash_on`: "hybrid" (default: host SHA-256 on the segment chains, the GPU queue on the other
+    fragments, the run's last batches wholly on the host), "host", "gpu". encode_many() streams
+    several files back to back in one pipeline run, so one file's last hashes overlap the next
+    file's copies."""
+
+    def __init__(self, k: int = geometry.DATA_SHARDS, m: int = geometry.PARITY_SHARDS,
+                 segment_size: int = geometry.SEGMENT_SIZE, device: int = 0,
+                 hash_on: str = "hybrid", batch_segments: int = 64, depth: int = 3,
+                 window: int = 0, host_threads: int = 16, tail_batches: int = -1,
+                 max_segments: int = 0, read_threads: int = 8):
+        if segment_size % k:
+            raise ValueError("segment_size must be a multiple of k")
+        if hash_on not in ("gpu", "host", "hybrid"):
+            raise ValueError("hash_on must be 'gpu', 'host' or 'hybrid'")
+        self.k, self.m, self.segment_size = k, m, segment_size
+        self.hash_on = hash_on
+        self.read_threads = read_threads
+        self.enc = Encoder(k, m, device)
+        try:
+            self.pipe = Pipeline(self.enc, segment_size // k, batch_segments=batch_segments,
+                                 depth=depth, hash=hash_on, window=window,
+                                 max_segments=max_segments, host_threads=host_threads,
+                                 tail_batches=tail_batches)
+        except BaseException:
+            self.enc.close()
+            raise
+
+    def encode_many(self, srcs, on_fragment=None, on_file=None):
+        """[FileRecord] of every source, in one pipeline run. on_fragment(file, seg, idx, view)
+        sees each fragment; on_file(file, FileRecord, stats) each file as soon as its records are
+        complete (later files still streaming). Returns ([FileRecord], run PipelineStats)."""
+        from .segments import FileRecord, SegmentList, file_hash
+        srcs = list(srcs)
+        recs = [dict() for _ in srcs]
+        out = [None] * len(srcs)
+
+        def on_rec(f, seg, sh, fl):
+            recs[f][seg] = SegmentList(sh, fl)
+
+        def on_done(f, st):
+            if not recs[f]:
+                from .reedsolomon import ErrShortData
+                raise ErrShortData(ErrShortData.__doc__)
+            r = FileRecord(b"", int(st.bytes_in), [recs[f][s] for s in range(len(recs[f]))])
+            r.file_hash = file_hash(r.segments)
+            recs[f] = None
+            out[f] = r
+            if on_file is not None:
+                on_file(f, r, _lib.PipelineStats(st.segments, st.bytes_in, st.seconds,
+                                                 st.read_seconds, st.wait_seconds))
+
+        def frags(f, seg, views):
+            for i, v in enumerate(views):
+                on_fragment(f, seg, i, v)
+
+        st = self.pipe.run_files(srcs, frags if on_fragment else None, on_rec, on_done,
+                                 self.read_threads)
+        return out, st
+
+    def encode(self, src: Source, on_fragment=None):
+        """(FileRecord, PipelineStats) of one file."""
+        cb = (lambda _f, seg, idx, v: on_fragment(seg, idx, v)) if on_fragment else None
+        recs, st = self.encode_many([src], cb)
+        return recs[0], st
+
+    def close(self) -> None:
+        self.pipe.close()
+        self.enc.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 def _source_size(src: Source) -> Optional[int]:
@@ -189,100 +332,45 @@ def _source_size(src: Source) -> Optional[int]:
     return None  # a stream
 
 
-# encode_file_records(hash_on="auto") hashes on the GPU from this size up. Measured fresh per
-# call, RS(2,1), 16 host threads (profiles/r05/records_crossover.jsonl): the GPU path pays
-# ~0.3 s pinning + ~0.3 s unpinning its 4.5 GiB ring and the last segment chain (0.5 s when the
-# chip is busy, 1.15 s for a lone one-segment file), so the host wins up to 16 GiB (1.26 s
-# against 1.43) and the GPU from 32 GiB (1.75 s against 2.28; 30 GB/s against 15.6 at 64 GiB).
-# CESS's SegmentCount = 1000 segments (15.6 GiB) keeps every declarable file on the host.
-AUTO_GPU_RECORD_BYTES = 20 << 30
-
-
-def record_hash_placement(hash_on: str, size: Optional[int], k: int, m: int) -> str:
-    """"gpu" or "host" for encode_file_records' hash_on ("auto" resolved by source size and
-    code width: a batch of >= 2048 fragments keeps the GPU's hash lanes busy)."""
-    if hash_on != "auto":
-        return hash_on
-    return "host" if (size is not None and size < AUTO_GPU_RECORD_BYTES
-                      and 64 * (k + m) < 2048) else "gpu"
+def record_hash_placement(hash_on: str, size: Optional[int] = None, k: int = 2,
+                          m: int = 1) -> str:
+    """Where encode_file_records' record hashes run: "gpu", "host" or "hybrid". "auto" is the
+    hybrid placement (segment chains on host SHA-256 threads, the other fragments on the GPU hash
+    queue, the last batches wholly on the host); with it the pipeline itself moves every batch of
+    a file too small to outlast one GPU chain to the host (cec_pipeline_opts.tail_batches = -1),
+    so no size threshold is needed here. Measured on one MI355X + its 16-CPU share, 8 GiB
+    in-memory file, RS(2,1): see `extra.host_e2e` of the bench line."""
+    if hash_on not in ("gpu", "host", "hybrid", "auto"):
+        raise ValueError("hash_on must be 'gpu', 'host', 'hybrid' or 'auto'")
+    return "hybrid" if hash_on == "auto" else hash_on
 
 
 def encode_file_records(path_or_buf: Source, k: int = geometry.DATA_SHARDS,
                         m: int = geometry.PARITY_SHARDS,
                         segment_size: int = geometry.SEGMENT_SIZE, device: int = 0,
                         on_fragment: Optional[Callable[[int, int, np.ndarray], None]] = None,
-                        max_segments: int = 0, hash_on: str = "gpu", hash_threads: int = 16,
-                        **kw):
-    """File -> FileRecord (SegmentLists + two-level file hash), encoded on the GPU.
-    on_fragment(seg, idx, view) sees each fragment (before its hash is known on the GPU path).
+                        max_segments: int = 0, hash_on: str = "auto", hash_threads: int = 16,
+                        session: Optional["RecordsSession"] = None, **kw):
+    """File -> (FileRecord, PipelineStats): SegmentLists + two-level file hash, encoded on the GPU
+    through the C pipeline. on_fragment(seg, idx, view) sees each fragment as soon as its
+    batch's parity is back (before its hash is known).
 
-    hash_on "gpu": the C pipeline (pinned multi-buffered copies, SegmentList hashes through the
-    GPU hash queue); a file's records land one 16 MiB segment chain (~0.47 s) after its last
-    batch. "host": SegmentEncoder with SHA-256 (OpenSSL SHA-NI) on `hash_threads` host threads
-    beside the GPU encode. "auto": the host below AUTO_GPU_RECORD_BYTES for codes whose batch
-    holds < 2048 fragments, the GPU otherwise and for streams of unknown size. The records are
-    the same either way."""
-    from .segments import FileRecord, SegmentList, file_hash
+    hash_on: "hybrid" / "auto" (segment chains on `hash_threads` host threads, the other
+    fragments on the GPU hash queue, the last batches on the host), "host" (every chain on the
+    host threads), "gpu" (every chain on the GPU hash queue). The records are the same either
+    way. `session`: a RecordsSession to reuse (its pinned ring and device slots stay allocated
+    between files); without one, a session sized to the file is created and closed here."""
     if segment_size % k:
         raise ValueError("segment_size must be a multiple of k")
-    if hash_on not in ("gpu", "host", "auto"):
-        raise ValueError("hash_on must be 'gpu', 'host' or 'auto'")
+    hash_on = record_hash_placement(hash_on, None, k, m)
+    if session is not None:
+        return session.encode(path_or_buf, on_fragment)
     size = _source_size(path_or_buf)
-    hash_on = record_hash_placement(hash_on, size, k, m)
-    if hash_on == "host":
-        return _encode_file_records_host(path_or_buf, size, k, m, segment_size, device,
-                                         on_fragment, max_segments, hash_threads,
-                                         kw.get("batch_segments"))
-    recs = {}
     if size is not None:  # a small file does not need 1 GiB pinned batches
-        # (the window stays: a chain finishes after `window` ticks of blocks/window each, so a
-        # narrower window only makes each tick coarser; measured 1.52 s against 1.11 at 8 GiB)
         kw.setdefault("batch_segments", max(1, min(64, -(-size // segment_size))))
-    enc = Encoder(k, m, device)
-    try:
-        with Pipeline(enc, segment_size // k, max_segments=max_segments, **kw) as p:
-            def frags(seg, views):
-                for i, v in enumerate(views):
-                    on_fragment(seg, i, v)
-
-            st = p.run(path_or_buf, frags if on_fragment else None,
-                       lambda seg, sh, fl: recs.__setitem__(seg, SegmentList(sh, fl)))
-    finally:
-        enc.close()
-    if not recs:
-        from .reedsolomon import ErrShortData
-        raise ErrShortData(ErrShortData.__doc__)
-    out = FileRecord(b"", int(st.bytes_in), [recs[s] for s in range(len(recs))])
-    out.file_hash = file_hash(out.segments)
-    return out, st
-
-
-def _encode_file_records_host(src, size, k, m, segment_size, device, on_fragment, max_segments,
-                              hash_threads, batch_segments=None):
-    """encode_file_records' host-hash path: SegmentEncoder (GPU encode, pinned double-buffered
-    batches sized to the file unless batch_segments is given, SHA-256 on host threads; the C
-    pipeline's other options do not apply). Returns (FileRecord, PipelineStats)."""
-    import time
-
-    from .segments import SegmentEncoder
-    if size is None:
-        raise ValueError("hash_on='host' needs a path or an in-memory source (known size)")
-    nseg = -(-size // segment_size)
-    if size == 0:
-        from .reedsolomon import ErrShortData
-        raise ErrShortData(ErrShortData.__doc__)
-    if max_segments and nseg > max_segments:
-        from .records import ErrTooManySegments
-        raise ErrTooManySegments(ErrTooManySegments.__doc__)
-    t0 = time.perf_counter()
-    se = SegmentEncoder(k, m, segment_size, batch_segments=batch_segments or min(64, nseg),
-                        device=device, hash_on="host", hash_threads=hash_threads)
-    try:
-        rec = se.encode_file(src, on_fragment=on_fragment)
-    finally:
-        se.close()
-    st = _lib.PipelineStats(len(rec.segments), rec.size, time.perf_counter() - t0, 0.0, 0.0)
-    return rec, st
+    with RecordsSession(k, m, segment_size, device, hash_on, max_segments=max_segments,
+                        host_threads=hash_threads, **kw) as ses:
+        return ses.encode(path_or_buf, on_fragment)
 
 
 def encode_file_records_multi(src: Union[str, bytes, bytearray, memoryview, np.ndarray],
@@ -335,5 +423,5 @@ def encode_file_records_multi(src: Union[str, bytes, bytearray, memoryview, np.n
     return out, [st for _, st in parts if st is not None]
 
 
-__all__ = ["Pipeline", "encode_file_records", "encode_file_records_multi", "CecError",
-           "AUTO_GPU_RECORD_BYTES", "record_hash_placement"]
+__all__ = ["Pipeline", "RecordsSession", "encode_file_records", "encode_file_records_multi",
+           "CecError", "record_hash_placement"]

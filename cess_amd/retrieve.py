@@ -24,6 +24,8 @@ import concurrent.futures as cf
 import hashlib
 import json
 import os
+import re
+import stat
 import time
 from typing import BinaryIO, Callable, Dict, Optional, Union
 
@@ -55,15 +57,29 @@ def record_from_json(obj: Union[str, dict]) -> FileRecord:
     return FileRecord(obj["file_hash"].encode(), int(obj["size"]), segs)
 
 
+_HEX64 = re.compile(rb"[0-9a-f]{64}")
+
+
 def dir_fetch(directory: str) -> FetchFn:
-    """Fragments stored as files named by their hash (what `cli encode --out DIR` writes)."""
+    """Fragments stored as files named by their hash (what `cli encode --out DIR` writes). A
+    recorded hash is used as a file name only when it is exactly 64 lowercase hex chars (a crafted
+    record must not name "../x", an absolute path or a device), and only regular files are read;
+    anything else is a missing fragment."""
     def fetch(_seg: int, _frag: int, h: bytes):
+        if not _HEX64.fullmatch(h):
+            return None
         path = os.path.join(directory, h.decode())
         try:
-            with open(path, "rb") as f:
-                return f.read()
-        except FileNotFoundError:
+            fd = os.open(path, os.O_RDONLY | getattr(os, "O_NONBLOCK", 0))
+        except (FileNotFoundError, NotADirectoryError):
             return None
+        try:
+            if not stat.S_ISREG(os.fstat(fd).st_mode):
+                return None
+            with os.fdopen(fd, "rb", closefd=False) as f:
+                return f.read()
+        finally:
+            os.close(fd)
     return fetch
 
 
@@ -73,7 +89,7 @@ class Retriever:
 
     def __init__(self, k: int = geometry.DATA_SHARDS, m: int = geometry.PARITY_SHARDS,
                  segment_size: int = geometry.SEGMENT_SIZE, device: int = 0,
-                 batch_segments: int = 64, threads: int = 8):
+                 batch_segments: int = 64, threads: int = 16):
         if segment_size % k:
             raise ValueError("segment_size must be a multiple of k")
         self.k, self.m, self.n = k, m, k + m
@@ -81,12 +97,18 @@ class Retriever:
         self.F = segment_size // k
         self.device = device
         self.B = max(1, batch_segments)
+        # two executors: `pool` runs the fetches + fragment checks of the next batch while
+        # `work` stages this batch's valid fragments, rebuilds and checks its segments (on one
+        # FIFO executor the staging and checks queued behind the next batch's gathers, so the
+        # rebuild did not overlap them). The default 16 threads is the GPU's CPU share.
         self.pool = cf.ThreadPoolExecutor(max_workers=max(1, threads))
+        self.work = cf.ThreadPoolExecutor(max_workers=max(1, threads))
         self.enc = None
         self.d_data = self.d_par = self.h_data = self.h_par = None
 
     def close(self) -> None:
         self.pool.shutdown(wait=True)
+        self.work.shutdown(wait=True)
         if self.enc is not None:
             self.enc.close()
             self.enc = None
@@ -172,7 +194,7 @@ class Retriever:
         def stage(c):
             i, f, a = c
             np.copyto(hd[i, f] if f < k else hp[i, f - k], a)
-        list(self.pool.map(stage, copies))
+        list(self.work.map(stage, copies))
         # only the valid fragments cross PCIe: the gather stops at k of them, so they are exactly
         # the survivors the rebuild reads (the slots of lost fragments are never read)
         for i, f, _a in copies:
@@ -224,8 +246,8 @@ class Retriever:
             for b0 in range(0, nseg, self.B):
                 idx = list(range(b0, min(nseg, b0 + self.B)))
                 got = [f.result() for f in pending]
-                # the next batch's fetches and checks run on the pool while this one is rebuilt
-                # on the GPU (the pool is otherwise idle then) and checked
+                # the next batch's fetches and fragment checks run on `pool` while this one is
+                # staged, rebuilt on the GPU and checked on `work`
                 pending = gather(b0 + self.B) if b0 + self.B < nseg else []
                 goods = [g for g, _, _, _ in got]
                 streams = [h for _, _, _, h in got]  # (hasher, data fragments streamed)
@@ -245,7 +267,7 @@ class Retriever:
                             raise ErrSegmentHashMismatch(f"segment {idx[i]} does not match "
                                                          f"its recorded hash")
                     return goods[i]
-                for g in self.pool.map(check, range(len(idx))):
+                for g in self.work.map(check, range(len(idx))):
                     for f in range(self.k):  # the data fragments in order, the padding dropped
                         take = min(self.F, rec.size - written)
                         if take <= 0:

@@ -134,6 +134,28 @@ int cec_sha256_batch(cec_codec* codec, const uint8_t* d_data, const uint8_t* d_p
 int cec_sha256_hex(const uint8_t* const* d_bufs, size_t n, size_t len, uint8_t* hex,
                    void* hip_stream);
 
+/* Host SHA-256 of n HOST buffers of `len` bytes (the records of a batch whose bytes are in host
+ * memory): 64 lowercase hex chars per buffer to hex[i*64 ...]; with prefix_hex, also the hex of
+ * each buffer's first prefix_len bytes (a nonzero multiple of 64, <= len; a segment's chain then
+ * yields data fragment 0's hash, as cec_hashq_add_prefix does on the GPU). Runs on `threads`
+ * threads of a process-wide pool (<= 1: the calling thread only); each core hashes several
+ * equal-length chains at once (SHA-NI interleaved 2 or 4 ways, or AVX-512 16 lanes), because one
+ * chain alone leaves most of a core's SHA throughput idle. Synchronous. Host only, no GPU. */
+int cec_sha256_host(const uint8_t* const* bufs, size_t n, size_t len, uint8_t* hex,
+                    size_t prefix_len, uint8_t* prefix_hex, int threads);
+/* Forms of the host hasher: which one runs is process-wide (cec_host_sha_set_form; -1 restores
+ * the default, SHA-NI x2 where the CPU has SHA-NI). cec_host_sha_probe times one form on the
+ * calling thread over `chains` chains of bytes_per_chain bytes and returns GB/s (< 0: the CPU
+ * lacks the form). */
+#define CEC_HSHA_SCALAR 0
+#define CEC_HSHA_NI1 1
+#define CEC_HSHA_NI2 2
+#define CEC_HSHA_NI4 3
+#define CEC_HSHA_X16 4
+int cec_host_sha_set_form(int form);
+int cec_host_sha_form(void);
+double cec_host_sha_probe(int form, size_t bytes_per_chain, int chains);
+
 /* Hash queue: streaming SHA-256 of many long device buffers (fragment and segment hashes).
  * Chains keep their state in HBM between launches, so one tick advances every live chain of
  * every batch added so far; a producer that adds a batch per step and ticks once per step hashes
@@ -184,22 +206,34 @@ int cec_hashq_set_option(cec_hashq* q, int option, int value);
 int cec_split_segment(const uint8_t* seg, size_t seg_len, int k, uint8_t* const* shards,
                       size_t shard_len);
 
-/* ---- host pipeline: a file in host memory through the GPU ------------------------------------
+/* ---- host pipeline: files in host memory through the GPU ------------------------------------
  * The north_star's pinned hipMemcpyAsync multi-buffering behind the C ABI. A pipeline owns a
- * ring of `depth` pinned host batches and device slots for one codec; cec_pipeline_run streams
- * a source through it batch by batch: read() fills a pinned batch (the file's next bytes; the
- * last segment is zero-padded, klauspost Split), H2D on a copy stream, cec_encode_batch on a
- * compute stream, parity D2H on a third stream, so reading batch i+1 overlaps the copies and
- * kernels of batch i and H2D overlaps D2H. With hash = 1 every SegmentList hash (segment hash
- * and the k+m fragment hashes, SHA-256 hex) is computed on the GPU by a hash queue that keeps
- * `window` batches hashing at once (device slots = window + 3).
+ * ring of `depth` pinned host batches and device slots for one codec; a run streams sources
+ * through it batch by batch: read() fills a pinned batch (the file's next bytes; the last
+ * segment is zero-padded, klauspost Split), H2D on a copy stream, cec_encode_batch on a compute
+ * stream, parity D2H on a third stream, so reading batch i+1 overlaps the copies and kernels of
+ * batch i and H2D overlaps D2H. The SegmentList hashes (segment hash and the k+m fragment
+ * hashes, SHA-256 hex, c-pallets/file-bank/src/types.rs:13-16) are computed where `hash` says:
+ *   CEC_PIPE_HASH_GPU     on the GPU by a hash queue that keeps `window` batches hashing at once
+ *                         (device slots = window + 3);
+ *   CEC_PIPE_HASH_HOST    on `host_threads` host threads (cec_sha256_host) from the pinned ring;
+ *   CEC_PIPE_HASH_HYBRID  the segment chains (fragment 0's digest on the way) on the host, the
+ *                         other fragments' chains on the GPU queue, except for the last batches
+ *                         of the run's last source, which the host hashes wholly (`tail_batches`;
+ *                         -1 = auto: the batches whose GPU chains would finish after the source's
+ *                         remaining batches have landed; needs the source's size).
+ * The pipeline is reusable: keep one for many files (its pinned ring is pinned once).
  *   read(user, dst, cap): write up to cap source bytes at dst; return the count, 0 at the end,
  *     < 0 to abort (CEC_ECALLBACK).
  *   on_fragments(user, seg, shards, shard_len): the k+m shards of segment `seg`, host memory
  *     valid during the call; in segment order, as soon as the batch's parity is back.
  *   on_record(user, seg, seg_hex, frag_hex): the segment's 64 hex chars and its k+m fragment
- *     hashes (k+m)*64 hex chars, fragment index order; in segment order, `window` batches later.
+ *     hashes (k+m)*64 hex chars, fragment index order; in segment order.
  * Callbacks run on the calling thread and return 0 (nonzero aborts with CEC_ECALLBACK). */
+#define CEC_PIPE_HASH_NONE 0
+#define CEC_PIPE_HASH_GPU 1
+#define CEC_PIPE_HASH_HOST 2
+#define CEC_PIPE_HASH_HYBRID 3
 typedef long long (*cec_read_fn)(void* user, uint8_t* dst, size_t cap);
 typedef int (*cec_fragments_fn)(void* user, uint64_t seg, const uint8_t* const* shards,
                                 size_t shard_len);
@@ -209,29 +243,54 @@ typedef struct cec_pipeline_opts {
   size_t shard_len;      /* F: a segment is k * F bytes */
   size_t batch_segments; /* segments per batch (0: 64) */
   int depth;             /* pinned host batches (0: 3; >= 2) */
-  int hash;              /* 1: SegmentList hashes on the GPU (on_record); 0: none */
-  int window;            /* batches hashing at once when hash = 1 (0: 32); the pipeline holds
-                            window + 3 device batch slots (1.5 GiB each for CESS batches) */
-  uint64_t max_segments; /* 0: no limit; else CEC_ESEGCOUNT when the source has more segments
+  int hash;              /* CEC_PIPE_HASH_*: 0 none, 1 GPU, 2 host, 3 hybrid */
+  int window;            /* batches hashing at once on the GPU queue (0: 32, hybrid 16); the
+                            pipeline holds window + 3 device batch slots (1.5 GiB each for CESS
+                            batches) and shrinks the window to what free HBM holds */
+  uint64_t max_segments; /* 0: no limit; else CEC_ESEGCOUNT when a source has more segments
                             (CEC_SEGMENT_COUNT: what one upload_declaration can carry) */
+  int host_threads;      /* host SHA-256 threads for hash = 2 / 3 (0: 16) */
+  int tail_batches;      /* hash = 3: batches at the end of the last source hashed wholly on
+                            the host (-1: auto, 0: none) */
 } cec_pipeline_opts;
 typedef struct cec_pipeline_stats {
   uint64_t segments;   /* segments encoded */
   uint64_t bytes_in;   /* source bytes read */
-  double seconds;      /* wall time of the run */
+  double seconds;      /* wall time of the run (per file: from its first read to its on_done) */
   double read_seconds; /* time inside read() */
-  double wait_seconds; /* host time blocked on the GPU */
+  double wait_seconds; /* host time blocked on the GPU or the host hashers */
 } cec_pipeline_stats;
 typedef struct cec_pipeline cec_pipeline;
 int cec_pipeline_create(cec_codec* codec, const cec_pipeline_opts* opts, cec_pipeline** out);
-/* Waits for the pipeline's own streams, then frees its pinned host ring and device slots. The HIP
- * runtime's hipHostFree / hipFree synchronise the whole device, so other codecs' work on this GPU
- * stalls until it is done: destroy a pipeline while the device is idle, or keep it (a pipeline is
- * reusable, one run per file). */
+/* Waits for the pipeline's own streams and host hash jobs, then frees its pinned host ring and
+ * device slots. The HIP runtime's hipHostFree / hipFree synchronise the whole device, so other
+ * codecs' work on this GPU stalls until it is done: destroy a pipeline while the device is idle,
+ * or keep it (a pipeline is reusable, one run per file or per list of files). */
 void cec_pipeline_destroy(cec_pipeline* p);
+/* The window the pipeline settled on (after fitting its slots into free HBM), its device batch
+ * slots and pinned host batches. Any output may be NULL. */
+int cec_pipeline_info(const cec_pipeline* p, int* window, int* device_slots, int* depth);
 /* Stream one source through the pipeline (reusable: run again for the next file). */
 int cec_pipeline_run(cec_pipeline* p, cec_read_fn read, cec_fragments_fn on_fragments,
                      cec_record_fn on_record, void* user, cec_pipeline_stats* stats);
+/* Several sources (files) in one run, back to back: batches never mix files, segment numbers
+ * count from 0 per file, each file's records come in segment order and its on_done once its
+ * last record is out, in file order, while the next files already stream (the hashing of one
+ * file's last batches overlaps the next file's copies). size: the source's bytes, 0 = unknown
+ * (needed only for the hybrid placement of the last batches). stats: the whole run. */
+typedef struct cec_source {
+  cec_read_fn read;
+  void* user; /* passed to read */
+  uint64_t size;
+} cec_source;
+typedef int (*cec_file_fragments_fn)(void* user, size_t file, uint64_t seg,
+                                     const uint8_t* const* shards, size_t shard_len);
+typedef int (*cec_file_record_fn)(void* user, size_t file, uint64_t seg, const uint8_t* seg_hex,
+                                  const uint8_t* frag_hex);
+typedef int (*cec_file_done_fn)(void* user, size_t file, const cec_pipeline_stats* file_stats);
+int cec_pipeline_run_files(cec_pipeline* p, const cec_source* sources, size_t nsources,
+                           cec_file_fragments_fn on_fragments, cec_file_record_fn on_record,
+                           cec_file_done_fn on_done, void* user, cec_pipeline_stats* stats);
 
 /* ---- storage audit chunks ---------------------------------------------
  * A fragment is CHUNK_COUNT = 1024 chunks (primitives/common/src/lib.rs:62): 8 KiB chunks of an

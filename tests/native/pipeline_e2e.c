@@ -5,7 +5,11 @@
  * C oracle (linked separately, test infrastructure) after the timed run. Prints one JSON line
  * with the end-to-end rate (PCIe-inclusive: H2D of the data, D2H of the parity, hashes on the
  * GPU).
- * usage: pipeline_e2e k m F nseg batch depth hash window [uniq] [check_every]
+ * usage: pipeline_e2e k m F nseg batch depth hash window [uniq] [check_every] [tail]
+ *                     [tail_batches]
+ * hash: 0 none, 1 GPU, 2 host, 3 hybrid (CEC_PIPE_HASH_*). Hash modes 2 and 3 run through
+ * cec_pipeline_run_files with the source's size (the hybrid placement of the last batches needs
+ * it; tail_batches -1 = auto), the others through cec_pipeline_run.
  * build: gcc -O2 -pthread tests/native/pipeline_e2e.c -Iinclude -Lcess_amd -lcessec
  *            -Loracle/build -loracle -Wl,-rpath,... -o pipeline_e2e */
 #include <pthread.h>
@@ -150,6 +154,24 @@ static int on_rec(void* user, uint64_t seg, const uint8_t* seg_hex, const uint8_
   return 0;
 }
 
+/* cec_pipeline_run_files callbacks: one source, so the file index is 0 */
+static int on_frags_f(void* user, size_t file, uint64_t seg, const uint8_t* const* shards,
+                      size_t shard_len) {
+  if (file != 0) ((ctx_t*)user)->bad++;
+  return on_frags(user, seg, shards, shard_len);
+}
+static int on_rec_f(void* user, size_t file, uint64_t seg, const uint8_t* seg_hex,
+                    const uint8_t* frag_hex) {
+  if (file != 0) ((ctx_t*)user)->bad++;
+  return on_rec(user, seg, seg_hex, frag_hex);
+}
+static int on_done_f(void* user, size_t file, const cec_pipeline_stats* st) {
+  ctx_t* x = (ctx_t*)user;
+  if (file != 0 || st->segments != x->nseg || st->bytes_in != x->total || x->recs_seen != x->nseg)
+    x->bad++;
+  return 0;
+}
+
 /* after the run: SegmentList hashes = SHA-256 hex of the oracle's segment and fragments */
 static void check_rec(ctx_t* x, sample_t* sm) {
   if (!sm->have_hex) {
@@ -188,6 +210,7 @@ int main(int argc, char** argv) {
   x.uniq = argc > 9 ? strtoull(argv[9], 0, 10) : 16;
   x.check_every = argc > 10 ? strtoull(argv[10], 0, 10) : 7;
   const size_t tail = argc > 11 ? strtoull(argv[11], 0, 10) : 0; /* bytes short of nseg * SB */
+  o.tail_batches = argc > 12 ? atoi(argv[12]) : -1;
   if (x.uniq > x.nseg) x.uniq = x.nseg;
   x.SB = (size_t)x.k * x.F;
   x.total = x.nseg * x.SB - tail;
@@ -202,7 +225,13 @@ int main(int argc, char** argv) {
     return 1;
   }
   cec_pipeline_stats st;
-  int rc = cec_pipeline_run(p, rd, on_frags, o.hash ? on_rec : NULL, &x, &st);
+  int rc;
+  if (o.hash >= CEC_PIPE_HASH_HOST) {
+    cec_source src = {rd, &x, x.total};
+    rc = cec_pipeline_run_files(p, &src, 1, on_frags_f, on_rec_f, on_done_f, &x, &st);
+  } else {
+    rc = cec_pipeline_run(p, rd, on_frags, o.hash ? on_rec : NULL, &x, &st);
+  }
   if (rc) {
     fprintf(stderr, "run: %d %s\n", rc, cec_last_error());
     return 1;
@@ -216,11 +245,12 @@ int main(int argc, char** argv) {
                  st.segments == x.nseg && st.bytes_in == x.total;
   printf("{\"pipeline\": \"%s\", \"k\": %d, \"m\": %d, \"fragment_bytes\": %zu, "
          "\"segments\": %llu, \"batch\": %zu, \"depth\": %d, \"hash\": %d, \"window\": %d, "
+         "\"tail_batches\": %d, "
          "\"bytes_in\": %llu, \"seconds\": %.4f, \"read_seconds\": %.4f, \"wait_seconds\": %.4f, "
          "\"e2e_GBps\": %.3f, \"pcie_gen5_x16_GBps_per_direction\": 63, \"checked\": %llu, "
          "\"bad\": %llu}\n",
          ok ? "ok" : "FAIL", x.k, x.m, x.F, (unsigned long long)st.segments, o.batch_segments,
-         o.depth, o.hash, o.window, (unsigned long long)st.bytes_in, st.seconds, st.read_seconds,
+         o.depth, o.hash, o.window, o.tail_batches, (unsigned long long)st.bytes_in, st.seconds, st.read_seconds,
          st.wait_seconds, st.bytes_in / st.seconds / 1e9, (unsigned long long)x.checked,
          (unsigned long long)x.bad);
   cec_pipeline_destroy(p);

@@ -62,6 +62,8 @@ def ctypes_class(t) -> str:
         return "void"
     if isinstance(t, type) and issubclass(t, ctypes._CFuncPtr):
         return "fn"
+    if t is ctypes.c_double:
+        return "f64"
     if t in (ctypes.c_void_p, ctypes.c_char_p) or (
             isinstance(t, type) and issubclass(t, ctypes._Pointer)):
         return "ptr"

@@ -221,6 +221,40 @@ def test_ct_variants_identical(torch, cess, corc, k, m, ln):
     enc.set_option(2, -1)
 
 
+@pytest.mark.parametrize("data_only", [0, 1])
+def test_mixed21_kargs_variant_leaves_untagged_segments(torch, cess, corc, data_only):
+    """Tuning variant 90 (RS(2,1) mixed-pattern rebuild, erasures in the kernel arguments):
+    segments with nothing to rebuild are not written (they used to get their parity
+    re-encoded, data_only included). Their parity slots hold marker bytes that must survive."""
+    k, m, ln, nseg = 2, 1, (1 << 16) + 48, 9
+    rng = np.random.default_rng(90)
+    data = rng.integers(0, 256, (nseg, k, ln), dtype=np.uint8)
+    par = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = np.ones((nseg, 3), np.uint8)
+    lost = {0: 0, 1: 1, 3: 0, 4: 2, 7: 1}  # segments 2, 5, 6, 8 intact
+    for s, f in lost.items():
+        present[s, f] = 0
+    marker = par.copy()
+    for s in (2, 5, 6, 8):
+        marker[s] = 0xA5  # not the codeword's parity: a write would show
+    d_data = to_dev(torch, data * present[:, :k, None])
+    d_par = to_dev(torch, marker * present[:, k:, None])
+    enc = cess.New(k, m, tuning=True)
+    enc.set_option(2, 90)
+    enc.ReconstructBatch(d_data, d_par, nseg, ln, present, data_only=bool(data_only))
+    torch.cuda.synchronize()
+    enc.set_option(2, -1)
+    assert np.array_equal(d_data.cpu().numpy(), data)
+    got = d_par.cpu().numpy()
+    for s in range(nseg):
+        if s in (2, 5, 6, 8):
+            assert (got[s] == 0xA5).all(), s
+        elif lost[s] == 2:
+            assert np.array_equal(got[s], par[s] if not data_only else 0 * par[s]), s
+        else:
+            assert np.array_equal(got[s], par[s]), s
+
+
 @pytest.mark.parametrize("variant", [70, 72, 73, 74, 75, 76, 77, 78, 83, 85, -1])
 @pytest.mark.parametrize("nseg,ln", [(1, 4096), (3, 16384), (9, 8192)])
 def test_fftdec_d_forms_identical(torch, cess, corc, variant, nseg, ln):

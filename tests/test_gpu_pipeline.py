@@ -32,6 +32,14 @@ def e2e_exe(tmp_path_factory):
     (4, 2, 4160, 33, 5, 3, 1, 3, 33, 1, 0),          # F % 64 == 0: prefix-digest segment chain
     (32, 32, 1000, 20, 4, 2, 1, 1, 20, 1, 999),      # F % 64 != 0, window 1, wide code
     (10, 4, 4096, 7, 64, 3, 1, 16, 7, 1, 0),         # one partial batch
+    # host / hybrid record hashes (cec_pipeline_run_files with the source's size)
+    (2, 1, 1 << 19, 41, 8, 3, 2, 0, 41, 1, 12345),   # host SHA-256, padded tail
+    (2, 1, 1 << 19, 41, 8, 3, 3, 2, 41, 1, 12345, -1),  # hybrid, auto tail
+    (2, 1, 1 << 19, 41, 8, 3, 3, 2, 41, 1, 12345, 0),   # hybrid, GPU takes every fragment
+    (2, 1, 1 << 19, 41, 8, 4, 3, 3, 41, 1, 12345, 2),   # hybrid, last 2 batches on the host
+    (4, 2, 4160, 33, 5, 3, 3, 3, 33, 1, 0, 1),       # hybrid, F % 64 == 0, k = 4
+    (32, 32, 1000, 20, 4, 2, 3, 1, 20, 1, 999, 1),   # hybrid, F % 64 != 0: GPU parity only
+    (10, 4, 4096, 7, 64, 3, 2, 16, 7, 1, 0),         # host, one partial batch
 ])
 def test_pipeline_from_c(e2e_exe, args):
     r = subprocess.run([e2e_exe] + [str(a) for a in args], capture_output=True, text=True,
@@ -41,11 +49,11 @@ def test_pipeline_from_c(e2e_exe, args):
     assert out["pipeline"] == "ok" and out["bad"] == 0 and out["checked"] == args[3]
 
 
-@pytest.mark.parametrize("hash_on", ["gpu", "host", "auto"])
+@pytest.mark.parametrize("hash_on", ["gpu", "host", "hybrid", "auto"])
 def test_pipeline_python_records(orc, hash_on):
-    """encode_file_records on either hash placement (the C pipeline's GPU hash queue, or
-    SegmentEncoder's host SHA-256 beside the GPU encode): the oracle's SegmentLists, file hash
-    and fragments, from bytes, a numpy array and a memoryview."""
+    """encode_file_records on every hash placement of the C pipeline (GPU hash queue, host
+    SHA-256 threads, hybrid): the oracle's SegmentLists, file hash and fragments, from bytes, a
+    numpy array and a memoryview."""
     from cess_amd.pipeline import encode_file_records
     as_array = lambda b: np.frombuffer(b, np.uint8)  # noqa: E731
     for size, seg, k, m, wrap in [(5 * MiB + 7, MiB, 2, 1, bytes),
@@ -68,10 +76,51 @@ def test_pipeline_python_records(orc, hash_on):
 def test_records_host_path_limits():
     import cess_amd
     from cess_amd.pipeline import encode_file_records
-    with pytest.raises(cess_amd.ErrTooManySegments):
-        encode_file_records(bytes(5 * 8192), 2, 1, 8192, max_segments=4, hash_on="host")
-    with pytest.raises(cess_amd.ErrShortData):
-        encode_file_records(b"", 2, 1, 8192, hash_on="host")
+    for hash_on in ("host", "hybrid"):
+        with pytest.raises(cess_amd.ErrTooManySegments):
+            encode_file_records(bytes(5 * 8192), 2, 1, 8192, max_segments=4, hash_on=hash_on)
+        with pytest.raises(cess_amd.ErrShortData):
+            encode_file_records(b"", 2, 1, 8192, hash_on=hash_on)
+
+
+@pytest.mark.parametrize("hash_on,tail,k,m,seg", [
+    ("hybrid", -1, 2, 1, MiB), ("hybrid", 0, 2, 1, MiB), ("hybrid", 2, 2, 1, MiB),
+    ("host", -1, 2, 1, MiB), ("gpu", -1, 2, 1, MiB), ("hybrid", 1, 4, 2, MiB // 2),
+    ("hybrid", 1, 32, 32, 32 * 1000)])
+def test_records_session_many_files(orc, tmp_path, hash_on, tail, k, m, seg):
+    """One RecordsSession (one pipeline) for several files in one run: ragged tails, a file
+    shorter than a segment, a path among in-memory buffers; records and fragments equal the
+    oracle's, on_file in file order; the session then takes another file; an empty file in the
+    list is an error (ErrShortData) and the session stays usable."""
+    import cess_amd
+    from cess_amd.pipeline import RecordsSession
+    sizes = [5 * seg + 7, 3 * seg, seg - 3, 9 * seg + 1]
+    blobs = [np.random.default_rng(100 + i).integers(0, 256, n, dtype=np.uint8).tobytes()
+             for i, n in enumerate(sizes)]
+    path = tmp_path / "f3.bin"
+    path.write_bytes(blobs[3])
+    srcs = blobs[:3] + [str(path)]
+    want = [orc.segment_list(b, k, m, seg) for b in blobs]
+    seen, frags = [], {}
+    with RecordsSession(k, m, seg, hash_on=hash_on, batch_segments=2, window=2,
+                        tail_batches=tail) as ses:
+        recs, st = ses.encode_many(
+            srcs, on_fragment=lambda f, s, i, v: frags.__setitem__(
+                (f, s, i), hashlib.sha256(v).hexdigest().encode()),
+            on_file=lambda f, r, fst: seen.append((f, fst.segments)))
+        assert seen == [(f, len(w)) for f, w in enumerate(want)]
+        assert st.segments == sum(len(w) for w in want) and st.bytes_in == sum(sizes)
+        for f, (r, w) in enumerate(zip(recs, want)):
+            assert [(x.hash, x.fragment_list) for x in r.segments] == w, f
+            assert r.file_hash == orc.file_hash(w) and r.size == sizes[f]
+            for s, sl in enumerate(w):
+                assert [frags[(f, s, i)] for i in range(k + m)] == sl[1]
+        r2, _ = ses.encode(blobs[2])
+        assert [(x.hash, x.fragment_list) for x in r2.segments] == want[2]
+        with pytest.raises(cess_amd.ErrShortData):
+            ses.encode_many([blobs[0], b"", blobs[1]])
+        r3, _ = ses.encode(blobs[1])
+        assert [(x.hash, x.fragment_list) for x in r3.segments] == want[1]
 
 
 def test_pipeline_segment_limit_and_callback_errors():
@@ -107,7 +156,7 @@ def test_cli_encode_streams_fragments_and_scale(tmp_path, orc, hash_on):
                         str(tmp_path / "deal.scale"), "--hash-on", hash_on],
                        capture_output=True, text=True, timeout=300, check=True, cwd=ROOT)
     rec = json.loads(r.stdout)
-    assert rec["pipeline"]["hash_on"] == ("host" if hash_on == "auto" else "gpu")
+    assert rec["pipeline"]["hash_on"] == ("hybrid" if hash_on == "auto" else "gpu")
     want = orc.segment_list(blob, 2, 1, 1 << 20)
     assert [(s["hash"].encode(), [f.encode() for f in s["fragment_list"]])
             for s in rec["segments"]] == want

@@ -85,23 +85,37 @@ def test_python_api_errors_without_gpu():
 
 
 def test_records_hash_placement_arguments():
-    """encode_file_records' hash_on is checked before any device work; the host path needs a
-    source of known size (a stream goes through the C pipeline)."""
+    """encode_file_records' hash_on is checked before any device work; "auto" is the hybrid
+    placement, which the C pipeline refines per batch (cec_pipeline_opts.tail_batches)."""
     import io
     from cess_amd import pipeline
     with pytest.raises(ValueError, match="hash_on"):
         pipeline.encode_file_records(b"x", hash_on="cpu")
-    with pytest.raises(ValueError, match="known size|in-memory"):
-        pipeline.encode_file_records(io.BytesIO(b"x"), hash_on="host")
     assert pipeline._source_size(np.zeros((3, 5), np.uint16)) == 30
     assert pipeline._source_size(memoryview(bytes(7))) == 7
     assert pipeline._source_size(io.BytesIO(b"x")) is None
-    assert pipeline.AUTO_GPU_RECORD_BYTES > 1000 * (16 << 20)  # SegmentCount files: host
     place = pipeline.record_hash_placement
-    assert place("auto", 1 << 30, 2, 1) == "host" and place("auto", 64 << 30, 2, 1) == "gpu"
-    assert place("auto", None, 2, 1) == "gpu"  # a stream of unknown size
-    assert place("auto", 1 << 20, 32, 32) == "gpu"  # 4096 fragments per batch
+    assert place("auto", 1 << 30, 2, 1) == "hybrid" and place("auto", None, 32, 32) == "hybrid"
     assert place("host", 64 << 30, 2, 1) == "host" and place("gpu", 1, 2, 1) == "gpu"
+    with pytest.raises(ValueError):
+        place("tpu")
+
+
+def test_reader_byte_counts(tmp_path):
+    """The pipeline's reader reports each source's size (the hybrid tail placement needs it)."""
+    import io
+    from cess_amd.pipeline import _Reader
+    p = tmp_path / "f"
+    p.write_bytes(bytes(1000))
+    for src, a, b, want in [(str(p), 0, None, 1000), (str(p), 100, 700, 600),
+                            (str(p), 900, 5000, 100), (bytes(50), 10, None, 40),
+                            (np.zeros(8, np.uint16), 0, None, 16), (io.BytesIO(b"x"), 0, None,
+                                                                    None)]:
+        r = _Reader(src, 2, a, b)
+        try:
+            assert r.nbytes == want
+        finally:
+            r.close()
 
 
 def test_join(tmp_path):

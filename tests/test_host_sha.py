@@ -1,0 +1,103 @@
+"""Host SHA-256 of libcessec (cec_sha256_host, cess_amd/csrc/sha256_host.cpp), CPU only: every
+form the CPU has (portable, SHA-NI x1 / x2 / x4, AVX-512 x16) against the reference's NIST SHAVS
+vectors (tests/golden/SHA256{Short,Long}Msg.rsp, from utils/ring/third_party/NIST/SHAVS/) and
+against hashlib at the padding edges, with prefix digests (a segment chain's fragment-0 digest)
+and groups that do not fill a form's width, on one and several threads."""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+from tests.conftest import parse_shavs
+
+FORMS = {"scalar": 0, "ni1": 1, "ni2": 2, "ni4": 3, "x16": 4}
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from cess_amd import _lib
+    return _lib.load()
+
+
+def host_hex(lib, bufs, length, prefix=0, threads=1):
+    n = len(bufs)
+    keep = [np.frombuffer(b, np.uint8) if len(b) else np.zeros(1, np.uint8) for b in bufs]
+    ptrs = (ctypes.c_void_p * max(1, n))(*[k.ctypes.data for k in keep])
+    hexo = np.zeros(64 * max(1, n), np.uint8)
+    phex = np.zeros(64 * max(1, n), np.uint8)
+    rc = lib.cec_sha256_host(ptrs, n, length, hexo.ctypes.data, prefix,
+                             phex.ctypes.data if prefix else None, threads)
+    assert rc == 0
+    out = [bytes(hexo[64 * i:64 * i + 64]).decode() for i in range(n)]
+    pre = [bytes(phex[64 * i:64 * i + 64]).decode() for i in range(n)] if prefix else None
+    return out, pre
+
+
+def forms(lib):
+    out = []
+    for name, f in FORMS.items():
+        if lib.cec_host_sha_set_form(f) == 0:
+            out.append(name)
+    lib.cec_host_sha_set_form(-1)
+    return out
+
+
+def test_shavs_every_form(lib):
+    vecs = parse_shavs("SHA256ShortMsg.rsp") + parse_shavs("SHA256LongMsg.rsp")
+    assert len(vecs) == 129
+    have = forms(lib)
+    assert "scalar" in have
+    try:
+        for name in have:
+            assert lib.cec_host_sha_set_form(FORMS[name]) == 0
+            for msg, md in vecs:
+                # the message as a group of 16 equal chains: every lane / interleave slot
+                got, _ = host_hex(lib, [msg] * 16, len(msg))
+                assert got == [md] * 16, (name, len(msg))
+    finally:
+        lib.cec_host_sha_set_form(-1)
+
+
+@pytest.mark.parametrize("length", [0, 1, 55, 56, 63, 64, 65, 119, 120, 127, 128, 4096 + 13])
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 16, 17, 35])
+def test_lengths_and_groups_vs_hashlib(lib, length, n):
+    rng = np.random.default_rng(length * 131 + n)
+    bufs = [rng.integers(0, 256, length, dtype=np.uint8).tobytes() for _ in range(n)]
+    want = [hashlib.sha256(b).hexdigest() for b in bufs]
+    prefix = 64 if length >= 64 else 0
+    for name in forms(lib):
+        lib.cec_host_sha_set_form(FORMS[name])
+        try:
+            for threads in (1, 3):
+                got, pre = host_hex(lib, bufs, length, prefix, threads)
+                assert got == want, (name, threads)
+                if prefix:
+                    assert pre == [hashlib.sha256(b[:prefix]).hexdigest() for b in bufs]
+        finally:
+            lib.cec_host_sha_set_form(-1)
+
+
+def test_segment_chain_prefix_is_fragment_zero(lib):
+    """The record convention: a segment's chain yields data fragment 0's digest as its prefix
+    (the split is contiguous), as the GPU hash queue's cec_hashq_add_prefix does."""
+    F = 4096 * 3
+    segs = [np.random.default_rng(s).integers(0, 256, 2 * F, dtype=np.uint8).tobytes()
+            for s in range(20)]
+    got, pre = host_hex(lib, segs, 2 * F, F, threads=4)
+    assert got == [hashlib.sha256(s).hexdigest() for s in segs]
+    assert pre == [hashlib.sha256(s[:F]).hexdigest() for s in segs]
+
+
+def test_arguments(lib):
+    buf = np.zeros(128, np.uint8)
+    ptrs = (ctypes.c_void_p * 1)(buf.ctypes.data)
+    hexo = np.zeros(64, np.uint8)
+    assert lib.cec_sha256_host(ptrs, 1, 128, hexo.ctypes.data, 32, hexo.ctypes.data, 1) == -1
+    assert lib.cec_sha256_host(ptrs, 1, 128, hexo.ctypes.data, 192, hexo.ctypes.data, 1) == -1
+    assert lib.cec_sha256_host(ptrs, 1, 128, hexo.ctypes.data, 64, None, 1) == -1
+    assert lib.cec_sha256_host(None, 1, 128, hexo.ctypes.data, 0, None, 1) == -1
+    assert lib.cec_sha256_host(None, 0, 128, None, 0, None, 1) == 0
+    assert lib.cec_host_sha_set_form(99) == -1
+    assert lib.cec_host_sha_probe(99, 1 << 16, 1) < 0
+    assert lib.cec_host_sha_probe(0, 1 << 12, 1) > 0

@@ -175,3 +175,53 @@ def test_cli_encode_then_decode(tmp_path):
         assert cli.main(["decode", str(tmp_path / "rec.json"), str(frag_dir), str(out),
                          "--segment-size", str(seg)]) == 2
     assert "segment 0" in json.loads(buf.getvalue().strip().splitlines()[-1])["error"]
+
+
+def test_cli_decode_tampered_records_and_fragment_names(tmp_path):
+    """`cli decode` answers every records problem with a JSON error and rc 2 (no traceback): a
+    file hash that does not cover the segments, a size the segments cannot hold, a fragment list
+    of the wrong length, unparsable JSON. dir_fetch opens only 64-hex names of regular files, so a
+    crafted record cannot make decode read "../x", an absolute path or a FIFO."""
+    import contextlib
+    import os
+    from cess_amd import cli
+    from cess_amd.retrieve import dir_fetch
+    k, m, seg = 2, 1, 1 << 14
+    blob, rec, frags = _file(3 * seg + 5, k, m, seg)
+    d = tmp_path / "frags"
+    d.mkdir()
+    for (s, f), b in frags.items():
+        (d / rec.segments[s].fragment_list[f].decode()).write_bytes(b)
+    good = rec.to_json()
+
+    def run(obj_or_text):
+        p = tmp_path / "rec.json"
+        p.write_text(obj_or_text if isinstance(obj_or_text, str) else json.dumps(obj_or_text))
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            rc = cli.main(["decode", str(p), str(d), str(tmp_path / "out.bin"), "--segment-size",
+                           str(seg)])
+        return rc, json.loads(buf.getvalue().strip().splitlines()[-1])
+
+    rc, st = run(good)
+    assert rc == 0 and (tmp_path / "out.bin").read_bytes() == blob
+    bad_hash = dict(good, file_hash="0" * 64)
+    bad_size = dict(good, size=100 * seg)
+    short = json.loads(json.dumps(good))
+    short["segments"][1]["fragment_list"] = short["segments"][1]["fragment_list"][:2]
+    for obj, what in [(bad_hash, "ErrRecordsInconsistent"), (bad_size, "ValueError"),
+                      (short, ""), ("{not json", "records")]:
+        rc, st = run(obj)
+        assert rc == 2 and what in st["error"], (what, st)
+    # fragment names from the records
+    fetch = dir_fetch(str(d))
+    h = rec.segments[0].fragment_list[0]
+    assert fetch(0, 0, h) == frags[(0, 0)]
+    (tmp_path / "secret").write_bytes(b"x")
+    for name in (b"../secret", str(tmp_path / "secret").encode(), h.upper(), h[:63], h + b"0"):
+        assert fetch(0, 0, name) is None
+    fifo = d / ("f" * 64)
+    os.mkfifo(fifo)
+    assert fetch(0, 0, b"f" * 64) is None  # not a regular file: no blocking open / read
+    (d / ("e" * 64)).mkdir()
+    assert fetch(0, 0, b"e" * 64) is None

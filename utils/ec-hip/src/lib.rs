@@ -30,7 +30,17 @@ pub struct cec_pipeline_opts {
     pub hash: c_int,
     pub window: c_int,
     pub max_segments: u64,
+    /// host SHA-256 threads for hash = 2 (host) / 3 (hybrid); 0 = 16
+    pub host_threads: c_int,
+    /// hash = 3: batches at the end of the last source hashed wholly on the host (-1 = auto)
+    pub tail_batches: c_int,
 }
+
+/// `cec_pipeline_opts.hash`: where the SegmentList hashes run.
+pub const CEC_PIPE_HASH_NONE: c_int = 0;
+pub const CEC_PIPE_HASH_GPU: c_int = 1;
+pub const CEC_PIPE_HASH_HOST: c_int = 2;
+pub const CEC_PIPE_HASH_HYBRID: c_int = 3;
 
 #[repr(C)]
 #[derive(Clone, Copy, Debug, Default)]
@@ -47,6 +57,23 @@ pub type cec_fragments_fn =
     extern "C" fn(user: *mut c_void, seg: u64, shards: *const *const u8, shard_len: usize) -> c_int;
 pub type cec_record_fn =
     extern "C" fn(user: *mut c_void, seg: u64, seg_hex: *const u8, frag_hex: *const u8) -> c_int;
+pub type cec_file_fragments_fn = extern "C" fn(user: *mut c_void, file: usize, seg: u64,
+                                               shards: *const *const u8, shard_len: usize)
+                                               -> c_int;
+pub type cec_file_record_fn = extern "C" fn(user: *mut c_void, file: usize, seg: u64,
+                                            seg_hex: *const u8, frag_hex: *const u8) -> c_int;
+pub type cec_file_done_fn =
+    extern "C" fn(user: *mut c_void, file: usize, stats: *const cec_pipeline_stats) -> c_int;
+
+/// One source of `cec_pipeline_run_files`: its read callback, that callback's user pointer and
+/// the source's size in bytes (0 = unknown).
+#[repr(C)]
+#[derive(Clone, Copy)]
+pub struct cec_source {
+    pub read: cec_read_fn,
+    pub user: *mut c_void,
+    pub size: u64,
+}
 
 extern "C" {
     pub fn cec_strerror(code: c_int) -> *const c_char;
@@ -65,6 +92,18 @@ extern "C" {
                             on_fragments: Option<cec_fragments_fn>,
                             on_record: Option<cec_record_fn>, user: *mut c_void,
                             stats: *mut cec_pipeline_stats) -> c_int;
+    pub fn cec_pipeline_info(p: *const cec_pipeline, window: *mut c_int,
+                             device_slots: *mut c_int, depth: *mut c_int) -> c_int;
+    pub fn cec_pipeline_run_files(p: *mut cec_pipeline, sources: *const cec_source,
+                                  nsources: usize, on_fragments: Option<cec_file_fragments_fn>,
+                                  on_record: Option<cec_file_record_fn>,
+                                  on_done: Option<cec_file_done_fn>, user: *mut c_void,
+                                  stats: *mut cec_pipeline_stats) -> c_int;
+    pub fn cec_sha256_host(bufs: *const *const u8, n: usize, len: usize, hex: *mut u8,
+                           prefix_len: usize, prefix_hex: *mut u8, threads: c_int) -> c_int;
+    pub fn cec_host_sha_set_form(form: c_int) -> c_int;
+    pub fn cec_host_sha_form() -> c_int;
+    pub fn cec_host_sha_probe(form: c_int, bytes_per_chain: usize, chains: c_int) -> f64;
     pub fn cec_scale_deal_info(seg_hex: *const u8, frag_hex: *const u8, nseg: usize,
                                nfrag: usize, out: *mut u8, out_cap: usize,
                                out_len: *mut usize) -> c_int;
