@@ -22,8 +22,9 @@ its average launch time (HIP events on the launch stream); `cpu_baseline` times 
 The default line also carries, at every N: `extra.config4` (BASELINE config 4's 64 GiB file
 sharded over the N GPUs, T1 on one GPU, efficiency T1 / (N T_N), sampled segments checked against
 the C oracle) and `extra.host_e2e` (an in-memory file per GPU through the C pipeline,
-PCIe-inclusive, with and without SegmentList hashing, the hashes on the GPU or on host
-threads); at N = 1 the one-GPU legs (reconstruct,
+PCIe-inclusive, with and without SegmentList hashing, the hashes on the GPU, on host threads or
+hybrid, plus records_stream: SegmentCount-size files back to back through one session); at N = 1
+the one-GPU legs (reconstruct,
 `extra.wide_code`: RS(32,32) encode / restoral / rebuilds / verify, `extra.config5`: BASELINE
 config 5's encode + SHA-256 step); at N > 1 `extra.degraded_gather` and its wide-code and C-ABI
 forms: the RCCL survivor / partial-product exchange of BASELINE config 4 (fragment f of segment s
@@ -363,6 +364,20 @@ def load_valu_slots(tag: str):
             return json.load(f)
     except (OSError, ValueError):
         return None
+
+
+def load_clock(tag: str, kernel: str):
+    """Shader clock (GHz) under `kernel` from profiles/r06/pmc_<tag>_clock.json (written by
+    tools/pmc_clock.py from a GRBM_GUI_ACTIVE pass), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r06", f"pmc_{tag}_clock.json")) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for name, v in ks.items():
+        if kernel in name:
+            return v.get("clock_GHz")
+    return None
 
 
 def load_traffic(tag: str, algo_bytes: int, kernel: str):
@@ -710,6 +725,13 @@ def config5_leg(dev, local, W: int = 96, warmup: int = 10, sample: int = 48) -> 
             "frac": round(ach / VALU_PEAK_TLANE, 4),
             "issue_slots_per_block": slots["issue_slots_per_block"],
             "basis": "whole step (hash ticks share the chip with the encode); peak at 2.4 GHz"}
+        clk = load_clock("c5", "k_sha256_tick1")
+        if clk:
+            out["sha_roofline"].update({
+                "clock_GHz": clk, "frac_at_clock": round(ach / (VALU_PEAK_TLANE * clk / 2.4), 4),
+                "clock_source": "profiles/r06/pmc_c5_clock.json (GRBM_GUI_ACTIVE / 8 XCDs / "
+                                "duration of the tick dispatches in a rocprofv3 --pmc pass of "
+                                "bench.py --config 5; not measured in this run)"})
     # digests: every batch encodes the same data, so each buffer's hex must be the hashlib digest
     # of the data fragments and of the parity fragments in that buffer
     rng = np.random.default_rng(0xC5)
@@ -863,23 +885,29 @@ def config4_leg(dev, local: int, world: int, rank: int, backend: str, reps: int 
 
 
 def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
-                 gib_per_rank: int = 8) -> dict:
+                 gib_per_rank: int = 8, stream_files: int = 4,
+                 stream_segments: int = 1000, reps: int = 3) -> dict:
     """The host-resident path at every N (PCIe-inclusive; never `value`): every rank streams its
     own synthetic in-memory file (`gib_per_rank` GiB of 16 MiB segments, RS(2,1)) through
     libcessec's C pipeline (cec_pipeline_*: pinned host ring, H2D / encode / D2H on three HIP
-    streams, the north_star's pinned hipMemcpyAsync multi-buffering), once without hashing and
-    once emitting every SegmentList record (segment + fragment SHA-256 on the GPU through the hash
-    queue, c-pallets/file-bank/src/types.rs:13-16), then once more with the same records hashed on
-    16 host SHA-NI threads beside the GPU encode (SegmentEncoder; the placement
-    encode_file_records picks below 20 GiB). Segments are sharded per GPU with no collective.
+    streams, the north_star's pinned hipMemcpyAsync multi-buffering): without hashing, then
+    emitting every SegmentList record (c-pallets/file-bank/src/types.rs:13-16) with the hashes on
+    the GPU hash queue, on 16 host SHA-256 threads (cec_sha256_host: AVX-512 16-lane / SHA-NI
+    multi-chain), and hybrid (segment chains on the host, the other fragments on the GPU queue,
+    the last batches on the host: the placement encode_file_records and the CLI use). Each
+    placement's pipeline is created once and warmed up outside the timed run (a long-lived
+    uploader pins its ring once). records_stream: `stream_files` files of `stream_segments`
+    segments (SegmentCount = 1000, runtime/src/lib.rs:1026: the largest declarable file) back to
+    back through one hybrid session in one run, records per file (each file is the rank's buffer
+    read as pieces, so no second copy is held). Segments are sharded per GPU with no collective.
     Whole-node rate = all ranks' file bytes / the max over ranks of the run time (barrier to
-    barrier). Sampled records are checked afterwards with hashlib and the C oracle, and the
-    host-hashed records against the GPU-hashed ones."""
+    barrier). Sampled records are checked afterwards with hashlib and the C oracle, and every
+    placement's records against the GPU-hashed ones."""
     import hashlib
     import torch
     import torch.distributed as dist
     import cess_amd
-    from cess_amd.pipeline import Pipeline
+    from cess_amd.pipeline import Pipeline, RecordsSession
     k, m, F = 2, 1, 8 * MiB
     seg_bytes = k * F
     nseg = gib_per_rank * (1 << 30) // seg_bytes
@@ -896,7 +924,7 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
         hb[s * seg_bytes:(s + n) * seg_bytes].copy_(d[:n].reshape(-1))
     del d
     torch.cuda.synchronize(dev)
-    enc = cess_amd.New(k, m, device=local)
+    torch.cuda.empty_cache()
 
     def barrier():
         if world > 1:
@@ -909,50 +937,91 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t[0])
 
+    def rate(t, n_bytes=nseg * seg_bytes):
+        return {"node_GBps": round(world * n_bytes / t / GB, 2),
+                "per_gpu_GBps": round(n_bytes / t / GB, 2)}
+
     out = {"workload": f"{gib_per_rank} GiB in-memory file per GPU ({nseg} x 16 MiB segments, "
                        f"RS(2,1)) through the C pipeline (cec_pipeline: 3 pinned 1 GiB host "
                        f"batches, H2D / encode / D2H streams)",
            "file_bytes_per_gpu": nseg * seg_bytes, "n_gpus": world,
            "basis": "file bytes of all ranks / max over ranks of the run (barrier to barrier); "
-                    "PCIe Gen5 x16 = 63 GB/s per direction per GPU"}
+                    "PCIe Gen5 x16 = 63 GB/s per direction per GPU; pipelines created and warmed "
+                    "up before the timed runs; seconds = the median of `runs_s`"}
+    def timed_runs(run):
+        """`reps` timed runs, each barrier to barrier and max over ranks; (median s, all s,
+        last result)."""
+        ts, res = [], None
+        for _ in range(reps):
+            barrier()
+            t0 = time.perf_counter()
+            res = run()
+            ts.append(reduce_max(time.perf_counter() - t0))
+        return sorted(ts)[len(ts) // 2], [round(t, 4) for t in ts], res
+
     recs = {}
+    enc = cess_amd.New(k, m, device=local)
     for name, hashing in (("no_hash", False), ("segment_lists", True)):
         with Pipeline(enc, F, batch_segments=64, depth=3, hash=hashing, window=32) as p:
             p.run(buf[:64 * seg_bytes])  # warm-up: pinned ring, device slots, hash queue
-            barrier()
-            t0 = time.perf_counter()
             on_rec = (lambda s, sh, fl: recs.__setitem__(s, (sh, fl))) if hashing else None
-            st = p.run(buf, on_record=on_rec)
-            t = time.perf_counter() - t0
-            barrier()
-        t = reduce_max(t)
-        out[name] = {"seconds": round(t, 4), "segments": int(st.segments),
-                     "node_GBps": round(world * nseg * seg_bytes / t / GB, 2),
-                     "per_gpu_GBps": round(nseg * seg_bytes / t / GB, 2)}
+            t, runs, st = timed_runs(lambda: p.run(buf, on_record=on_rec))
+        out[name] = {"seconds": round(t, 4), "runs_s": runs, "segments": int(st.segments),
+                     **rate(t)}
+        if hashing:
+            out[name]["hash_on"] = "gpu"
     enc.close()
-    # the same records with the hashes on host SHA-NI threads beside the GPU encode (SegmentEncoder,
-    # what encode_file_records(hash_on="auto") picks below 20 GiB); records must equal the GPU's
-    from cess_amd.segments import SegmentEncoder
-    se = SegmentEncoder(k, m, seg_bytes, batch_segments=64, device=local, hash_on="host",
-                        hash_threads=16)
-    try:
-        se.encode_file(buf[:64 * seg_bytes])  # warm-up: pinned batches, thread pools
-        barrier()
-        t0 = time.perf_counter()
-        hrec = se.encode_file(buf)
-        t = time.perf_counter() - t0
-        barrier()
-    finally:
-        se.close()
-    t = reduce_max(t)
-    host_same = len(hrec.segments) == nseg and all(
-        (hrec.segments[s].hash, list(hrec.segments[s].fragment_list)) ==
-        (recs[s][0], list(recs[s][1])) for s in range(nseg) if s in recs)
-    out["segment_lists_host_sha"] = {
-        "seconds": round(t, 4), "segments": len(hrec.segments), "hash_threads": 16,
-        "node_GBps": round(world * nseg * seg_bytes / t / GB, 2),
-        "per_gpu_GBps": round(nseg * seg_bytes / t / GB, 2),
-        "records_equal_gpu_hashed": bool(not reduce_max(0.0 if host_same else 1.0))}
+
+    def same(rec) -> bool:
+        return len(rec.segments) == nseg and all(
+            (rec.segments[s].hash, list(rec.segments[s].fragment_list)) ==
+            (recs[s][0], list(recs[s][1])) for s in range(nseg) if s in recs)
+
+    # the same records hashed on host threads and hybrid (long-lived sessions)
+    lib = cess_amd._lib.load()
+    for name, mode in (("segment_lists_host_sha", "host"), ("segment_lists_hybrid", "hybrid")):
+        with RecordsSession(k, m, seg_bytes, local, mode, batch_segments=64, depth=3,
+                            host_threads=16) as ses:
+            ses.encode(buf[:64 * seg_bytes])  # warm-up
+            t, runs, (rec, st) = timed_runs(lambda: ses.encode(buf))
+            info = ses.pipe.info()
+            leg = {"seconds": round(t, 4), "runs_s": runs, "segments": len(rec.segments),
+                   "hash_threads": 16,
+                   "host_sha_form": {0: "scalar", 1: "sha-ni x1", 2: "sha-ni x2",
+                                     3: "sha-ni x4", 4: "avx-512 x16"}.get(
+                                         lib.cec_host_sha_form(), "?"),
+                   "window": info["window"], "depth": info["depth"]}
+            leg["records_equal_gpu_hashed"] = bool(not reduce_max(0.0 if same(rec) else 1.0))
+            if mode == "hybrid" and stream_files:
+                # records_stream: SegmentCount-size files back to back in one run
+                per = stream_segments * seg_bytes
+                pieces, left = [], per
+                while left:
+                    take = min(left, buf.size)
+                    pieces.append(buf[:take])
+                    left -= take
+                done_t = []
+                barrier()
+                t1 = time.perf_counter()
+                srecs, sst = ses.encode_many([pieces] * stream_files, on_file=lambda f, r, fs:
+                                             done_t.append(time.perf_counter() - t1))
+                ts = time.perf_counter() - t1
+                barrier()
+                sok = all(len(r.segments) == stream_segments for r in srecs)
+                for r in srecs:  # segment s of a stream file is buffer segment s % nseg
+                    for s in sorted({0, nseg - 1, nseg, stream_segments - 1}):
+                        want = recs.get(s % nseg)
+                        sok &= want is not None and (r.segments[s].hash, list(
+                            r.segments[s].fragment_list)) == (want[0], list(want[1]))
+                tsm = reduce_max(ts)
+                out["records_stream"] = {
+                    "files": stream_files, "segments_per_file": stream_segments,
+                    "file_bytes": per, "seconds": round(tsm, 4),
+                    "file_done_s": [round(x, 3) for x in done_t], **rate(tsm, stream_files * per),
+                    "records_per_file": True, "hash_on": "hybrid",
+                    "records_equal_gpu_hashed_sampled": bool(not reduce_max(0.0 if sok else 1.0))}
+        leg.update(rate(t))
+        out[name] = leg
     # checker: sampled records against hashlib over the file bytes and the C oracle's parity
     from oracle.c_oracle import load_c_oracle
     orc = load_c_oracle()
@@ -1021,9 +1090,12 @@ def line_problems(out: dict) -> list:
     e2e = ex.get("host_e2e")
     if e2e is not None and not e2e.get("records_match_hashlib_and_oracle"):
         bad.append("extra.host_e2e records unchecked or wrong")
-    if e2e is not None and "segment_lists_host_sha" in e2e and not e2e[
-            "segment_lists_host_sha"].get("records_equal_gpu_hashed"):
-        bad.append("extra.host_e2e host-hashed records differ from the GPU-hashed ones")
+    for leg in ("segment_lists_host_sha", "segment_lists_hybrid"):
+        if e2e is not None and leg in e2e and not e2e[leg].get("records_equal_gpu_hashed"):
+            bad.append(f"extra.host_e2e.{leg} records differ from the GPU-hashed ones")
+    if e2e is not None and "error" not in e2e and not (e2e.get("records_stream") or {}).get(
+            "records_equal_gpu_hashed_sampled"):
+        bad.append("extra.host_e2e.records_stream missing or its records wrong")
     if n == 1:
         c5 = ex.get("config5") or {}
         if not c5.get("digests_match_hashlib") or not c5.get("step_GBps"):

@@ -28,7 +28,9 @@ struct Job {
 struct JobState {
   Job job;
   int form = 0;
-  std::atomic<int> left{0};
+  size_t next = 0;      // next chain to hand out (under the pool's lock)
+  size_t per_task = 1;  // groups per task (forms other than x16)
+  std::atomic<int> left{0};  // chains (x16) or tasks not yet finished
   std::mutex mu;
   std::condition_variable cv;
   bool done = false;
@@ -39,7 +41,7 @@ void hash_range(const Job& j, size_t c0, size_t n, int form);
 // valid until it is ready.
 std::shared_ptr<JobState> submit(const Job& job, int threads);
 bool ready(const std::shared_ptr<JobState>& js);
-// Block until the job is done; with help, the caller runs queued tasks meanwhile.
+// Block until the job is done (the second argument is unused: the workers do all hashing).
 void wait(const std::shared_ptr<JobState>& js, bool help);
 
 }  // namespace hsha

@@ -278,8 +278,9 @@ std::atomic<int> g_form{-1};
 int best_form() {
   int f = g_form.load(std::memory_order_relaxed);
   if (f >= 0) return f;
-  // default before (or without) a probe: SHA-NI two chains per core where present
-  return has_ni() ? CEC_HSHA_NI2 : (has_x16() ? CEC_HSHA_X16 : CEC_HSHA_SCALAR);
+  // the default: 16 chains per core in AVX-512 lanes where present (5.5 GB/s per core on the
+  // EPYC 9575F against 3.6 for SHA-NI x2, profiles/r06/host_sha_probe.jsonl), else SHA-NI x2
+  return has_x16() ? CEC_HSHA_X16 : (has_ni() ? CEC_HSHA_NI2 : CEC_HSHA_SCALAR);
 }
 
 bool form_supported(int form) {
@@ -369,18 +370,107 @@ void hash_range(const Job& j, size_t c0, size_t n, int form) {
 }
 
 // ---- the worker pool ---------------------------------------------------------------------------
+// Jobs queue in submission order. A job of the x16 form is handed out chain by chain: a worker
+// keeps up to 16 chains in the lanes of its zmm registers and refills a lane as soon as its
+// chain ends (the multi-buffer scheme), so the lanes stay full across the different lengths of
+// one batch's chains (16 MiB segments, 8 MiB fragments) and across jobs. With fewer chains than
+// that in its lanes a worker advances them on SHA-NI two at a time instead (x16 on n lanes does
+// n/16 of its work; SHA-NI x2 beats it below ~11 lanes, by the per-thread rates of
+// profiles/r06/host_sha_probe.jsonl), and chains are shared out among idle workers. Jobs of the
+// other forms are handed out as tasks of whole groups.
 namespace {
 
-struct Task {
+constexpr int kLanes = 16;
+constexpr uint64_t kStepBlocks = 1024;  // lanes are refilled at least every 64 KiB per lane
+constexpr int kMinX16Lanes = 11;
+alignas(64) const uint8_t kZeros[kStepBlocks * 64] = {};
+
+void one_lane_blocks(uint32_t* st, const uint8_t* p, size_t nblk) {
+  uint32_t* s1[1] = {st};
+  const uint8_t* p1[1] = {p};
+  blocks(has_ni() ? CEC_HSHA_NI1 : CEC_HSHA_SCALAR, s1, p1, 1, nblk);
+}
+
+void chain_done(const std::shared_ptr<JobState>& js) {
+  if (js->left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+    std::lock_guard<std::mutex> l(js->mu);
+    js->done = true;
+    js->cv.notify_all();
+  }
+}
+
+struct Lane {
   std::shared_ptr<JobState> js;
-  size_t c0, n;
+  size_t ci = 0;
+  const uint8_t* p = nullptr;
+  uint64_t done = 0, full = 0, pre = 0;  // blocks hashed, full blocks, prefix blocks (0: none)
+  bool pre_done = true;
+  uint32_t st[8];
+
+  void start(std::shared_ptr<JobState> j, size_t c) {
+    js = std::move(j);
+    ci = c;
+    p = js->job.bufs[c];
+    done = 0;
+    full = js->job.len / 64;
+    pre = js->job.prefix_len / 64;
+    pre_done = pre == 0;
+    std::memcpy(st, IV, sizeof IV);
+  }
+  uint64_t to_event() const { return (pre_done ? full : pre) - done; }
+  // the prefix digest: a copy of the state finished with the prefix's padding block
+  void prefix() {
+    const Job& j = js->job;
+    uint32_t c[8];
+    std::memcpy(c, st, sizeof c);
+    uint8_t pad[128];
+    pad_blocks(nullptr, j.prefix_len, pad);
+    one_lane_blocks(c, pad, 1);
+    to_hex(c, j.prefix_hex + (ci / j.per * j.prefix_outer + ci % j.per) * 64);
+    pre_done = true;
+  }
+  void finish() {
+    const Job& j = js->job;
+    uint8_t pad[128];
+    const int nb = pad_blocks(j.bufs[ci] + full * 64, j.len, pad);
+    one_lane_blocks(st, pad, (size_t)nb);
+    to_hex(st, j.hex + (ci / j.per * j.hex_outer + ci % j.per) * 64);
+    chain_done(js);
+    js.reset();
+  }
 };
+
+// Advance the n active lanes by `step` blocks (step <= each lane's blocks to its next event).
+void step_lanes(Lane* L, int n, uint64_t step) {
+  if (!step) return;
+  uint32_t* st[kLanes];
+  const uint8_t* p[kLanes];
+  if (n >= kMinX16Lanes && has_x16()) {
+    uint32_t dummy[kLanes][8];
+    for (int i = 0; i < kLanes; ++i) {
+      st[i] = i < n ? L[i].st : dummy[i];
+      p[i] = i < n ? L[i].p : kZeros;
+    }
+    x16_blocks(st, p, step);
+  } else {
+    for (int i = 0; i < n; ++i) {
+      st[i] = L[i].st;
+      p[i] = L[i].p;
+    }
+    blocks(CEC_HSHA_NI2, st, p, n, step);
+  }
+  for (int i = 0; i < n; ++i) {
+    L[i].done += step;
+    L[i].p += step * 64;
+  }
+}
 
 struct Pool {
   std::mutex mu;
   std::condition_variable cv;
-  std::deque<Task> q;
+  std::deque<std::shared_ptr<JobState>> q;  // jobs with chains / tasks not yet handed out
   std::vector<std::thread> th;
+  int idle = 0;
   bool stop = false;
 
   ~Pool() {
@@ -395,38 +485,83 @@ struct Pool {
     std::lock_guard<std::mutex> l(mu);
     while ((int)th.size() < n) th.emplace_back([this] { loop(); });
   }
+
+  // (under mu) chains of x16 jobs into free lanes: at most a fair share when workers are idle
+  void take_chains(Lane* L, int& n) {
+    size_t avail = 0;
+    for (auto& js : q)
+      if (js->form == CEC_HSHA_X16) avail += js->job.n - js->next;
+    if (!avail) return;
+    size_t want = (size_t)(kLanes - n);
+    if (idle > 0) want = std::min(want, std::max<size_t>(1, (avail + idle) / (idle + 1)));
+    for (auto it = q.begin(); it != q.end() && want;) {
+      auto& js = *it;
+      if (js->form != CEC_HSHA_X16) {
+        ++it;
+        continue;
+      }
+      while (want && js->next < js->job.n) {
+        L[n++].start(js, js->next++);
+        --want;
+      }
+      if (js->next == js->job.n)
+        it = q.erase(it);
+      else
+        ++it;
+    }
+  }
+  // (under mu) a task of groups from the oldest job of another form
+  bool take_task(std::shared_ptr<JobState>& js, size_t& c0, size_t& cn) {
+    for (auto it = q.begin(); it != q.end(); ++it) {
+      if ((*it)->form == CEC_HSHA_X16) continue;
+      js = *it;
+      const size_t W = (size_t)form_width(js->form);
+      c0 = js->next;
+      cn = std::min(js->job.n - c0, js->per_task * W);
+      js->next += cn;
+      if (js->next == js->job.n) q.erase(it);
+      return true;
+    }
+    return false;
+  }
+
   void loop() {
+    Lane L[kLanes];
+    int n = 0;
     while (true) {
-      Task t;
+      std::shared_ptr<JobState> tjs;
+      size_t t0 = 0, tn = 0;
       {
         std::unique_lock<std::mutex> l(mu);
-        cv.wait(l, [&] { return stop || !q.empty(); });
-        if (stop && q.empty()) return;
-        t = std::move(q.front());
-        q.pop_front();
+        while (true) {
+          if (n < kLanes) take_chains(L, n);
+          if (n) break;
+          if (take_task(tjs, t0, tn)) break;
+          if (stop) return;
+          ++idle;
+          cv.wait(l);
+          --idle;
+        }
       }
-      run(t);
+      if (tjs) {
+        hash_range(tjs->job, t0, tn, tjs->form);
+        // tasks count as one unit each in `left`
+        chain_done(tjs);
+        continue;
+      }
+      uint64_t step = kStepBlocks;
+      for (int i = 0; i < n; ++i) step = std::min(step, L[i].to_event());
+      step_lanes(L, n, step);
+      for (int i = 0; i < n; ++i) {
+        if (!L[i].pre_done && L[i].done == L[i].pre) L[i].prefix();
+        if (L[i].pre_done && L[i].done == L[i].full) {
+          L[i].finish();
+          if (i != n - 1) std::swap(L[i], L[n - 1]);
+          --n;
+          --i;
+        }
+      }
     }
-  }
-  static void run(const Task& t) {
-    hash_range(t.js->job, t.c0, t.n, t.js->form);
-    if (t.js->left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
-      std::lock_guard<std::mutex> l(t.js->mu);
-      t.js->done = true;
-      t.js->cv.notify_all();
-    }
-  }
-  // one task from the queue on the calling thread (a waiter helps instead of sleeping)
-  bool help() {
-    Task t;
-    {
-      std::lock_guard<std::mutex> l(mu);
-      if (q.empty()) return false;
-      t = std::move(q.front());
-      q.pop_front();
-    }
-    run(t);
-    return true;
   }
 };
 
@@ -441,27 +576,25 @@ std::shared_ptr<JobState> submit(const Job& job, int threads) {
   auto js = std::make_shared<JobState>();
   js->job = job;
   js->form = best_form();
-  const size_t W = (size_t)form_width(js->form);
-  const size_t groups = (job.n + W - 1) / W;
-  if (!groups) {
+  if (!job.n) {
     js->done = true;
     return js;
   }
   threads = std::max(1, threads);
+  if (js->form == CEC_HSHA_X16) {
+    js->left.store((int)job.n);  // one unit per chain
+  } else {
+    // tasks of whole groups; a few per thread so a slow core does not hold the job
+    const size_t W = (size_t)form_width(js->form);
+    const size_t groups = (job.n + W - 1) / W;
+    js->per_task = std::max<size_t>(1, groups / ((size_t)threads * 2));
+    js->left.store((int)((groups + js->per_task - 1) / js->per_task));
+  }
   Pool& P = pool();
   P.grow(threads);
-  // tasks of whole groups; a few per thread so a slow core does not hold the job
-  const size_t per_task = std::max<size_t>(1, groups / ((size_t)threads * 2));
-  std::vector<Task> tasks;
-  for (size_t g = 0; g < groups; g += per_task) {
-    const size_t c0 = g * W;
-    const size_t n = std::min(job.n, (g + per_task) * W) - c0;
-    tasks.push_back(Task{js, c0, n});
-  }
-  js->left.store((int)tasks.size());
   {
     std::lock_guard<std::mutex> l(P.mu);
-    for (auto& t : tasks) P.q.push_back(std::move(t));
+    P.q.push_back(js);
   }
   P.cv.notify_all();
   return js;
@@ -471,10 +604,7 @@ bool ready(const std::shared_ptr<JobState>& js) {
   return js->left.load(std::memory_order_acquire) == 0 || js->done;
 }
 
-void wait(const std::shared_ptr<JobState>& js, bool help) {
-  if (help)
-    while (!ready(js) && pool().help()) {
-    }
+void wait(const std::shared_ptr<JobState>& js, bool) {
   std::unique_lock<std::mutex> l(js->mu);
   js->cv.wait(l, [&] { return js->done; });
 }

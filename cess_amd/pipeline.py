@@ -23,16 +23,22 @@ from .reedsolomon import CecError, Encoder, check
 Source = Union[str, bytes, bytearray, memoryview, np.ndarray, BinaryIO]
 
 
+def _as_u8(x) -> np.ndarray:
+    return x.reshape(-1).view(np.uint8) if isinstance(x, np.ndarray) else np.frombuffer(x,
+                                                                                      np.uint8)
+
+
 class _Reader:
     """read() callback over a path (parallel os.preadv, GIL released), an in-memory buffer
-    (parallel numpy copies) or a binary stream (readinto)."""
+    (parallel numpy copies), a list of in-memory buffers read back to back as one file (pieces
+    gathered from elsewhere, no joined copy) or a binary stream (readinto)."""
 
     def __init__(self, src: Source, threads: int = 8, start: int = 0,
                  stop: Optional[int] = None, pool: Optional[cf.ThreadPoolExecutor] = None):
         self.own_pool = pool is None
         self.pool = pool or cf.ThreadPoolExecutor(max_workers=threads)
         self.threads = threads
-        self.fd = self.arr = self.stream = None
+        self.fd = self.arr = self.stream = self.parts = None
         self.pos = 0
         if isinstance(src, str):
             self.fd = os.open(src, os.O_RDONLY)
@@ -41,10 +47,13 @@ class _Reader:
             if stop is not None:
                 self.size = min(self.size, stop)
         elif isinstance(src, (bytes, bytearray, memoryview, np.ndarray)):
-            arr = (src.reshape(-1).view(np.uint8) if isinstance(src, np.ndarray)
-                   else np.frombuffer(src, np.uint8))
-            self.arr = arr[start:stop]
+            self.arr = _as_u8(src)[start:stop]
             self.size = self.arr.size
+        elif isinstance(src, (list, tuple)):
+            if start or stop is not None:
+                raise ValueError("a byte range needs a path or a single in-memory buffer")
+            self.parts = [_as_u8(x) for x in src]
+            self.size = sum(x.size for x in self.parts)
         else:
             if start or stop is not None:
                 raise ValueError("a byte range needs a path or an in-memory source")
@@ -71,7 +80,22 @@ class _Reader:
             return 0
         step = max(4 << 20, -(-n // self.threads))
         futs = []
-        for a in range(0, n, step):
+        if self.parts is not None:  # copy runs of the pieces that cover [pos, pos + n)
+            off, done = self.pos, 0
+            for x in self.parts:
+                if off >= x.size:
+                    off -= x.size
+                    continue
+                take = min(x.size - off, n - done)
+                for a in range(0, take, step):
+                    e = min(take, a + step)
+                    futs.append(self.pool.submit(np.copyto, np.frombuffer(
+                        mv[done + a:done + e], np.uint8), x[off + a:off + e]))
+                done += take
+                off = 0
+                if done == n:
+                    break
+        for a in range(0, n if self.parts is None else 0, step):
             e = min(n, a + step)
             if self.arr is not None:
                 futs.append(self.pool.submit(np.copyto, np.frombuffer(mv[a:e], np.uint8),
@@ -329,6 +353,8 @@ def _source_size(src: Source) -> Optional[int]:
         return src.nbytes
     if isinstance(src, (bytes, bytearray)):
         return len(src)
+    if isinstance(src, (list, tuple)):  # in-memory pieces read back to back
+        return sum(_source_size(x) for x in src)
     return None  # a stream
 
 

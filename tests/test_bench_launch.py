@@ -108,17 +108,24 @@ def test_line_keys_config4():
 
 def test_line_keys_host_e2e():
     """The host-resident leg's records: the GPU-hashed ones checked against hashlib and the C
-    oracle, the host-hashed ones equal to the GPU-hashed ones."""
+    oracle, the host-hashed and hybrid ones equal to the GPU-hashed ones, and the records_stream
+    leg (SegmentCount-size files back to back) present with its sampled records right."""
     ok = {"records_match_hashlib_and_oracle": True,
-          "segment_lists_host_sha": {"records_equal_gpu_hashed": True}}
+          "segment_lists_host_sha": {"records_equal_gpu_hashed": True},
+          "segment_lists_hybrid": {"records_equal_gpu_hashed": True},
+          "records_stream": {"records_equal_gpu_hashed_sampled": True}}
     assert not any("host_e2e" in p for p in bench.line_problems(
         _line(1, extra={"config4": C4, "host_e2e": ok})))
-    differ = dict(ok, segment_lists_host_sha={"records_equal_gpu_hashed": False})
-    assert "extra.host_e2e host-hashed records differ from the GPU-hashed ones" in \
-        bench.line_problems(_line(1, extra={"config4": C4, "host_e2e": differ}))
+    for leg in ("segment_lists_host_sha", "segment_lists_hybrid"):
+        differ = dict(ok, **{leg: {"records_equal_gpu_hashed": False}})
+        assert f"extra.host_e2e.{leg} records differ from the GPU-hashed ones" in \
+            bench.line_problems(_line(1, extra={"config4": C4, "host_e2e": differ}))
     unchecked = dict(ok, records_match_hashlib_and_oracle=False)
     assert "extra.host_e2e records unchecked or wrong" in bench.line_problems(
         _line(1, extra={"config4": C4, "host_e2e": unchecked}))
+    no_stream = {k: v for k, v in ok.items() if k != "records_stream"}
+    assert "extra.host_e2e.records_stream missing or its records wrong" in bench.line_problems(
+        _line(1, extra={"config4": C4, "host_e2e": no_stream}))
 
 
 def test_line_keys_multi_gpu():
@@ -160,6 +167,10 @@ def test_line_keys_one_gpu():
     assert bench.line_problems(_line(1, extra=cold_less)) == ["wide_code.encode lacks its cold mean"]
 
 
+# problems line_problems() reports for lines recorded before round 6 added the leg
+R06_NEW = {"extra.host_e2e.records_stream missing or its records wrong"}
+
+
 @pytest.mark.parametrize("name", ["bench_default_b.json", "bench_default_c.json",
                                   "bench_default_e.json", "bench_default_g.json",
                                   "bench_default_h.json", "bench_default_i.json", "bench_default_j.json",
@@ -168,14 +179,14 @@ def test_line_keys_one_gpu():
                                   "bench_gpus2_gloo_one_gpu_b.json",
                                   "bench_gpus4_gloo_one_gpu_b.json"])
 def test_recorded_lines_have_every_key(name):
-    """The lines this round's GPU runs printed (profiles/r05/): the N = 1 default line and the
+    """The lines round 5's GPU runs printed (profiles/r05/): the N = 1 default line and the
     one-GPU rehearsals of the N = 2 and N = 4 lines (gloo ranks sharing GPU 0) carry everything
-    line_problems() asks for."""
+    line_problems() asks for, except the legs round 6 added (R06_NEW)."""
     import json
     path = os.path.join(ROOT, "profiles", "r05", name)
     with open(path) as f:
         line = json.load(f)
-    assert bench.line_problems(line) == []
+    assert [p for p in bench.line_problems(line) if p not in R06_NEW] == []
     if line["n_gpus"] > 1:
         ex = line["extra"]
         assert ex["degraded_gather"]["bit_exact"] and ex["degraded_gather"]["backend"] == "gloo"

@@ -444,3 +444,26 @@ def test_host_code_under_sanitizers(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     assert "sanitize host ok" in r.stdout
+
+
+def test_reader_pieces():
+    """A file given as several in-memory pieces is read back to back (no joined copy), across
+    piece boundaries at any read size."""
+    from cess_amd.pipeline import _Reader, _source_size
+    rng = np.random.default_rng(4)
+    parts = [rng.integers(0, 256, n, dtype=np.uint8) for n in (5 << 20, 1, 3 << 20, 777)]
+    want = np.concatenate(parts)
+    assert _source_size(parts) == want.size
+    for cap in (1 << 20, 5 << 20, (5 << 20) + 1, 123457):
+        r = _Reader(parts, 3)
+        assert r.nbytes == want.size
+        out, tmp = [], np.zeros(cap, np.uint8)
+        try:
+            while True:
+                n = r(tmp.ctypes.data, cap)
+                if not n:
+                    break
+                out.append(tmp[:n].copy())
+        finally:
+            r.close()
+        assert np.array_equal(np.concatenate(out), want)

@@ -101,3 +101,34 @@ def test_arguments(lib):
     assert lib.cec_host_sha_set_form(99) == -1
     assert lib.cec_host_sha_probe(99, 1 << 16, 1) < 0
     assert lib.cec_host_sha_probe(0, 1 << 12, 1) > 0
+
+
+def test_concurrent_jobs_share_the_lanes(lib):
+    """Jobs of different lengths (with and without prefix digests) submitted at once from several
+    threads: the pool's workers mix their chains in one register's lanes and refill a lane as its
+    chain ends; every digest still equals hashlib's."""
+    import concurrent.futures as cf
+    rng = np.random.default_rng(11)
+    jobs = []
+    for j, (n, length, prefix) in enumerate([(37, 64 * 300, 64 * 100), (5, 64 * 1000 + 7, 0),
+                                             (23, 64 * 50, 64 * 50), (64, 119, 0),
+                                             (16, 64 * 777, 64), (3, 0, 0)]):
+        bufs = [rng.integers(0, 256, length, dtype=np.uint8).tobytes() for _ in range(n)]
+        jobs.append((bufs, length, prefix))
+
+    def run(job):
+        bufs, length, prefix = job
+        got, pre = host_hex(lib, bufs, length, prefix, threads=8)
+        ok = got == [hashlib.sha256(b).hexdigest() for b in bufs]
+        if prefix:
+            ok = ok and pre == [hashlib.sha256(b[:prefix]).hexdigest() for b in bufs]
+        return ok
+
+    for name in forms(lib):
+        lib.cec_host_sha_set_form(FORMS[name])
+        try:
+            with cf.ThreadPoolExecutor(len(jobs)) as ex:
+                for _ in range(3):
+                    assert all(ex.map(run, jobs)), name
+        finally:
+            lib.cec_host_sha_set_form(-1)
