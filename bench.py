@@ -46,6 +46,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+T_START = time.perf_counter()  # the process's start (extra.resources wall times)
 MiB = 1 << 20
 GB = 1e9
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
@@ -364,6 +365,37 @@ def load_valu_slots(tag: str):
             return json.load(f)
     except (OSError, ValueError):
         return None
+
+
+# per-rank resource marks the legs record (extra.resources: the N = 8 line's footprint)
+RES = {}
+
+
+def hbm_used_gib(dev) -> float:
+    import torch
+    free, total = torch.cuda.mem_get_info(dev)
+    return round((total - free) / 2**30, 2)
+
+
+def resources(dev, world: int, rank: int, t_start: float) -> dict:
+    """Every rank's peak host RSS, peak torch HBM, the HBM marks the legs recorded and its wall
+    time so far, gathered to rank 0 (None elsewhere)."""
+    import resource
+    import torch
+    import torch.distributed as dist
+    mine = dict(RES, rank=rank, wall_s=round(time.perf_counter() - t_start, 1),
+                peak_rss_GiB=round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 2),
+                torch_peak_reserved_GiB=round(torch.cuda.max_memory_reserved(dev) / 2**30, 2),
+                hbm_used_now_GiB=hbm_used_gib(dev))
+    if world == 1:
+        return {"ranks": [mine]}
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    if rank != 0:
+        return None
+    return {"ranks": got, "note": "hbm_used_* = the whole device's used HBM (mem_get_info) at "
+                                  "that point; ranks sharing one GPU (CESS_DEVICE rehearsal) all "
+                                  "see the same device"}
 
 
 def load_clock(tag: str, kernel: str):
@@ -826,6 +858,8 @@ def config4_leg(dev, local: int, world: int, rank: int, backend: str, reps: int 
             barrier()
         host_ms = (time.perf_counter() - t0) * 1e3 / reps
         ev_ms = a.elapsed_time(b) / reps
+        RES["hbm_used_after_t1_GiB" if timed_alone else "hbm_used_after_shards_GiB"] = \
+            hbm_used_gib(dev)
         rows = sorted({0, 1, nseg // 3, nseg // 2, (2 * nseg) // 3, nseg - 2, nseg - 1} &
                       set(range(nseg)))
         ok = oracle_sample_check(d_data, d_par, rows, seg0, k, m, F, seed)
@@ -959,10 +993,17 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
             ts.append(reduce_max(time.perf_counter() - t0))
         return sorted(ts)[len(ts) // 2], [round(t, 4) for t in ts], res
 
+    # ranks sharing one GPU (the CESS_DEVICE rehearsal) split its HBM: the hash windows shrink
+    # with the world (every pipeline also fits its window to free HBM when it is created)
+    shared = "CESS_DEVICE" in os.environ and world > 1
+    gpu_window = max(2, 32 // world) if shared else 32
+    hybrid_window = max(2, 16 // world) if shared else 0
+    if shared:
+        out["shared_gpu_windows"] = {"gpu": gpu_window, "hybrid": hybrid_window}
     recs = {}
     enc = cess_amd.New(k, m, device=local)
     for name, hashing in (("no_hash", False), ("segment_lists", True)):
-        with Pipeline(enc, F, batch_segments=64, depth=3, hash=hashing, window=32) as p:
+        with Pipeline(enc, F, batch_segments=64, depth=3, hash=hashing, window=gpu_window) as p:
             p.run(buf[:64 * seg_bytes])  # warm-up: pinned ring, device slots, hash queue
             on_rec = (lambda s, sh, fl: recs.__setitem__(s, (sh, fl))) if hashing else None
             t, runs, st = timed_runs(lambda: p.run(buf, on_record=on_rec))
@@ -981,7 +1022,7 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
     lib = cess_amd._lib.load()
     for name, mode in (("segment_lists_host_sha", "host"), ("segment_lists_hybrid", "hybrid")):
         with RecordsSession(k, m, seg_bytes, local, mode, batch_segments=64, depth=3,
-                            host_threads=16) as ses:
+                            host_threads=16, window=hybrid_window) as ses:
             ses.encode(buf[:64 * seg_bytes])  # warm-up
             t, runs, (rec, st) = timed_runs(lambda: ses.encode(buf))
             info = ses.pipe.info()
@@ -1039,6 +1080,7 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
     bad = reduce_max(0.0 if ok else 1.0)
     out["records_match_hashlib_and_oracle"] = not bad
     out["records_checked_per_gpu"] = 3
+    RES["hbm_used_in_host_e2e_GiB"] = hbm_used_gib(dev)
     del buf
     return out
 
@@ -1631,6 +1673,11 @@ def main() -> None:
             # baseline beside it (OpenSSL SHA-256, SHA-NI where the host has it)
             wk, wm, wF = CONFIGS[5][:3]
             out["cpu_baseline"]["sha256"] = cpu_sha256(wk, wm, wF, args.cpu_seconds / 2)
+
+    if not args.no_extra and args.config == 2:
+        res = resources(dev, world, rank, T_START)
+        if rank == 0:
+            out.setdefault("extra", {})["resources"] = res
 
     if cabi_pending:
         cabi_legs(out["extra"], gather_leg, degraded_gather, enc, (k, m, F), world, rank, dev,

@@ -194,6 +194,26 @@ def test_recorded_lines_have_every_key(name):
         assert "RCCL refuses" in ex["degraded_gather_cabi"]["skipped"]
 
 
+@pytest.mark.parametrize("name", ["bench_gpus8_gloo_one_gpu.json"])
+def test_recorded_round6_lines(name):
+    """Round 6's recorded lines (profiles/r06/): the one-GPU rehearsal of the N = 8 default line
+    (8 gloo ranks sharing GPU 0) carries every key line_problems() asks for,
+    the host_e2e records_stream leg included, and its per-rank footprint (extra.resources: peak
+    host RSS, HBM after config 4's T1 and shards) for all 8 ranks; its wall time (bench start to
+    exit, beside it) is well inside the driver's 600 s."""
+    import json
+    with open(os.path.join(ROOT, "profiles", "r06", name)) as f:
+        line = json.load(f)
+    assert line["n_gpus"] == 8 and bench.line_problems(line) == []
+    res = line["extra"]["resources"]["ranks"]
+    assert sorted(r["rank"] for r in res) == list(range(8))
+    assert all(r["peak_rss_GiB"] > 0 and "hbm_used_after_shards_GiB" in r for r in res)
+    assert "hbm_used_after_t1_GiB" in res[0]
+    with open(os.path.join(ROOT, "profiles", "r06", name.replace(".json", "_wall.json"))) as f:
+        wall = json.load(f)
+    assert wall["rc"] == 0 and wall["wall_s"] < 300
+
+
 def test_cabi_legs_watchdog_ends_a_stalled_exchange(tmp_path):
     """bench.cabi_legs (the C-ABI exchange legs of the N > 1 line, run last): an exchange that
     never returns (a peer stuck in RCCL) does not cost the line. Past the deadline the legs are
