@@ -33,7 +33,7 @@ from . import geometry
 def _placement(args) -> str:
     """Where the record hashes ran: "gpu", "host" or "hybrid"."""
     from .pipeline import record_hash_placement
-    return "gpu" if args.devices else record_hash_placement(args.hash_on)
+    return record_hash_placement(args.hash_on)
 
 
 def _report(args, rec, st) -> dict:
@@ -73,7 +73,7 @@ def _encode(args) -> int:
             devs = [int(x) for x in args.devices.split(",")]
             rec, sts = encode_file_records_multi(args.file[0], devs, args.k, args.m,
                                                  args.segment_size, max_segments=limit,
-                                                 window=args.window)
+                                                 hash_on=args.hash_on, window=args.window)
             st = sts[0]
             st.seconds = max(x.seconds for x in sts)
             st.read_seconds = max(x.read_seconds for x in sts)

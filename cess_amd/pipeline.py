@@ -403,15 +403,19 @@ def encode_file_records_multi(src: Union[str, bytes, bytearray, memoryview, np.n
                               devices, k: int = geometry.DATA_SHARDS,
                               m: int = geometry.PARITY_SHARDS,
                               segment_size: int = geometry.SEGMENT_SIZE,
-                              max_segments: int = 0, read_threads: int = 8, **kw):
+                              max_segments: int = 0, read_threads: int = 8,
+                              hash_on: str = "auto", hash_threads: int = 16, **kw):
     """File -> FileRecord with the segments sharded over several GPUs from ONE host process (an
     uploader on a multi-GPU node): contiguous segment ranges per device
-    (distributed.shard_range; segments are independent, no data exchange), one C pipeline per
-    device on its own host thread (pinned multi-buffered copies per GPU), records merged in
-    segment order. `devices` may repeat a device (several pipelines sharing one GPU).
-    Returns (FileRecord, [PipelineStats per device])."""
+    (distributed.shard_range; segments are independent, no data exchange), one RecordsSession
+    (C pipeline) per device on its own host thread, records merged in segment order. `devices`
+    may repeat a device (several pipelines sharing one GPU). hash_on as in encode_file_records;
+    each pipeline hashes on its own `hash_threads` host threads (the GPU's CPU share) and takes
+    its own HBM: window + 3 device batch slots of up to 1.5 GiB (a CESS batch of 64 segments;
+    batch_segments shrinks for small shards), fitted to the free HBM when it is created, so
+    pipelines sharing a GPU split what is left. Returns (FileRecord, [PipelineStats per device])."""
     from .distributed import shard_range
-    from .segments import FileRecord, SegmentList, file_hash
+    from .segments import FileRecord, file_hash
     size = os.path.getsize(src) if isinstance(src, str) else (
         src.nbytes if isinstance(src, np.ndarray) else len(src))
     if size == 0:
@@ -422,29 +426,26 @@ def encode_file_records_multi(src: Union[str, bytes, bytearray, memoryview, np.n
         from .records import ErrTooManySegments
         raise ErrTooManySegments(ErrTooManySegments.__doc__)
     devices = list(devices)
+    mode = record_hash_placement(hash_on)
     kw.setdefault("batch_segments", max(1, min(64, -(-nseg // len(devices)))))
 
     def work(i):
         a, b = shard_range(nseg, len(devices), i)
         if b <= a:
-            return {}, None
-        recs = {}
-        enc = Encoder(k, m, devices[i])
-        try:
-            with Pipeline(enc, segment_size // k, **kw) as p:
-                st = p.run(src, on_record=lambda s, sh, fl: recs.__setitem__(
-                    a + s, SegmentList(sh, fl)), read_threads=read_threads,
-                    start=a * segment_size, stop=min(size, b * segment_size))
-        finally:
-            enc.close()
-        return recs, st
+            return [], None
+        with RecordsSession(k, m, segment_size, devices[i], mode, host_threads=hash_threads,
+                            read_threads=read_threads, **kw) as ses:
+            rng = (a * segment_size, min(size, b * segment_size))
+            recs = {}
+            st = ses.pipe.run_files([src], None, lambda _f, s, sh, fl: recs.__setitem__(
+                s, (sh, fl)), None, read_threads, [rng])
+        from .segments import SegmentList
+        return [SegmentList(*recs[s]) for s in range(b - a)], st
 
     with cf.ThreadPoolExecutor(max_workers=len(devices)) as ex:
         parts = list(ex.map(work, range(len(devices))))
-    recs = {}
-    for r, _ in parts:
-        recs.update(r)
-    out = FileRecord(b"", size, [recs[s] for s in range(nseg)])
+    segs = [sl for p, _ in parts for sl in p]
+    out = FileRecord(b"", size, segs)
     out.file_hash = file_hash(out.segments)
     return out, [st for _, st in parts if st is not None]
 

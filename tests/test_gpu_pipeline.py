@@ -217,7 +217,8 @@ def test_library_first_then_torch():
 @pytest.mark.parametrize("devices,size,seg,k,m", [([0, 0, 0], 7 * MiB + 5, MiB, 2, 1),
                                                   ([0, 0], 3 * MiB, MiB // 2, 4, 2),
                                                   ([0, 0, 0, 0, 0], 2 * MiB, MiB, 2, 1)])
-def test_multi_device_file_records(orc, tmp_path, devices, size, seg, k, m):
+@pytest.mark.parametrize("hash_on", ["auto", "gpu", "host"])
+def test_multi_device_file_records(orc, tmp_path, devices, size, seg, k, m, hash_on):
     """One host process sharding a file's segments over several pipelines (here several on GPU 0,
     as an uploader on an 8-GPU node would use 8 devices): the merged records equal the oracle's,
     from an in-memory buffer and from a path; more devices than segments leaves some idle."""
@@ -227,7 +228,8 @@ def test_multi_device_file_records(orc, tmp_path, devices, size, seg, k, m):
     path = tmp_path / "f.bin"
     path.write_bytes(blob)
     for src in (blob, str(path)):
-        rec, stats = encode_file_records_multi(src, devices, k, m, seg, window=2)
+        rec, stats = encode_file_records_multi(src, devices, k, m, seg, window=2,
+                                               hash_on=hash_on)
         assert [(s.hash, s.fragment_list) for s in rec.segments] == want
         assert rec.file_hash == orc.file_hash(want) and rec.size == size
         assert sum(st.segments for st in stats) == len(want)
