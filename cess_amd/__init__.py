@@ -21,12 +21,13 @@ from .reedsolomon import (
     New,
     fill_synthetic,
     sha256_hex_device,
+    sha256_hex_host,
     xor_batch,
 )
 
 __all__ = [
     "geometry", "CecError", "Encoder", "New", "ErrInvShardNum", "ErrMaxShardNum",
     "ErrReconstructRequired", "ErrShardNoData", "ErrShardSize", "ErrShortData",
-    "ErrTooFewShards", "HipError", "fill_synthetic", "sha256_hex_device", "HashQueue",
-    "sha256_blocks", "records", "ErrTooManySegments", "audit", "xor_batch",
+    "ErrTooFewShards", "HipError", "fill_synthetic", "sha256_hex_device", "sha256_hex_host",
+    "HashQueue", "sha256_blocks", "records", "ErrTooManySegments", "audit", "xor_batch",
 ]

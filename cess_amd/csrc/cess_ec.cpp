@@ -1158,7 +1158,7 @@ int cec_set_option(cec_codec* c, int option, int value) {
       c->opts.ct_variant = value == 0 && cec::max_ct_variant() == 0 ? -1 : value;
       return CEC_OK;
     case CEC_OPT_SHA_MODE:
-      if (value < 0 || value > 2) return set_err(CEC_EINVAL, "sha mode out of range");
+      if (value < 0 || value > 3) return set_err(CEC_EINVAL, "sha mode out of range");
       c->opts.sha_mode = value;
       return CEC_OK;
     case CEC_OPT_RT_MODE:

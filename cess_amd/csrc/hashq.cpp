@@ -188,7 +188,7 @@ int cec_hashq_status(const cec_hashq* q, uint64_t ticket, int* done, size_t* liv
 int cec_hashq_set_option(cec_hashq* q, int option, int value) {
   if (!q) return cec::set_error(CEC_EINVAL, "null");
   if (option == CEC_HQOPT_TICK) {
-    if (value < 0 || value > 3) return cec::set_error(CEC_EINVAL, "tick kernel must be 0..3");
+    if (value < 0 || value > 4) return cec::set_error(CEC_EINVAL, "tick kernel must be 0..4");
     q->tick_mode = value;
     return CEC_OK;
   }

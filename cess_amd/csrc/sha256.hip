@@ -175,8 +175,9 @@ __device__ __forceinline__ const uint8_t* sha_src(const uint8_t* const* ptrs, co
   return ptrs ? ptrs[i] : shard_ptr(L, (int)(i % nshards), (uint32_t)(i / nshards));
 }
 
+template <int QS = 64>
 __device__ __forceinline__ void sha_expand_store(uint32_t (&w)[16], u32x4* __restrict__ dst) {
-  // dst[q * 64] = {W+K}[4q .. 4q+3] for this lane
+  // dst[q * QS] = {W+K}[4q .. 4q+3] for this lane
 #pragma unroll
   for (int t = 0; t < 64; t += 4) {
     uint32_t o[4];
@@ -195,17 +196,102 @@ __device__ __forceinline__ void sha_expand_store(uint32_t (&w)[16], u32x4* __res
       }
       o[s] = wt + kSha256K[u];
     }
-    dst[(t / 4) * 64] = u32x4{o[0], o[1], o[2], o[3]};
+    dst[(t / 4) * QS] = u32x4{o[0], o[1], o[2], o[3]};
   }
 }
 
-__global__ __launch_bounds__(128) void k_sha256_2w(const uint8_t* const* __restrict__ ptrs,
+__device__ __forceinline__ void sha_store_hex(uint8_t* __restrict__ o, const uint32_t (&h)[8]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t word = h[q];
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const uint32_t nib = (word >> (28 - 4 * s)) & 15u;
+      const uint32_t chr = nib < 10 ? '0' + nib : 'a' + nib - 10;
+      if (s < 4) lo |= chr << (8 * s);
+      else hi |= chr << (8 * (s - 4));
+    }
+    *reinterpret_cast<uint32_t*>(o + 8 * q) = lo;
+    *reinterpret_cast<uint32_t*>(o + 8 * q + 4) = hi;
+  }
+}
+
+// Lane-pair rounds (the latency form of the two-wave kernels, k_sha256_lp and k_sha256_tick_lp):
+// a chain's 64 rounds on TWO lanes of a consumer wave. The even lane carries (e, f, g, h) and
+// computes T1 = h + Sigma1(e) + Ch(e, f, g) + K + W, the odd lane carries (a, b, c, d) and computes
+// T2 = Sigma0(a) + Maj(a, b, c), with the same instructions: the rotate amounts sit in VGPRs
+// (v_alignbit takes its shift per lane), Maj(a, b, c) = Ch(a ^ c, b, c) makes Maj a Ch of the
+// lane's own history, and the odd lane reads zeros where the even lane reads K + W. One DPP
+// quad_perm [1,0,3,2] exchange per round: the even lane sends T1, the odd lane d, and each adds
+// what it receives (even: e = d + T1, odd: a = T2 + T1). 11 VALU instructions (16 issue slots)
+// per round on the pair against 14 (22) on one lane: a lone wave's block drops from 3660 to 3204
+// s_memtime ticks (tools/sha_latency.hip, profiles/r06/sha_latency_forms.jsonl). A pair spends
+// two lanes per chain, so these are the kernels of the latency regime only (few chains).
+__device__ __forceinline__ uint32_t sha_swap_pair(uint32_t v) {  // lane l ^ 1
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+}
+
+struct ShaLp {
+  uint32_t r1, r2, r3, M;
+  bool even;
+};
+
+__device__ __forceinline__ ShaLp sha_lp(bool even) {
+  // even: Sigma1 rotates, odd: Sigma0 rotates and the Maj operand mask (a ^ c)
+  return ShaLp{even ? 6u : 2u, even ? 11u : 13u, even ? 25u : 22u, even ? 0u : ~0u, even};
+}
+
+// One block: src[q * QS] = K + W of rounds 4q .. 4q + 3 (zeros on the odd lane); the pair's
+// halves (X0..X3: e, f, g, h on the even lane, a, b, c, d on the odd lane) advance in place.
+template <int QS>
+__device__ __forceinline__ void sha_lp_block(const u32x4* __restrict__ src, const ShaLp& L,
+                                             uint32_t& X0, uint32_t& X1, uint32_t& X2,
+                                             uint32_t& X3) {
+  uint32_t x0 = X0, x1 = X1, x2 = X2, x3 = X3;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const u32x4 kw4 = src[q * QS];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const uint32_t kw = s4 == 0 ? kw4.x : s4 == 1 ? kw4.y : s4 == 2 ? kw4.z : kw4.w;
+      const uint32_t S = xor3(__builtin_amdgcn_alignbit(x0, x0, L.r1),
+                              __builtin_amdgcn_alignbit(x0, x0, L.r2),
+                              __builtin_amdgcn_alignbit(x0, x0, L.r3));
+      const uint32_t P = __builtin_amdgcn_bitop3_b32(x0, x2, L.M, 0x78);  // x0 ^ (x2 & M)
+      const uint32_t CM = ch(P, x1, x2);          // even: Ch(e, f, g); odd: Maj(a, b, c)
+      const uint32_t HK = (L.even ? x3 : 0u) + kw;  // even: h + K + W; odd: 0
+      const uint32_t V = S + CM + HK;             // even: T1; odd: T2
+      const uint32_t U = L.even ? V : x3;         // what the partner needs: T1 / d
+      const uint32_t xn = V + sha_swap_pair(U);   // even: e = d + T1; odd: a = T2 + T1
+      x3 = x2; x2 = x1; x1 = x0; x0 = xn;
+    }
+  }
+  X0 += x0; X1 += x1; X2 += x2; X3 += x3;
+}
+
+// The whole state (a..h) from a pair's halves, on the even lane (both lanes must execute it).
+__device__ __forceinline__ void sha_lp_full(uint32_t (&h)[8], uint32_t X0, uint32_t X1,
+                                            uint32_t X2, uint32_t X3) {
+  h[0] = sha_swap_pair(X0);
+  h[1] = sha_swap_pair(X1);
+  h[2] = sha_swap_pair(X2);
+  h[3] = sha_swap_pair(X3);
+  h[4] = X0; h[5] = X1; h[6] = X2; h[7] = X3;
+}
+
+// LP: two consumer waves on lane pairs (sha_lp_block) instead of one on single lanes; ring
+// column 64 holds the odd lanes' zeros.
+template <bool LP>
+__global__ __launch_bounds__(LP ? 192 : 128) void k_sha256_2w(const uint8_t* const* __restrict__ ptrs,
                                                    Layout L, int nshards, uint64_t n,
                                                    uint64_t len, uint8_t* __restrict__ hex_out) {
-  __shared__ u32x4 ring[2][16][64];
+  constexpr int QS = LP ? 65 : 64;
+  __shared__ u32x4 ring[2][16][QS];
   const int lane = threadIdx.x & 63;
   // wave-uniform by construction (SGPR), so the two sides' barriers never run under one EXEC mask
-  const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool producer = wave == 0;
   const uint64_t i = (uint64_t)blockIdx.x * 64 + lane;
   const bool live = i < n;
   const uint64_t nfull = len >> 6;
@@ -268,10 +354,28 @@ __global__ __launch_bounds__(128) void k_sha256_2w(const uint8_t* const* __restr
           w[15] = (uint32_t)bits;
         }
       }
-      sha_expand_store(w, &ring[blk & 1][0][lane]);
+      sha_expand_store<QS>(w, &ring[blk & 1][0][lane]);
       __syncthreads();
     }
     __syncthreads();  // matches the consumer's final iteration
+  } else if constexpr (LP) {
+    // lane pair p = lane / 2 of consumer wave 1 or 2 hashes buffer 32 (wave - 1) + p
+    const int c = 32 * (wave - 1) + (lane >> 1);
+    const bool even = (lane & 1) == 0;
+    if (lane < 32) ring[lane >> 4][lane & 15][64] = u32x4{0, 0, 0, 0};  // the zero column
+    const uint64_t ic = (uint64_t)blockIdx.x * 64 + c;
+    const ShaLp lp = sha_lp(even);
+    const int col = even ? c : 64;
+    uint32_t X0 = even ? 0x510e527fu : 0x6a09e667u, X1 = even ? 0x9b05688cu : 0xbb67ae85u,
+             X2 = even ? 0x1f83d9abu : 0x3c6ef372u, X3 = even ? 0x5be0cd19u : 0xa54ff53au;
+    __syncthreads();  // block 0 produced (and the zero column written)
+    for (uint64_t blk = 0; blk < nb; ++blk) {
+      sha_lp_block<QS>(&ring[blk & 1][0][col], lp, X0, X1, X2, X3);
+      __syncthreads();  // this buffer consumed / next one produced
+    }
+    uint32_t h[8];
+    sha_lp_full(h, X0, X1, X2, X3);
+    if (ic < n && even) sha_store_hex(hex_out + ic * 64, h);
   } else {
     uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                      0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
@@ -323,23 +427,6 @@ __global__ __launch_bounds__(128) void k_sha256_2w(const uint8_t* const* __restr
 // tens of thousands of chains at once, where one batch alone (4096 fragments of a 1 GiB
 // RS(32,32) batch; 192 of a 1 GiB RS(2,1) batch) fills a few percent of its SIMDs. Same
 // two-wave structure as k_sha256_2w; chains of one wave may be at different blocks.
-__device__ __forceinline__ void sha_store_hex(uint8_t* __restrict__ o, const uint32_t (&h)[8]) {
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const uint32_t word = h[q];
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const uint32_t nib = (word >> (28 - 4 * s)) & 15u;
-      const uint32_t chr = nib < 10 ? '0' + nib : 'a' + nib - 10;
-      if (s < 4) lo |= chr << (8 * s);
-      else hi |= chr << (8 * (s - 4));
-    }
-    *reinterpret_cast<uint32_t*>(o + 8 * q) = lo;
-    *reinterpret_cast<uint32_t*>(o + 8 * q + 4) = hi;
-  }
-}
-
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
@@ -426,6 +513,77 @@ __device__ __noinline__ void sha_prefix_hex(uint32_t h0, uint32_t h1, uint32_t h
   sha_prefix_hex_inl(h, blocks, hex);
 }
 
+// The producer wave of the latency-form ticks: loads, byte-swaps and expands every block of its
+// 64 chains into the LDS ring ([buf][word/4][QS columns] u32x4, column = lane), one barrier per
+// block, `trips` barriers in all (the consumers' count).
+template <int PF, int QS>
+__device__ __forceinline__ void sha_tick_produce(u32x4* __restrict__ ring, int lane,
+                                                 const ShaChain* ch_, bool live, uint64_t blk0,
+                                                 uint64_t nfull, uint32_t r, uint64_t nb,
+                                                 uint64_t len, uint32_t nblk, uint32_t trips) {
+  const uint8_t* src = live ? ch_->src : nullptr;
+  const bool al16 = live && ((uintptr_t)src & 15) == 0;
+  // Fast phase: blocks every lane of the wave has as aligned message data (the bulk of a
+  // tick), one wave-uniform loop with the next block's loads in flight. General phase: the
+  // rest (padding blocks, unaligned buffers, lanes that are done), loaded directly.
+  const uint64_t dat = blk0 < nfull ? nfull - blk0 : 0;
+  const uint32_t mine = al16 ? (uint32_t)(dat < nblk ? dat : nblk) : 0u;
+  const uint32_t nfast = __builtin_amdgcn_readfirstlane(wave_min_u32(live ? mine : ~0u));
+  // lanes past n take no part in nfast; their loads are masked off
+  // nx[j] holds block b + j: PF blocks of loads in flight ahead of the one being expanded
+  u32x4 nx[PF][4] = {};
+#pragma unroll
+  for (int j = 0; j < PF; ++j)
+    if ((uint32_t)j < nfast && live) {
+      const uint8_t* p = src + ((blk0 + j) << 6);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nx[j][q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+    }
+  auto slot = [&](uint32_t blk) CEC_SHA_AI { return ring + (blk & 1) * 16 * QS + lane; };
+  auto expand = [&](u32x4 (&v)[4], uint32_t blk) CEC_SHA_AI {
+    uint32_t w[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      w[4 * q + 0] = __builtin_bswap32(v[q].x);
+      w[4 * q + 1] = __builtin_bswap32(v[q].y);
+      w[4 * q + 2] = __builtin_bswap32(v[q].z);
+      w[4 * q + 3] = __builtin_bswap32(v[q].w);
+    }
+    const uint32_t nb_next = blk + PF;
+    if (nb_next < nfast && live) {
+      const uint8_t* p = src + ((blk0 + nb_next) << 6);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+    }
+    sha_expand_store<QS>(w, slot(blk));
+    __syncthreads();
+  };
+  uint32_t b = 0;
+  for (; b + PF <= nfast; b += PF) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) expand(nx[j], b + j);
+  }
+#pragma unroll
+  for (int j = 0; j < PF; ++j)
+    if (b < nfast) {
+      expand(nx[j], b);
+      ++b;
+    }
+  for (; b < trips; ++b) {
+    uint32_t w[16];
+    if (b < nblk) {
+      // staged in the ring buffer this block is about to be written to (consumed at b - 2)
+      sha_block_general(w, src, blk0 + b, nfull, r, nb, len, slot(b), QS);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) w[q] = 0;
+    }
+    sha_expand_store<QS>(w, slot(b));
+    __syncthreads();
+  }
+  __syncthreads();  // matches the consumers' final iteration
+}
+
 template <int PF>
 __global__ __launch_bounds__(128) void k_sha256_tick(ShaChain* __restrict__ tab, uint32_t mask,
                                                      uint64_t head, uint32_t n,
@@ -450,66 +608,8 @@ __global__ __launch_bounds__(128) void k_sha256_tick(ShaChain* __restrict__ tab,
   const uint32_t trips = wave_max_u32(nblk);
   if (trips == 0) return;
   if (producer) {
-    const uint8_t* src = live ? ch_->src : nullptr;
-    const bool al16 = live && ((uintptr_t)src & 15) == 0;
-    // Fast phase: blocks every lane of the wave has as aligned message data (the bulk of a
-    // tick), one wave-uniform loop with the next block's loads in flight. General phase: the
-    // rest (padding blocks, unaligned buffers, lanes that are done), loaded directly.
-    const uint64_t dat = blk0 < nfull ? nfull - blk0 : 0;
-    const uint32_t mine = al16 ? (uint32_t)(dat < nblk ? dat : nblk) : 0u;
-    const uint32_t nfast = __builtin_amdgcn_readfirstlane(wave_min_u32(live ? mine : ~0u));
-    // lanes past n take no part in nfast; their loads are masked off
-    // nx[j] holds block b + j: PF blocks of loads in flight ahead of the one being expanded
-    u32x4 nx[PF][4] = {};
-#pragma unroll
-    for (int j = 0; j < PF; ++j)
-      if ((uint32_t)j < nfast && live) {
-        const uint8_t* p = src + ((blk0 + j) << 6);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) nx[j][q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
-      }
-    auto expand = [&](u32x4 (&v)[4], uint32_t blk) CEC_SHA_AI {
-      uint32_t w[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        w[4 * q + 0] = __builtin_bswap32(v[q].x);
-        w[4 * q + 1] = __builtin_bswap32(v[q].y);
-        w[4 * q + 2] = __builtin_bswap32(v[q].z);
-        w[4 * q + 3] = __builtin_bswap32(v[q].w);
-      }
-      const uint32_t nb_next = blk + PF;
-      if (nb_next < nfast && live) {
-        const uint8_t* p = src + ((blk0 + nb_next) << 6);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
-      }
-      sha_expand_store(w, &ring[blk & 1][0][lane]);
-      __syncthreads();
-    };
-    uint32_t b = 0;
-    for (; b + PF <= nfast; b += PF) {
-#pragma unroll
-      for (int j = 0; j < PF; ++j) expand(nx[j], b + j);
-    }
-#pragma unroll
-    for (int j = 0; j < PF; ++j)
-      if (b < nfast) {
-        expand(nx[j], b);
-        ++b;
-      }
-    for (; b < trips; ++b) {
-      uint32_t w[16];
-      if (b < nblk) {
-        // staged in the ring buffer this block is about to be written to (consumed at b - 2)
-        sha_block_general(w, src, blk0 + b, nfull, r, nb, len, &ring[b & 1][0][lane], 64);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) w[q] = 0;
-      }
-      sha_expand_store(w, &ring[b & 1][0][lane]);
-      __syncthreads();
-    }
-    __syncthreads();  // matches the consumer's final iteration
+    sha_tick_produce<PF, 64>(&ring[0][0][0], lane, ch_, live, blk0, nfull, r, nb, len, nblk,
+                             trips);
   } else {
     uint32_t h[8] = {};
     uint64_t pre = 0;  // block count after which the prefix digest is due (0: none)
@@ -548,6 +648,93 @@ __global__ __launch_bounds__(128) void k_sha256_tick(ShaChain* __restrict__ tab,
       for (int q = 0; q < 8; ++q) ch_->h[q] = h[q];
       ch_->blk = blk0 + nblk;
       if (blk0 + nblk == nb && ch_->hex) sha_store_hex(ch_->hex, h);
+    }
+  }
+}
+
+// Lane-pair tick (the latency regime: few chains, so a chain's time is one wave's issue rate per
+// block). The producer wave expands the schedules of 64 chains as in k_sha256_tick; two consumer
+// waves run the rounds on lane pairs (sha_lp_block). Three waves per 64 chains: the launcher picks
+// it while the live chains leave the SIMDs idle.
+template <int PF>
+__global__ __launch_bounds__(192) void k_sha256_tick_lp(ShaChain* __restrict__ tab, uint32_t mask,
+                                                        uint64_t head, uint32_t n,
+                                                        uint32_t max_blocks) {
+  constexpr int QS = 65;  // column 64: zeros, the odd lanes' K + W
+  __shared__ u32x4 ring[2][16][QS];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // every wave computes the trip count over the group's 64 chains (lane = chain), so all three
+  // agree on the number of barriers
+  const uint32_t i = blockIdx.x * 64 + lane;
+  const bool live = i < n;
+  ShaChain* ch_ = &tab[(uint32_t)(head + i) & mask];
+  uint64_t len = 0, blk0 = 0;
+  if (live) {
+    len = ch_->len;
+    blk0 = ch_->blk;
+  }
+  const uint64_t nfull = len >> 6;
+  const uint32_t r = (uint32_t)(len & 63);
+  const uint64_t nb = nfull + (r >= 56 ? 2 : 1);
+  const uint64_t rem = live ? nb - blk0 : 0;
+  const uint32_t nblk = rem < max_blocks ? (uint32_t)rem : max_blocks;
+  const uint32_t trips = wave_max_u32(nblk);
+  if (trips == 0) return;
+  if (wave == 0) {
+    sha_tick_produce<PF, QS>(&ring[0][0][0], lane, ch_, live, blk0, nfull, r, nb, len, nblk,
+                             trips);
+    return;
+  }
+  // consumer wave 1 or 2: lane pair p = lane / 2 runs chain c = 32 (wave - 1) + p
+  const int c = 32 * (wave - 1) + (lane >> 1);
+  const bool even = (lane & 1) == 0;
+  if (lane < 32) ring[lane >> 4][lane & 15][64] = u32x4{0, 0, 0, 0};  // the zero column
+  const uint32_t ic = blockIdx.x * 64 + c;
+  const bool livec = ic < n;
+  ShaChain* cc = &tab[(uint32_t)(head + ic) & mask];
+  uint64_t lenc = 0, b0 = 0, pre = 0;
+  uint32_t X0 = 0, X1 = 0, X2 = 0, X3 = 0;
+  if (livec) {
+    lenc = cc->len;
+    b0 = cc->blk;
+    pre = cc->pre_blk;
+    const int o = even ? 4 : 0;
+    X0 = cc->h[o];
+    X1 = cc->h[o + 1];
+    X2 = cc->h[o + 2];
+    X3 = cc->h[o + 3];
+  }
+  const uint64_t nbc = (lenc >> 6) + ((lenc & 63) >= 56 ? 2 : 1);
+  const uint64_t remc = livec ? nbc - b0 : 0;
+  const uint32_t nblkc = remc < max_blocks ? (uint32_t)remc : max_blocks;
+  const ShaLp lp = sha_lp(even);
+  const int col = even ? c : 64;
+  auto full = [&](uint32_t (&h)[8]) CEC_SHA_AI { sha_lp_full(h, X0, X1, X2, X3); };
+  __syncthreads();  // block 0 produced (and the zero column written)
+  for (uint32_t b = 0; b < trips; ++b) {
+    if (b < nblkc) {
+      sha_lp_block<QS>(&ring[b & 1][0][col], lp, X0, X1, X2, X3);
+      if (b0 + b + 1 == pre) {  // both lanes of the pair: the exchange needs the partner
+        uint32_t h[8];
+        full(h);
+        if (even) sha_prefix_hex(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], pre, cc->pre_hex);
+      }
+    }
+    __syncthreads();  // this buffer consumed / next one produced
+  }
+  if (livec && nblkc) {
+    const int o = even ? 4 : 0;
+    cc->h[o] = X0;
+    cc->h[o + 1] = X1;
+    cc->h[o + 2] = X2;
+    cc->h[o + 3] = X3;
+    const bool last = b0 + nblkc == nbc && cc->hex;
+    uint32_t h[8];
+    full(h);
+    if (even) {
+      cc->blk = b0 + nblkc;
+      if (last) sha_store_hex(cc->hex, h);
     }
   }
 }
@@ -672,10 +859,14 @@ void launch_sha256_hex(int sha_mode, const uint8_t* const* ptrs, const Layout* L
   const unsigned g = (unsigned)((n + 63) / 64);
   // Two waves per group while the groups leave SIMDs idle (latency regime: one serial chain
   // per buffer); one wave per group once 2 * groups would exceed the chip's 1024 SIMDs.
-  const bool two = sha_mode == 2 || (sha_mode != 1 && g <= 512);
-  if (two)
-    hipLaunchKernelGGL(k_sha256_2w, dim3(g), dim3(128), 0, st, ptrs, L ? *L : dummy, nshards, n,
-                       len, hex_out);
+  // The lane-pair form (three waves per group) while those still fit one per SIMD.
+  const int v = sha_mode >= 1 && sha_mode <= 3 ? sha_mode : (g <= 341 ? 3 : g <= 512 ? 2 : 1);
+  if (v == 3)
+    hipLaunchKernelGGL(k_sha256_2w<true>, dim3(g), dim3(192), 0, st, ptrs, L ? *L : dummy,
+                       nshards, n, len, hex_out);
+  else if (v == 2)
+    hipLaunchKernelGGL(k_sha256_2w<false>, dim3(g), dim3(128), 0, st, ptrs, L ? *L : dummy,
+                       nshards, n, len, hex_out);
   else
     hipLaunchKernelGGL(k_sha256, dim3(g), dim3(64), 0, st, ptrs, L ? *L : dummy, nshards, n, len,
                        hex_out);
@@ -691,14 +882,24 @@ void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
                      pre_hex_outer);
 }
 
+// live chains below which the auto tick is the lane-pair form (three waves per 64 chains): at
+// 32,768 chains it still hashes 823 GB/s against the two-wave tick's 693, at 65,536 783 against
+// 1,366 (tools/sha_scale.py, profiles/r06/sha_scale_lp.jsonl)
+constexpr uint64_t kTickLpMaxChains = 3u << 14;
+
 void launch_sha256_tick(int tick_mode, ShaChain* tab, uint32_t mask, uint64_t head, uint32_t n,
                         uint32_t max_blocks, uint64_t live, hipStream_t st) {
   if (n == 0 || max_blocks == 0) return;
   // auto (0): the two-wave kernel while live chains are few (one wave's issue rate bounds a
   // chain), the one-wave kernel once 2^17 live chains give every SIMD several waves (measured
   // crossover, profiles/r01/sha_scale_*.jsonl)
-  const int v = tick_mode >= 1 && tick_mode <= 3 ? tick_mode : (live >= (1u << 17) ? 3 : 1);
-  if (v == 3)
+  const int v = tick_mode >= 1 && tick_mode <= 4
+                    ? tick_mode
+                    : (live >= (1u << 17) ? 3 : live >= kTickLpMaxChains ? 1 : 4);
+  if (v == 4)
+    hipLaunchKernelGGL(k_sha256_tick_lp<1>, dim3((n + 63) / 64), dim3(192), 0, st, tab, mask,
+                       head, n, max_blocks);
+  else if (v == 3)
     hipLaunchKernelGGL(k_sha256_tick1<-1>, dim3((n + 63) / 64), dim3(64), 0, st, tab, mask, head,
                        n, max_blocks);
   else if (v == 2)

@@ -120,7 +120,7 @@ class HashQueue:
 
     def set_option(self, option: int, value: int) -> None:
         """cec_hashq_set_option (CEC_HQOPT_TICK: 0 auto, 1/2 two-wave prefetch depth, 3 one
-        wave)."""
+        wave, 4 lane pairs: the shortest chain latency)."""
         check(_lib.load().cec_hashq_set_option(self._h, option, value), "HashQueue.set_option")
 
     def tick(self, max_blocks: int = 0) -> None:

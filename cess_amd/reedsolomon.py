@@ -353,6 +353,33 @@ def xor_batch(d_dst, d_src, nsrc: int, src_stride: int, length: int, stream=None
                                     _stream_handle(stream)), "xor_batch")
 
 
+def sha256_hex_host(bufs, length: int, threads: int = 16) -> List[bytes]:
+    """SHA-256 hex of equal-length HOST buffers (numpy arrays / bytes-likes, or addresses) with
+    libcessec's multi-chain host hasher (cec_sha256_host: 16 chains per core in AVX-512 lanes or
+    SHA-NI interleaved, on `threads` threads; the GIL is released during the call)."""
+    n = len(bufs)
+    if n == 0:
+        return []
+    keep = []
+    ptrs = []
+    for b in bufs:
+        if isinstance(b, int):
+            ptrs.append(b)
+            continue
+        a = b if isinstance(b, np.ndarray) else np.frombuffer(b, np.uint8)
+        if a.nbytes < length:
+            raise ValueError("buffer shorter than length")
+        if length and not a.flags.c_contiguous:
+            a = np.ascontiguousarray(a)
+        keep.append(a)
+        ptrs.append(a.ctypes.data)
+    out = np.zeros(n * 64, dtype=np.uint8)
+    arr = (c_void_p * n)(*ptrs)
+    check(_lib.load().cec_sha256_host(arr, n, length, out.ctypes.data, 0, None, threads),
+          "sha256_hex_host")
+    return [out[i * 64:(i + 1) * 64].tobytes() for i in range(n)]
+
+
 def sha256_hex_device(d_ptrs: Sequence[int], length: int) -> List[bytes]:
     """SHA-256 hex of device buffers (addresses) of equal length, computed on the GPU."""
     n = len(d_ptrs)

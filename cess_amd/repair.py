@@ -24,7 +24,8 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from . import geometry, records
-from .reedsolomon import CecError, Encoder, ErrTooFewShards, sha256_hex_device
+from .reedsolomon import (CecError, Encoder, ErrTooFewShards, sha256_hex_device,
+                          sha256_hex_host)
 
 
 class ErrFragmentHashMismatch(CecError, ValueError):
@@ -79,7 +80,7 @@ def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, pres
     erasure patterns) and, with `expected` ([{fragment index: recorded hash}] per segment),
     return per-segment booleans: rebuilt fragments hash to the recorded values. hash_on "gpu":
     all of them hashed in one GPU launch, one chain per fragment, where they were rebuilt;
-    "host": copied out once and hashed by `hash_threads` host threads (OpenSSL via hashlib);
+    "host": copied out once and hashed by `hash_threads` host threads (cec_sha256_host);
     "auto": the host below AUTO_GPU_CHECK_FRAGMENTS fragments (a chain is serial, so a few
     chains run faster on host cores), the GPU from there. With `complete_calls`, return
     (ok, calls): calls = {(segment, fragment index): restoral_order_complete call data} for
@@ -106,10 +107,8 @@ def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, pres
     elif hash_on == "gpu":
         got = sha256_hex_device([t.data_ptr() for t in frags], shard_len)
     else:
-        import concurrent.futures as cf
         host = torch.stack(frags).cpu().numpy()
-        with cf.ThreadPoolExecutor(max(1, hash_threads)) as ex:  # hashlib drops the GIL
-            got = list(ex.map(lambda a: hashlib.sha256(a).hexdigest().encode(), host))
+        got = sha256_hex_host(list(host), shard_len, hash_threads)
     ok = [True] * nseg
     calls = {}
     for (s, i, h), g in zip(which, got):

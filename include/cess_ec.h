@@ -197,7 +197,9 @@ int cec_hashq_finish(cec_hashq* q);
 int cec_hashq_status(const cec_hashq* q, uint64_t ticket, int* done, size_t* live_chains,
                      uint64_t* blocks_left);
 /* Queue options. CEC_HQOPT_TICK: tick kernel, 0 = auto by live chains, 1 or 2 = two waves
- * (schedule producer loading 1 or 2 blocks ahead + rounds consumer), 3 = one wave per 64 chains. */
+ * (schedule producer loading 1 or 2 blocks ahead + rounds consumer), 3 = one wave per 64 chains,
+ * 4 = lane pairs (a producer wave + two consumer waves running each chain's rounds on two lanes:
+ * the shortest chain latency, for few live chains). */
 #define CEC_HQOPT_TICK 1
 int cec_hashq_set_option(cec_hashq* q, int option, int value);
 
@@ -501,7 +503,9 @@ int cec_fill_synthetic(uint8_t* d_out, size_t seg_bytes, size_t nseg, uint64_t s
 #define CEC_OPT_CT_VARIANT 2    /* compile-time kernel variant for tuning sweeps: -1 = default;
                                    other values need the tuning build (libcessec_tune.so) */
 #define CEC_OPT_SHA_MODE 3      /* cec_sha256_batch kernel: 0 = auto, 1 = one wave per 64
-                                   buffers, 2 = two waves (schedule producer + rounds consumer) */
+                                   buffers, 2 = two waves (schedule producer + rounds consumer),
+                                   3 = a producer + two consumer waves on lane pairs (the shortest
+                                   chain latency; auto picks it for up to 341 x 64 buffers) */
 #define CEC_OPT_RT_MODE 4       /* run-time-coefficient kernel: 0 = Horner over input groups
                                    with index-mode table XORs when 4 <= inputs <= 32, 1 = always
                                    the per-bit mask kernel, 2 = Horner with v_mov table reads */

@@ -26,7 +26,7 @@ def cess(torch):
     return cess_amd
 
 
-@pytest.fixture(params=[1, 2, 3], ids=["tick2w", "tick2w_pf2", "tick1w"])
+@pytest.fixture(params=[1, 2, 3, 4], ids=["tick2w", "tick2w_pf2", "tick1w", "tick_lanepair"])
 def tick_variant(cess, request):
     """Every test below runs on each tick kernel (CEC_HQOPT_TICK, set per queue by mkq)."""
     return request.param

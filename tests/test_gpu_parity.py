@@ -391,7 +391,7 @@ def test_full_geometry_rs3232(torch, cess, corc):
     assert torch.equal(d_data, ref_d) and torch.equal(d_par, ref_p)
 
 
-@pytest.fixture(params=[1, 2], ids=["sha1wave", "sha2wave"])
+@pytest.fixture(params=[1, 2, 3], ids=["sha1wave", "sha2wave", "sha_lanepair"])
 def sha_mode(request):
     """Run a SHA-256 test with each kernel form (CEC_OPT_SHA_MODE on the test's codec)."""
     return request.param
