@@ -997,7 +997,7 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
     # with the world (every pipeline also fits its window to free HBM when it is created)
     shared = "CESS_DEVICE" in os.environ and world > 1
     gpu_window = max(2, 32 // world) if shared else 32
-    hybrid_window = max(2, 16 // world) if shared else 0
+    hybrid_window = max(2, 32 // world) if shared else 0
     if shared:
         out["shared_gpu_windows"] = {"gpu": gpu_window, "hybrid": hybrid_window}
     recs = {}
@@ -1021,7 +1021,7 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
     # the same records hashed on host threads and hybrid (long-lived sessions)
     lib = cess_amd._lib.load()
     for name, mode in (("segment_lists_host_sha", "host"), ("segment_lists_hybrid", "hybrid")):
-        with RecordsSession(k, m, seg_bytes, local, mode, batch_segments=64, depth=3,
+        with RecordsSession(k, m, seg_bytes, local, mode, batch_segments=64,
                             host_threads=16, window=hybrid_window) as ses:
             ses.encode(buf[:64 * seg_bytes])  # warm-up
             t, runs, (rec, st) = timed_runs(lambda: ses.encode(buf))

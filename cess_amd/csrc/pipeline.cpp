@@ -35,6 +35,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -71,9 +73,9 @@ double now_s() {
       .count();
 }
 
-// GPU time of one 64-byte block of a lone chain (the latency-form tick, DESIGN.md §4: ~1.8 us
+// GPU time of one 64-byte block of a lone chain (the lane-pair tick, DESIGN.md §4: 1.67-1.70 us
 // measured; a little slack for the ticks' launch gaps). Used only to place a batch's chains.
-constexpr double kGpuChainSecondsPerBlock = 1.9e-6;
+constexpr double kGpuChainSecondsPerBlock = 1.8e-6;
 
 }  // namespace
 
@@ -150,9 +152,14 @@ struct cec_pipeline {
     SB = (size_t)k * F;
     B = o.batch_segments ? o.batch_segments : 64;
     mode = o.hash;
-    depth = o.depth ? o.depth : 3;
+    // host hashing holds a pinned batch until its chains are hashed (a 16 MiB chain in one of 16
+    // AVX-512 lanes takes ~50 ms), so the host placements keep one batch more in the ring
+    depth = o.depth ? o.depth : (host_hash() ? 4 : 3);
     if (depth < 2) return cec::set_error(CEC_EINVAL, "depth must be >= 2");
-    window = o.window ? o.window : (mode == CEC_PIPE_HASH_HYBRID ? 16 : 32);
+    // Ticks share the compute stream's hardware queue and, as the round-robin falls, the parity
+    // copies' too (rocprof timeline, profiles/r06/): a batch then costs its D2H plus its tick
+    // there, so the tick (blocks / window x ~1.7 us) must stay well under a batch's interval
+    window = o.window ? o.window : 32;
     if (window < 1) return cec::set_error(CEC_EINVAL, "window must be >= 1");
     host_threads = o.host_threads > 0 ? o.host_threads : 16;
     tail_batches = o.tail_batches;
@@ -397,6 +404,7 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
   p->wait_host_jobs();
   const double t0 = now_s();
   double t_read = 0, t_wait = 0;
+  double w_d2h = 0, w_slot = 0, w_rec = 0;  // (CEC_PIPELINE_TRACE) where the waits went
   const int n = p->k + p->m;
   using Batch = cec_pipeline::Batch;
   std::deque<Batch> inflight;  // batch order; popped once fully delivered
@@ -436,6 +444,7 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
     const double w = now_s();
     PL_TRY(hipEventSynchronize(p->ev_d2h[b.ds]));  // (a later reuse of the slot only waits more)
     t_wait += now_s() - w;
+    w_d2h += now_s() - w;
     p->submit_host_parity(b);
     if (on_fragments) {
       const uint8_t* sh[256];
@@ -464,6 +473,7 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
         const double w = now_s();
         p->host_wait(o);
         t_wait += now_s() - w;
+        w_slot += now_s() - w;
       }
     return CEC_OK;
   };
@@ -496,6 +506,7 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
       }
       p->host_wait(b);
       t_wait += now_s() - w;
+      w_rec += now_s() - w;
       if (on_record && p->mode != CEC_PIPE_HASH_NONE) {
         const int g0 = b.gpu ? (b.gpu_seg ? 0 : p->hybrid_gpu_first()) : n;
         for (size_t s = 0; s < b.nseg; ++s) {
@@ -636,6 +647,10 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
     if (s) PL_TRY(hipStreamSynchronize(s));
   p->wait_host_jobs();
   PL_RC(files_done());
+  if (getenv("CEC_PIPELINE_TRACE"))
+    fprintf(stderr, "cec_pipeline: %.4f s, read %.4f, wait %.4f (d2h %.4f, host slot %.4f, "
+            "records %.4f), mode %d, window %d, depth %d\n", now_s() - t0, t_read, t_wait,
+            w_d2h, w_slot, w_rec, p->mode, p->window, p->depth);
   if (stats) {
     stats->segments = segs_total;
     stats->bytes_in = bytes_in;

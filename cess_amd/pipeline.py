@@ -277,7 +277,7 @@ class RecordsSession:
 
     def __init__(self, k: int = geometry.DATA_SHARDS, m: int = geometry.PARITY_SHARDS,
                  segment_size: int = geometry.SEGMENT_SIZE, device: int = 0,
-                 hash_on: str = "hybrid", batch_segments: int = 64, depth: int = 3,
+                 hash_on: str = "hybrid", batch_segments: int = 64, depth: int = 0,
                  window: int = 0, host_threads: int = 16, tail_batches: int = -1,
                  max_segments: int = 0, read_threads: int = 8):
         if segment_size % k:

@@ -244,11 +244,11 @@ typedef int (*cec_record_fn)(void* user, uint64_t seg, const uint8_t* seg_hex,
 typedef struct cec_pipeline_opts {
   size_t shard_len;      /* F: a segment is k * F bytes */
   size_t batch_segments; /* segments per batch (0: 64) */
-  int depth;             /* pinned host batches (0: 3; >= 2) */
+  int depth;             /* pinned host batches (0: 3, host / hybrid hashing 4; >= 2) */
   int hash;              /* CEC_PIPE_HASH_*: 0 none, 1 GPU, 2 host, 3 hybrid */
-  int window;            /* batches hashing at once on the GPU queue (0: 32, hybrid 16); the
-                            pipeline holds window + 3 device batch slots (1.5 GiB each for CESS
-                            batches) and shrinks the window to what free HBM holds */
+  int window;            /* batches hashing at once on the GPU queue (0: 32); the pipeline
+                            holds window + 3 device batch slots (1.5 GiB each for CESS batches)
+                            and shrinks the window to what free HBM holds */
   uint64_t max_segments; /* 0: no limit; else CEC_ESEGCOUNT when a source has more segments
                             (CEC_SEGMENT_COUNT: what one upload_declaration can carry) */
   int host_threads;      /* host SHA-256 threads for hash = 2 / 3 (0: 16) */

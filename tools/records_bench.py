@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--modes", default="none,gpu,host,hybrid")
     ap.add_argument("--tails", default="-1")
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--depth", type=int, default=3)
+    ap.add_argument("--depth", type=int, default=0, help="0: the pipeline's default")
     ap.add_argument("--window", type=int, default=0)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--stream", type=int, default=0, help="files in the records_stream leg")
