@@ -471,6 +471,7 @@ struct Pool {
   std::deque<std::shared_ptr<JobState>> q;  // jobs with chains / tasks not yet handed out
   std::vector<std::thread> th;
   int idle = 0;
+  size_t lanes_busy = 0;  // chains in the workers' lanes
   bool stop = false;
 
   ~Pool() {
@@ -486,14 +487,21 @@ struct Pool {
     while ((int)th.size() < n) th.emplace_back([this] { loop(); });
   }
 
-  // (under mu) chains of x16 jobs into free lanes: at most a fair share when workers are idle
+  // (under mu) chains of x16 jobs into free lanes. With enough chains for every worker to fill
+  // kMinX16Lanes lanes, a worker fills all 16 (x16 at 5.5 GB/s per core beats SHA-NI x2's 3.6
+  // once a worker holds 11 chains: 256 chains of 16 MiB on 16 threads 88.6 GB/s,
+  // profiles/r06/host_sha_probe_4g.jsonl); with fewer, the chains are shared out among the idle
+  // workers, who run them on SHA-NI (spreading 64 chains over 16 threads beats 4 full registers).
   void take_chains(Lane* L, int& n) {
     size_t avail = 0;
     for (auto& js : q)
       if (js->form == CEC_HSHA_X16) avail += js->job.n - js->next;
     if (!avail) return;
     size_t want = (size_t)(kLanes - n);
-    if (idle > 0) want = std::min(want, std::max<size_t>(1, (avail + idle) / (idle + 1)));
+    const bool plenty = avail + lanes_busy >= (size_t)kMinX16Lanes * th.size();
+    if (idle > 0 && !plenty)
+      want = std::min(want, std::max<size_t>(1, (avail + idle) / (idle + 1)));
+    lanes_busy += std::min(want, avail);
     for (auto it = q.begin(); it != q.end() && want;) {
       auto& js = *it;
       if (js->form != CEC_HSHA_X16) {
@@ -528,11 +536,14 @@ struct Pool {
   void loop() {
     Lane L[kLanes];
     int n = 0;
+    size_t finished = 0;  // lanes freed since this worker last held the lock
     while (true) {
       std::shared_ptr<JobState> tjs;
       size_t t0 = 0, tn = 0;
       {
         std::unique_lock<std::mutex> l(mu);
+        lanes_busy -= finished;
+        finished = 0;
         while (true) {
           if (n < kLanes) take_chains(L, n);
           if (n) break;
@@ -559,6 +570,7 @@ struct Pool {
           if (i != n - 1) std::swap(L[i], L[n - 1]);
           --n;
           --i;
+          ++finished;
         }
       }
     }
