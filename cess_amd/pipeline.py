@@ -329,6 +329,25 @@ class RecordsSession:
                                  self.read_threads)
         return out, st
 
+    def encode_range(self, src: Source, seg_start: int, seg_stop: int):
+        """(FileRecord, PipelineStats) of segments [seg_start, seg_stop) of a file or buffer (one
+        rank's or one device's contiguous shard of a file encoded across GPUs); segment numbers
+        count from the range's first segment, `file_hash` covers the range only."""
+        from .segments import FileRecord, SegmentList, file_hash
+        size = _source_size(src)
+        if size is None:
+            raise ValueError("encode_range needs a path or an in-memory buffer")
+        a, b = seg_start * self.segment_size, min(size, seg_stop * self.segment_size)
+        if seg_start < 0 or b <= a:
+            from .reedsolomon import ErrShortData
+            raise ErrShortData(ErrShortData.__doc__)
+        recs = {}
+        st = self.pipe.run_files([src], None, lambda _f, s, sh, fl: recs.__setitem__(
+            s, SegmentList(sh, fl)), None, self.read_threads, [(a, b)])
+        out = FileRecord(b"", b - a, [recs[s] for s in range(len(recs))])
+        out.file_hash = file_hash(out.segments)
+        return out, st
+
     def encode(self, src: Source, on_fragment=None):
         """(FileRecord, PipelineStats) of one file."""
         cb = (lambda _f, seg, idx, v: on_fragment(seg, idx, v)) if on_fragment else None
@@ -435,12 +454,8 @@ def encode_file_records_multi(src: Union[str, bytes, bytearray, memoryview, np.n
             return [], None
         with RecordsSession(k, m, segment_size, devices[i], mode, host_threads=hash_threads,
                             read_threads=read_threads, **kw) as ses:
-            rng = (a * segment_size, min(size, b * segment_size))
-            recs = {}
-            st = ses.pipe.run_files([src], None, lambda _f, s, sh, fl: recs.__setitem__(
-                s, (sh, fl)), None, read_threads, [rng])
-        from .segments import SegmentList
-        return [SegmentList(*recs[s]) for s in range(b - a)], st
+            rec, st = ses.encode_range(src, a, b)
+        return rec.segments, st
 
     with cf.ThreadPoolExecutor(max_workers=len(devices)) as ex:
         parts = list(ex.map(work, range(len(devices))))

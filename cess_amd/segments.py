@@ -148,21 +148,24 @@ class _ParallelReader:
 
 def encode_file_sharded(path: str, rank: int, world: int, group=None, **kw) -> Optional[FileRecord]:
     """Encode a file across `world` GPU ranks (one process per GPU): rank r encodes a
-    contiguous range of segments (distributed.shard_range) with no data exchange, then the
-    SegmentLists are gathered on rank 0 (object gather over the process group), which returns
-    the whole-file record. Other ranks return None."""
+    contiguous range of segments (distributed.shard_range) with no data exchange through the C
+    pipeline (pipeline.RecordsSession: hybrid record hashes by default; keyword arguments as
+    RecordsSession's, `device` defaulting to 0), then the SegmentLists are gathered on rank 0
+    (object gather over the process group), which returns the whole-file record. Other ranks
+    return None."""
     import os as _os
 
     from .distributed import shard_range
+    from .pipeline import RecordsSession
     seg_size = kw.get("segment_size", geometry.SEGMENT_SIZE)
     size = _os.path.getsize(path)
     nseg = (size + seg_size - 1) // seg_size
     a, b = shard_range(nseg, world, rank)
     part = []
     if b > a:
-        se = SegmentEncoder(**kw)
-        part = se.encode_range(path, a, b).segments
-        se.close()
+        kw.setdefault("batch_segments", max(1, min(64, b - a)))
+        with RecordsSession(**kw) as ses:
+            part = ses.encode_range(path, a, b)[0].segments
     if world > 1:
         import torch.distributed as dist
         parts = [None] * world if rank == 0 else None

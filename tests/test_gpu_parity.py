@@ -680,6 +680,16 @@ def test_encode_file_sharded_single_rank(tmp_path, orc):
         se.close()
         want = orc.segment_list(blob, 2, 1, 1 << 20)[a:b]
         assert [(s.hash, s.fragment_list) for s in rec.segments] == want
+    from cess_amd.pipeline import RecordsSession
+    for hash_on in ("hybrid", "host", "gpu"):
+        with RecordsSession(2, 1, 1 << 20, 0, hash_on, batch_segments=2) as ses:
+            for world_slice in range(3):
+                a, b = shard_range(6, 3, world_slice)
+                want = orc.segment_list(blob, 2, 1, 1 << 20)[a:b]
+                for src in (str(p), np.frombuffer(blob, np.uint8)):
+                    rec, _ = ses.encode_range(src, a, b)
+                    assert [(s.hash, s.fragment_list) for s in rec.segments] == want, hash_on
+                    assert rec.file_hash == orc.file_hash(want)
     rec = encode_file_sharded(str(p), 0, 1, segment_size=1 << 20, batch_segments=4)
     assert [(s.hash, s.fragment_list) for s in rec.segments] == orc.segment_list(
         blob, 2, 1, 1 << 20)
