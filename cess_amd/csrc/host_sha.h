@@ -44,4 +44,13 @@ bool ready(const std::shared_ptr<JobState>& js);
 // Block until the job is done (the second argument is unused: the workers do all hashing).
 void wait(const std::shared_ptr<JobState>& js, bool help);
 
+// Cumulative counters of the pool's workers (diagnostics: the pipeline's CEC_PIPELINE_TRACE).
+struct PoolStats {
+  double busy_s = 0;          // worker time spent hashing
+  uint64_t lane_blocks = 0;   // blocks hashed by lane steps (x16 and SHA-NI lane steps)
+  uint64_t x16_steps = 0, ni_steps = 0, x16_lane_steps = 0;  // steps, and lanes used by x16 ones
+  uint64_t spilled = 0;       // chains given back to idle workers
+};
+PoolStats stats();
+
 }  // namespace hsha

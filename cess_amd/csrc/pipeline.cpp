@@ -403,6 +403,7 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
     if (s) PL_TRY(hipStreamSynchronize(s));
   p->wait_host_jobs();
   const double t0 = now_s();
+  const hsha::PoolStats ps0 = hsha::stats();
   double t_read = 0, t_wait = 0;
   double w_d2h = 0, w_slot = 0, w_rec = 0;  // (CEC_PIPELINE_TRACE) where the waits went
   const int n = p->k + p->m;
@@ -647,10 +648,20 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
     if (s) PL_TRY(hipStreamSynchronize(s));
   p->wait_host_jobs();
   PL_RC(files_done());
-  if (getenv("CEC_PIPELINE_TRACE"))
+  if (getenv("CEC_PIPELINE_TRACE")) {
+    const hsha::PoolStats ps = hsha::stats();
+    const double wall = now_s() - t0;
+    const uint64_t xs = ps.x16_steps - ps0.x16_steps;
     fprintf(stderr, "cec_pipeline: %.4f s, read %.4f, wait %.4f (d2h %.4f, host slot %.4f, "
-            "records %.4f), mode %d, window %d, depth %d\n", now_s() - t0, t_read, t_wait,
-            w_d2h, w_slot, w_rec, p->mode, p->window, p->depth);
+            "records %.4f), mode %d, window %d, depth %d; host SHA workers busy %.3f s = %.2f of "
+            "%d threads, x16 steps %llu at %.1f lanes, SHA-NI steps %llu, spilled %llu\n", wall,
+            t_read, t_wait, w_d2h, w_slot, w_rec, p->mode, p->window, p->depth,
+            ps.busy_s - ps0.busy_s, (ps.busy_s - ps0.busy_s) / (wall * p->host_threads),
+            p->host_threads, (unsigned long long)xs,
+            xs ? (double)(ps.x16_lane_steps - ps0.x16_lane_steps) / (double)xs : 0.0,
+            (unsigned long long)(ps.ni_steps - ps0.ni_steps),
+            (unsigned long long)(ps.spilled - ps0.spilled));
+  }
   if (stats) {
     stats->segments = segs_total;
     stats->bytes_in = bytes_in;

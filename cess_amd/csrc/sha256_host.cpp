@@ -440,9 +440,21 @@ struct Lane {
   }
 };
 
+struct Counters {
+  std::atomic<uint64_t> busy_ns{0}, lane_blocks{0}, x16_steps{0}, ni_steps{0}, x16_lanes{0},
+      spilled{0};
+} g_count;
+
+uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 // Advance the n active lanes by `step` blocks (step <= each lane's blocks to its next event).
 void step_lanes(Lane* L, int n, uint64_t step) {
   if (!step) return;
+  g_count.lane_blocks.fetch_add(step * (uint64_t)n, std::memory_order_relaxed);
   uint32_t* st[kLanes];
   const uint8_t* p[kLanes];
   if (n >= kMinX16Lanes && has_x16()) {
@@ -452,7 +464,10 @@ void step_lanes(Lane* L, int n, uint64_t step) {
       p[i] = i < n ? L[i].p : kZeros;
     }
     x16_blocks(st, p, step);
+    g_count.x16_steps.fetch_add(1, std::memory_order_relaxed);
+    g_count.x16_lanes.fetch_add((uint64_t)n, std::memory_order_relaxed);
   } else {
+    g_count.ni_steps.fetch_add(1, std::memory_order_relaxed);
     for (int i = 0; i < n; ++i) {
       st[i] = L[i].st;
       p[i] = L[i].p;
@@ -469,9 +484,11 @@ struct Pool {
   std::mutex mu;
   std::condition_variable cv;
   std::deque<std::shared_ptr<JobState>> q;  // jobs with chains / tasks not yet handed out
+  std::deque<Lane> spill;                   // chains in progress given back by a worker
   std::vector<std::thread> th;
   int idle = 0;
   size_t lanes_busy = 0;  // chains in the workers' lanes
+  size_t avail = 0;       // x16 chains not yet in any lane (queued jobs' chains + spill)
   bool stop = false;
 
   ~Pool() {
@@ -486,22 +503,26 @@ struct Pool {
     std::lock_guard<std::mutex> l(mu);
     while ((int)th.size() < n) th.emplace_back([this] { loop(); });
   }
-
   // (under mu) chains of x16 jobs into free lanes. With enough chains for every worker to fill
   // kMinX16Lanes lanes, a worker fills all 16 (x16 at 5.5 GB/s per core beats SHA-NI x2's 3.6
   // once a worker holds 11 chains: 256 chains of 16 MiB on 16 threads 88.6 GB/s,
   // profiles/r06/host_sha_probe_4g.jsonl); with fewer, the chains are shared out among the idle
   // workers, who run them on SHA-NI (spreading 64 chains over 16 threads beats 4 full registers).
+  // Chains a worker gave back (spill) go first.
   void take_chains(Lane* L, int& n) {
-    size_t avail = 0;
-    for (auto& js : q)
-      if (js->form == CEC_HSHA_X16) avail += js->job.n - js->next;
     if (!avail) return;
     size_t want = (size_t)(kLanes - n);
     const bool plenty = avail + lanes_busy >= (size_t)kMinX16Lanes * th.size();
     if (idle > 0 && !plenty)
       want = std::min(want, std::max<size_t>(1, (avail + idle) / (idle + 1)));
-    lanes_busy += std::min(want, avail);
+    want = std::min(want, avail);
+    lanes_busy += want;
+    avail -= want;
+    while (want && !spill.empty()) {
+      L[n++] = std::move(spill.front());
+      spill.pop_front();
+      --want;
+    }
     for (auto it = q.begin(); it != q.end() && want;) {
       auto& js = *it;
       if (js->form != CEC_HSHA_X16) {
@@ -517,6 +538,26 @@ struct Pool {
       else
         ++it;
     }
+  }
+  // A worker whose lanes hold more than its share of the chains in flight while other workers
+  // idle and nothing is queued (a job's last chains, all taken greedily by a few workers: 32
+  // chains of 16 MiB on two x16 registers take 48 ms, on 16 cores' SHA-NI 9 ms) gives the
+  // surplus back; idle workers pick it up at once, the others at their next step. (under mu)
+  void rebalance(Lane* L, int& n) {
+    if (n <= 1 || idle == 0 || avail) return;
+    const size_t fair = std::max<size_t>(1, (lanes_busy + th.size() - 1) / th.size());
+    if ((size_t)n <= fair) return;
+    // keep the lanes closest to their end; give back the longest
+    std::sort(L, L + n, [](const Lane& a, const Lane& b) {
+      return a.full - a.done < b.full - b.done;
+    });
+    const int give = n - (int)fair;
+    for (int i = (int)fair; i < n; ++i) spill.push_back(std::move(L[i]));
+    n = (int)fair;
+    lanes_busy -= (size_t)give;
+    avail += (size_t)give;
+    g_count.spilled.fetch_add((uint64_t)give, std::memory_order_relaxed);
+    cv.notify_all();
   }
   // (under mu) a task of groups from the oldest job of another form
   bool take_task(std::shared_ptr<JobState>& js, size_t& c0, size_t& cn) {
@@ -546,7 +587,10 @@ struct Pool {
         finished = 0;
         while (true) {
           if (n < kLanes) take_chains(L, n);
-          if (n) break;
+          if (n) {
+            rebalance(L, n);
+            break;
+          }
           if (take_task(tjs, t0, tn)) break;
           if (stop) return;
           ++idle;
@@ -554,8 +598,10 @@ struct Pool {
           --idle;
         }
       }
+      const uint64_t b0 = now_ns();
       if (tjs) {
         hash_range(tjs->job, t0, tn, tjs->form);
+        g_count.busy_ns.fetch_add(now_ns() - b0, std::memory_order_relaxed);
         // tasks count as one unit each in `left`
         chain_done(tjs);
         continue;
@@ -563,6 +609,7 @@ struct Pool {
       uint64_t step = kStepBlocks;
       for (int i = 0; i < n; ++i) step = std::min(step, L[i].to_event());
       step_lanes(L, n, step);
+      g_count.busy_ns.fetch_add(now_ns() - b0, std::memory_order_relaxed);
       for (int i = 0; i < n; ++i) {
         if (!L[i].pre_done && L[i].done == L[i].pre) L[i].prefix();
         if (L[i].pre_done && L[i].done == L[i].full) {
@@ -607,6 +654,7 @@ std::shared_ptr<JobState> submit(const Job& job, int threads) {
   {
     std::lock_guard<std::mutex> l(P.mu);
     P.q.push_back(js);
+    if (js->form == CEC_HSHA_X16) P.avail += job.n;
   }
   P.cv.notify_all();
   return js;
@@ -619,6 +667,17 @@ bool ready(const std::shared_ptr<JobState>& js) {
 void wait(const std::shared_ptr<JobState>& js, bool) {
   std::unique_lock<std::mutex> l(js->mu);
   js->cv.wait(l, [&] { return js->done; });
+}
+
+PoolStats stats() {
+  PoolStats s;
+  s.busy_s = 1e-9 * (double)g_count.busy_ns.load();
+  s.lane_blocks = g_count.lane_blocks.load();
+  s.x16_steps = g_count.x16_steps.load();
+  s.ni_steps = g_count.ni_steps.load();
+  s.x16_lane_steps = g_count.x16_lanes.load();
+  s.spilled = g_count.spilled.load();
+  return s;
 }
 
 void set_form(int form) { g_form.store(form); }

@@ -144,9 +144,9 @@ int cec_sha256_hex(const uint8_t* const* d_bufs, size_t n, size_t len, uint8_t* 
 int cec_sha256_host(const uint8_t* const* bufs, size_t n, size_t len, uint8_t* hex,
                     size_t prefix_len, uint8_t* prefix_hex, int threads);
 /* Forms of the host hasher: which one runs is process-wide (cec_host_sha_set_form; -1 restores
- * the default, SHA-NI x2 where the CPU has SHA-NI). cec_host_sha_probe times one form on the
- * calling thread over `chains` chains of bytes_per_chain bytes and returns GB/s (< 0: the CPU
- * lacks the form). */
+ * the default: AVX-512 x16 where the CPU has it, else SHA-NI x2 where it has SHA-NI).
+ * cec_host_sha_probe times one form on the calling thread over `chains` chains of
+ * bytes_per_chain bytes and returns GB/s (< 0: the CPU lacks the form). */
 #define CEC_HSHA_SCALAR 0
 #define CEC_HSHA_NI1 1
 #define CEC_HSHA_NI2 2

@@ -132,3 +132,22 @@ def test_concurrent_jobs_share_the_lanes(lib):
                     assert all(ex.map(run, jobs)), name
         finally:
             lib.cec_host_sha_set_form(-1)
+
+
+def test_greedy_lanes_then_tail_spill(lib):
+    """More chains than 11 per worker: workers fill all 16 lanes; the job's last chains, taken
+    by a few workers, are given back to the idle ones mid-chain (the spill) and finish there.
+    Every digest (and every prefix digest) still equals hashlib's."""
+    rng = np.random.default_rng(3)
+    n, length, prefix = 200, 64 * 2000 + 5, 64 * 700
+    base = rng.integers(0, 256, length + n, dtype=np.uint8).tobytes()
+    bufs = [base[i:i + length] for i in range(n)]
+    if "x16" in forms(lib):
+        lib.cec_host_sha_set_form(FORMS["x16"])
+    try:
+        for _ in range(2):
+            got, pre = host_hex(lib, bufs, length, prefix, threads=16)
+            assert got == [hashlib.sha256(b).hexdigest() for b in bufs]
+            assert pre == [hashlib.sha256(b[:prefix]).hexdigest() for b in bufs]
+    finally:
+        lib.cec_host_sha_set_form(-1)

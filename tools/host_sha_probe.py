@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--threads", default="1,8,16")
     ap.add_argument("--mib", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--probe-only", action="store_true")
     a = ap.parse_args()
     lib = ctypes.CDLL(os.path.join(ROOT, "cess_amd", "libcessec.so"))
     lib.cec_host_sha_probe.restype = ctypes.c_double
@@ -39,11 +40,13 @@ def main():
     except OSError:
         pass
     for form in range(5):
-        for w in (1, 2, 4, 16):
+        for w in (1, 2, 4, 16, 18):
             g = lib.cec_host_sha_probe(form, 4 << 20, w)
             if g > 0:
                 print(json.dumps({"probe": NAMES[form], "chains": w, "GBps_one_thread": round(g, 3),
                                   "cpu": cpu}), flush=True)
+    if a.probe_only:
+        return
     total = a.mib << 20
     buf = np.random.default_rng(1).integers(0, 256, total, dtype=np.uint8)
     for chain in (16 << 20, 8 << 20):

@@ -11,12 +11,18 @@ import argparse
 import hashlib
 import json
 import os
+import resource
 import sys
 import time
 
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def cpu_seconds():
+    r = resource.getrusage(resource.RUSAGE_SELF)
+    return r.ru_utime + r.ru_stime
 
 
 def check(rec, buf, seg, k, picks):
@@ -42,6 +48,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--depth", type=int, default=0, help="0: the pipeline's default")
     ap.add_argument("--window", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=64, help="segments per batch")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--stream", type=int, default=0, help="files in the records_stream leg")
     ap.add_argument("--stream-segments", type=int, default=1000)
@@ -72,37 +79,45 @@ def main():
             t0 = time.perf_counter()
             if mode == "none":
                 enc = Encoder(k, m, 0)
-                pipe = Pipeline(enc, seg // k, hash=False, depth=a.depth)
+                pipe = Pipeline(enc, seg // k, hash=False, depth=a.depth,
+                                batch_segments=a.batch)
                 ses = None
             else:
                 ses = RecordsSession(k, m, seg, 0, mode, depth=a.depth, window=a.window,
-                                     host_threads=a.threads, tail_batches=tail)
+                                     host_threads=a.threads, tail_batches=tail,
+                                     batch_segments=a.batch)
             t_create = time.perf_counter() - t0
-            times, ok = [], True
+            times, cpus, ok = [], [], True
             for _ in range(a.reps):
+                c0 = cpu_seconds()
                 t0 = time.perf_counter()
                 if ses is None:
                     st = pipe.run(src)
                 else:
                     rec, st = ses.encode(src)
                 times.append(time.perf_counter() - t0)
+                cpus.append(cpu_seconds() - c0)
                 if ses is not None:
                     ok = ok and check(rec, src, seg, k, picks) and len(rec.segments) == nseg
             info = (ses.pipe if ses else pipe).info()
-            out = {"mode": mode, "tail_batches": tail, "create_s": round(t_create, 3),
-                   "seconds": [round(t, 4) for t in times], "best_GBps":
+            out = {"mode": mode, "tail_batches": tail, "batch_segments": a.batch, "create_s": round(t_create, 3),
+                   "seconds": [round(t, 4) for t in times],
+                   "cpu_seconds": [round(c, 3) for c in cpus], "best_GBps":
                    round(size / min(times) / 1e9, 2), "records_ok": ok, **info}
             print(json.dumps(out), flush=True)
             if a.stream and ses is not None:
                 files = [buf[:nstream]] * a.stream
                 done_t = []
+                c0 = cpu_seconds()
                 t0 = time.perf_counter()
                 recs, st = ses.encode_many(files, on_file=lambda f, r, s: done_t.append(
                     time.perf_counter() - t0))
                 dt = time.perf_counter() - t0
+                dc = cpu_seconds() - c0
                 ok2 = all(check(r, buf, seg, k, [0, a.stream_segments - 1]) for r in recs)
                 print(json.dumps({"mode": mode, "tail_batches": tail, "records_stream": a.stream,
                                   "file_bytes": nstream, "seconds": round(dt, 4),
+                                  "cpu_seconds": round(dc, 3),
                                   "GBps": round(a.stream * nstream / dt / 1e9, 2),
                                   "file_done_s": [round(x, 3) for x in done_t],
                                   "records_ok": ok2}), flush=True)
