@@ -471,21 +471,24 @@ def launch_ranks(n: int, argv) -> int:
 
 
 def cabi_legs(ex_out, gather_leg, degraded_gather, enc, code, world, rank, dev, deadline,
-              emit):
-    """The degraded read through libcessec's own RCCL communicator (cec_dist_*, the C ABI a Go /
-    Rust host uses) at world > 1, on the same placement as the torch legs: RS(2,1) survivors and
-    RS(32,32) both exchanges. They run last, after every other measurement, under a watchdog: a
-    rank that fails or stalls inside the collective exchange would otherwise hold every rank in
-    it, so past `deadline` seconds each rank records the legs as not finished, rank 0 prints the
-    line it has (`emit`), and the process ends with status WATCHDOG_EXIT (os._exit: the peers are
-    stuck in RCCL), so the driver's rc records that a rank hung while the line stays parseable."""
+              emit, torch_legs=False, cabi=True):
+    """The cross-GPU exchange legs of the N > 1 line, run last, after every other measurement,
+    under one watchdog: with `torch_legs` the degraded read over the torch.distributed group
+    (RS(2,1) survivors, RS(32,32) both exchanges), then (`cabi`) the same through libcessec's
+    own RCCL communicator (cec_dist_*, the C ABI a Go / Rust host uses), on the same placement.
+    A leg that raises is recorded as an error and the next one runs. A rank that fails or stalls
+    inside a collective exchange would otherwise hold every rank in it, so past `deadline`
+    seconds each rank records the unfinished legs as such, rank 0 prints the line it has (`emit`),
+    and the process ends with status WATCHDOG_EXIT (os._exit: the peers are stuck in RCCL), so the
+    driver's rc records that a rank hung while the line stays parseable."""
     import threading
     import torch
     import torch.distributed as dist
     import cess_amd
     k, m, F = code
     done = threading.Event()
-    legs = ("degraded_gather_cabi", "wide_degraded_gather_cabi")
+    legs = ((("degraded_gather", "wide_degraded_gather") if torch_legs else ()) +
+            (("degraded_gather_cabi", "wide_degraded_gather_cabi") if cabi else ()))
 
     def watchdog():
         if done.wait(deadline):
@@ -503,26 +506,36 @@ def cabi_legs(ex_out, gather_leg, degraded_gather, enc, code, world, rank, dev, 
             os._exit(WATCHDOG_EXIT)
 
     threading.Thread(target=watchdog, daemon=True).start()
-    transport = "libcessec cec_dist_degraded_read (own RCCL communicator)"
-    try:
-        leg = gather_leg(degraded_gather(enc, k, m, F, world, rank, dev, 64, "survivors", "cabi"))
-        leg["transport"] = transport
-        ex_out[legs[0]] = leg
-        wk, wm, wF = CONFIGS[5][:3]
-        wenc = cess_amd.New(wk, wm, device=dev.index)
-        wide = {}
-        for ex in ("survivors", "partials"):
-            wide[ex] = gather_leg(degraded_gather(wenc, wk, wm, wF, world, rank, dev, 32, ex,
-                                                  "cabi"), code=(wk, wF))
-            wide[ex]["transport"] = transport
-        ex_out[legs[1]] = wide
-        wenc.close()
-    except Exception as e:  # noqa: BLE001 - reported in the line
-        ok = 0
-        for name in legs:
-            ex_out.setdefault(name, {"error": f"{type(e).__name__}: {e}"})
-    else:
-        ok = 1
+    ok = 1
+    for via, suffix, transport in (("torch", "", "torch.distributed group"),
+                                   ("cabi", "_cabi",
+                                    "libcessec cec_dist_degraded_read (own RCCL communicator)")):
+        if "degraded_gather" + suffix not in legs:
+            continue
+        try:
+            leg = gather_leg(degraded_gather(enc, k, m, F, world, rank, dev, 64, "survivors",
+                                             via))
+            leg["transport"] = transport
+            ex_out["degraded_gather" + suffix] = leg
+            # the wide code's single-fragment degraded read, both exchanges:
+            # RS(32,32) with 16 MiB segments (F = 512 KiB), 8 fragments per GPU at world 8; 32
+            # segments per GPU keep the survivor leg's grouped point-to-point batch under ~900
+            # transfers per rank
+            wk, wm, wF = CONFIGS[5][:3]
+            wenc = cess_amd.New(wk, wm, device=dev.index)
+            try:
+                wide = {}
+                for ex in ("survivors", "partials"):
+                    wide[ex] = gather_leg(degraded_gather(wenc, wk, wm, wF, world, rank, dev, 32,
+                                                          ex, via), code=(wk, wF))
+                    wide[ex]["transport"] = transport
+                ex_out["wide_degraded_gather" + suffix] = wide
+            finally:
+                wenc.close()
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            ok = 0
+            for name in ("degraded_gather" + suffix, "wide_degraded_gather" + suffix):
+                ex_out.setdefault(name, {"error": f"{type(e).__name__}: {e}"[:400]})
     # every rank that got here agrees (cec_dist fails a caller error on all ranks alike); a rank
     # stuck in the exchange never arrives, and the watchdog then ends the ones waiting here
     if world > 1:
@@ -1214,8 +1227,8 @@ def main() -> None:
                     help="config 6: the erasures of a segment are consecutive shard indices "
                          "(random start, wrapping) instead of random ones")
     ap.add_argument("--cabi-deadline", type=float, default=240.0,
-                    help="world > 1: seconds the C-ABI (cec_dist) exchange legs may take before "
-                         "the line is printed without them")
+                    help="world > 1: seconds the exchange legs (torch group, then the C-ABI "
+                         "cec_dist) may take before the line is printed without the unfinished")
     ap.add_argument("--erasures", type=int, default=0,
                     help="config 6: random erasures per segment (default m)")
     ap.add_argument("--lose-parity", action="store_true",
@@ -1586,26 +1599,16 @@ def main() -> None:
         # (PCIe-inclusive; the north_star's pinned double-buffering, sharded per GPU)
         out["extra"]["host_e2e"] = guarded(host_e2e_leg, dev, local, world, rank, backend)
 
-    cabi_pending = False
+    exchange_pending = cabi_pending = False
     if args.config == 4:
         out["degraded_gather"] = gather_leg(gather)
     elif world > 1 and not args.no_extra and args.config == 2:
         # config 4's exchange step measured in the default (scaling) run as well, through both
         # transports: the torch.distributed group and libcessec's own RCCL communicator (the C
-        # ABI a Go / Rust host uses), on the same placement and lost list
+        # ABI a Go / Rust host uses), on the same placement and lost list. Both run last, under
+        # one watchdog (cabi_legs below): they are the line's only cross-GPU collectives
         ex_out = out.setdefault("extra", {})
-        ex_out["degraded_gather"] = gather_leg(
-            degraded_gather(enc, k, m, F, world, rank, dev, 64))
-        # the wide code's single-fragment degraded read, both exchanges: RS(32,32)
-        # with 16 MiB segments (F = 512 KiB), 8 fragments per GPU at world 8; 32 segments per GPU
-        # keep the survivor leg's grouped point-to-point batch under ~900 transfers per rank
-        wk, wm, wF = CONFIGS[5][:3]
-        wenc = cess_amd.New(wk, wm, device=local)
-        ex_out["wide_degraded_gather"] = {
-            ex: gather_leg(degraded_gather(wenc, wk, wm, wF, world, rank, dev, 32, ex),
-                           code=(wk, wF))
-            for ex in ("survivors", "partials")}
-        wenc.close()
+        exchange_pending = True
         if "CESS_DEVICE" in os.environ:
             # ranks sharing one GPU (the one-GPU rehearsal): RCCL refuses a communicator with
             # two ranks on one device ("Duplicate GPU detected"), so the C-ABI group cannot form
@@ -1679,10 +1682,10 @@ def main() -> None:
         if rank == 0:
             out.setdefault("extra", {})["resources"] = res
 
-    if cabi_pending:
+    if exchange_pending:
         cabi_legs(out["extra"], gather_leg, degraded_gather, enc, (k, m, F), world, rank, dev,
                   args.cabi_deadline, lambda: print(json.dumps(out), flush=True) if rank == 0
-                  else None)
+                  else None, torch_legs=True, cabi=cabi_pending)
 
     if world > 1:
         dist.barrier()
