@@ -256,3 +256,25 @@ def test_cabi_legs_error_is_reported():
     assert ex["degraded_gather_cabi"]["error"] == "RuntimeError: cec_dist_create: no RCCL"
     line = {"config": {"baseline_config": 2}, "n_gpus": 2, "extra": ex}
     assert any("cec_dist_create: no RCCL" in p for p in bench.line_problems(line))
+
+
+def test_exchange_legs_torch_error_then_cabi():
+    """The N > 1 line's exchange legs (torch group first, then the C ABI) under one watchdog: a
+    torch-group leg that raises is recorded as an error and the C-ABI legs still run."""
+    import torch
+    ex = {}
+
+    def gather(*a, **k):
+        via = a[9] if len(a) > 9 else k.get("transport", "torch")
+        if via == "torch":
+            raise RuntimeError("NCCL error: unhandled system error")
+        return {"bit_exact": True, "via": via}
+
+    bench.cabi_legs(ex, lambda g, **k: dict(g), gather, None, (2, 1, 4096), 1, 0,
+                    torch.device("cpu"), 30.0, lambda: None, torch_legs=True)
+    assert "NCCL error" in ex["degraded_gather"]["error"]
+    assert "NCCL error" in ex["wide_degraded_gather"]["error"]
+    assert ex["degraded_gather_cabi"]["via"] == "cabi"
+    assert ex["degraded_gather_cabi"]["transport"].startswith("libcessec")
+    # (the wide legs build an RS(32,32) codec, which needs a GPU: on CPU they record that error)
+    assert "NCCL error" not in json.dumps(ex["wide_degraded_gather_cabi"])
