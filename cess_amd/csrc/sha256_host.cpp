@@ -27,6 +27,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -544,7 +545,8 @@ struct Pool {
   // chains of 16 MiB on two x16 registers take 48 ms, on 16 cores' SHA-NI 9 ms) gives the
   // surplus back; idle workers pick it up at once, the others at their next step. (under mu)
   void rebalance(Lane* L, int& n) {
-    if (n <= 1 || idle == 0 || avail) return;
+    static const bool off = getenv("CEC_HOST_SHA_NO_SPILL") != nullptr;  // A/B measurements
+    if (off || n <= 1 || idle == 0 || avail) return;
     const size_t fair = std::max<size_t>(1, (lanes_busy + th.size() - 1) / th.size());
     if ((size_t)n <= fair) return;
     // keep the lanes closest to their end; give back the longest

@@ -16,11 +16,14 @@
  *   -2 = host only: print the plan's shape (and whether the stand-in was loaded), no GPU.
  *   GROUP_OPS: CEC_DIST_OPT_GROUP_OPS (transfers per rank per RCCL group; default: the library's).
  * prints one line "world_n ok ..." on success, "FAIL ..." lines otherwise (exit 1). */
+#include <execinfo.h>
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "cess_ec.h"
 
@@ -186,7 +189,21 @@ static void* rank_main(void* arg) {
   return (void*)(long)(ret != 0);
 }
 
+/* a crash names where it happened (stderr), so one failure is enough to find its cause */
+static void on_fatal(int sig) {
+  static const char msg[] = "dist_world_n: fatal signal, backtrace:\n";
+  void* frames[64];
+  const int nf = backtrace(frames, 64);
+  (void)!write(2, msg, sizeof msg - 1);
+  backtrace_symbols_fd(frames, nf, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 int main(int argc, char** argv) {
+  signal(SIGSEGV, on_fatal);
+  signal(SIGBUS, on_fatal);
+  signal(SIGABRT, on_fatal);
   if (argc != 8 && argc != 9) {
     fprintf(stderr, "usage: %s WORLD K M NSEG F EXCHANGE ABORT_RANK [GROUP_OPS]\n", argv[0]);
     return 2;

@@ -61,7 +61,7 @@ struct Shared {
   int arrived = 0;
   std::vector<std::vector<uint8_t>> contrib;
   std::vector<uint8_t> result;
-  // every event the group created; destroyed (after completion) when the last rank leaves
+  // every event the group created (see release(): kept for the life of the process)
   std::vector<hipEvent_t> events;
 };
 
@@ -237,16 +237,14 @@ ncclResult_t enqueue(bool send, const void* buf, size_t count, ncclDataType_t t,
 
 void release(ncclComm_t comm) {
   std::shared_ptr<Shared> sh = comm->sh;
-  std::vector<hipEvent_t> evs;
   {
     std::lock_guard<std::mutex> lk(sh->mu);
-    if (--sh->refs == 0) evs.swap(sh->events);
-  }
-  // the group's last rank: its events complete before they are destroyed (each waits for its
-  // own recorded work only, not the device)
-  for (hipEvent_t e : evs) {
-    (void)hipEventSynchronize(e);
-    (void)hipEventDestroy(e);
+    // The group's events are not destroyed here: they were recorded on the ranks' streams, and
+    // by the time the last rank leaves, the other ranks may have destroyed those streams (their
+    // work complete). Synchronizing such an event can make HIP re-read its recording queue (a
+    // SIGSEGV seen once in the world-8 case, profiles/r06/gpu_tests_check3.log), and a few
+    // hundred events per test process are not worth the risk: they live until the process ends.
+    --sh->refs;
   }
   std::lock_guard<std::mutex> lk(g_reg_mu);
   auto it = g_reg.find(comm->key);
