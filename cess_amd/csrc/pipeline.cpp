@@ -420,7 +420,25 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
   size_t cur = 0;  // source being read
   if (nsrc) files[0].t0 = t0;
   // per-batch wall time of the source reads so far (hybrid placement of the last batches)
-  double interval = (double)(p->B * p->SB) / 45e9, last_batch_t = t0;
+  double sec_per_byte = 1.0 / 45e9, last_batch_t = t0;
+  // Batch sizes. A full batch is B segments; the run's first batches ramp up (B/8, B/4, B/2:
+  // the first copy, encode and host hashes start after a short read instead of a whole batch),
+  // and the last source's last 2B segments, when its size is known, go in halves down to B/8 (the
+  // last parity copy and hashes drain after a short batch). The records do not depend on it.
+  const bool ramp = p->B >= 8 && !getenv("CEC_PIPELINE_NO_RAMP");
+  auto batch_bytes = [&](uint64_t idx, size_t src, uint64_t src_read) -> size_t {
+    size_t segs = p->B;
+    if (ramp && idx < 3) segs = p->B >> (3 - idx);
+    if (ramp && src + 1 == nsrc && srcs[src].size > src_read) {
+      const uint64_t left = (srcs[src].size - src_read + p->SB - 1) / p->SB;
+      if (left <= 2 * p->B) {  // halves of what is left, none under B/8
+        uint64_t want = std::max<uint64_t>(p->B / 8, (left + 1) / 2);
+        if (left - want < p->B / 8 && left <= p->B) want = left;
+        segs = std::min<size_t>(segs, (size_t)want);
+      }
+    }
+    return segs * p->SB;
+  };
   const double gpu_chain_s =
       (double)cec::sha256_blocks(p->F) * kGpuChainSecondsPerBlock;
   std::vector<uint8_t> rec(64 * (size_t)n);
@@ -541,7 +559,7 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
     if (i >= (uint64_t)p->depth) PL_RC(host_through(i - p->depth));
     // read the next batch of the current source into pinned memory (overlaps the GPU work)
     uint8_t* dst = p->h_in[hs];
-    const size_t cap = p->B * p->SB;
+    const size_t cap = batch_bytes(i, cur, files[cur].bytes);
     size_t got = 0;
     const double r0 = now_s();
     while (got < cap) {
@@ -569,11 +587,12 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
     bool host_frags = p->mode == CEC_PIPE_HASH_HOST;
     if (p->mode == CEC_PIPE_HASH_HYBRID && cur + 1 == nsrc && srcs[cur].size) {
       const uint64_t size = srcs[cur].size, after = fs.bytes + got;
-      const uint64_t left = size > after ? (size - after + cap - 1) / cap : 0;  // batches after
-      if (p->tail_batches >= 0)
-        host_frags = left < (uint64_t)p->tail_batches;
-      else  // auto: the GPU's chains would finish after the source's remaining batches land
-        host_frags = (double)(left + 1) * interval < gpu_chain_s;
+      const uint64_t left_bytes = size > after ? size - after : 0;
+      const uint64_t full = p->B * p->SB;
+      if (p->tail_batches >= 0)  // full batches after this one
+        host_frags = (left_bytes + full - 1) / full < (uint64_t)p->tail_batches;
+      else  // auto: the GPU's chains would finish after the source's remaining bytes land
+        host_frags = (double)(left_bytes + got) * sec_per_byte < gpu_chain_s;
     }
     if (i >= (uint64_t)p->nd) {
       // device slot ds: its previous batch's parity read out and (hashing) its hex copied out
@@ -616,7 +635,7 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
       PL_RC(cec_hashq_tick(p->hq, p->tick_blocks));
     }
     const double tb = now_s();
-    interval = 0.5 * interval + 0.5 * (tb - last_batch_t);
+    sec_per_byte = 0.5 * sec_per_byte + 0.5 * (tb - last_batch_t) / (double)got;
     last_batch_t = tb;
     // deliver whatever has completed, without blocking (a slot's event re-recorded by a newer
     // batch completes later on the same stream, so a query of it is conservative)
