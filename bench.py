@@ -933,7 +933,7 @@ def config4_leg(dev, local: int, world: int, rank: int, backend: str, reps: int 
 
 def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
                  gib_per_rank: int = 8, stream_files: int = 4,
-                 stream_segments: int = 1000, reps: int = 3) -> dict:
+                 stream_segments: int = 1000, reps: int = 5) -> dict:
     """The host-resident path at every N (PCIe-inclusive; never `value`): every rank streams its
     own synthetic in-memory file (`gib_per_rank` GiB of 16 MiB segments, RS(2,1)) through
     libcessec's C pipeline (cec_pipeline_*: pinned host ring, H2D / encode / D2H on three HIP
