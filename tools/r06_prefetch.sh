@@ -1,5 +1,6 @@
 #!/bin/bash
-# Host SHA x16: software prefetch distance A/B (CEC_HOST_SHA_PREFETCH bytes ahead per lane).
+# Host SHA x16: software prefetch distance A/B (CEC_HOST_SHA_PREFETCH bytes ahead per lane; the
+# knob existed for this measurement only and was removed after it: profiles/r06/prefetch_ab/).
 set -o pipefail
 OUT=gpurun_out/r06pf; rm -rf $OUT; mkdir -p $OUT
 for pf in 0 256 512 1024 2048 0; do
