@@ -523,37 +523,48 @@ __device__ __forceinline__ void sha_tick_produce(u32x4* __restrict__ ring, int l
                                                  uint64_t len, uint32_t nblk, uint32_t trips) {
   const uint8_t* src = live ? ch_->src : nullptr;
   const bool al16 = live && ((uintptr_t)src & 15) == 0;
-  // Fast phase: blocks every lane of the wave has as aligned message data (the bulk of a
-  // tick), one wave-uniform loop with the next block's loads in flight. General phase: the
-  // rest (padding blocks, unaligned buffers, lanes that are done), loaded directly.
+  // Fast blocks: this lane's aligned message data in this tick (the bulk of a tick), loaded with
+  // the next PF blocks in flight. The count is per lane: the 64 chains of a group come from
+  // adds of any size, so they may differ in length and progress (a finished chain beside a
+  // running one). The wave runs the fast loop for its longest run; a lane past its own runs the
+  // general path (padding blocks, unaligned buffers) or writes zeros, masked. (A wave-uniform
+  // count, the minimum over the lanes, sent every chain of a group that held a finished one
+  // through the byte-wise general path: 3x slower ticks, profiles/r06/gpumode_ramp/.)
   const uint64_t dat = blk0 < nfull ? nfull - blk0 : 0;
   const uint32_t mine = al16 ? (uint32_t)(dat < nblk ? dat : nblk) : 0u;
-  const uint32_t nfast = __builtin_amdgcn_readfirstlane(wave_min_u32(live ? mine : ~0u));
-  // lanes past n take no part in nfast; their loads are masked off
+  const uint32_t nfast = __builtin_amdgcn_readfirstlane(wave_max_u32(mine));
   // nx[j] holds block b + j: PF blocks of loads in flight ahead of the one being expanded
   u32x4 nx[PF][4] = {};
 #pragma unroll
   for (int j = 0; j < PF; ++j)
-    if ((uint32_t)j < nfast && live) {
+    if ((uint32_t)j < mine) {
       const uint8_t* p = src + ((blk0 + j) << 6);
 #pragma unroll
       for (int q = 0; q < 4; ++q) nx[j][q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
     }
   auto slot = [&](uint32_t blk) CEC_SHA_AI { return ring + (blk & 1) * 16 * QS + lane; };
-  auto expand = [&](u32x4 (&v)[4], uint32_t blk) CEC_SHA_AI {
+  auto produce = [&](u32x4 (&v)[4], uint32_t blk) CEC_SHA_AI {
     uint32_t w[16];
+    if (blk < mine) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      w[4 * q + 0] = __builtin_bswap32(v[q].x);
-      w[4 * q + 1] = __builtin_bswap32(v[q].y);
-      w[4 * q + 2] = __builtin_bswap32(v[q].z);
-      w[4 * q + 3] = __builtin_bswap32(v[q].w);
-    }
-    const uint32_t nb_next = blk + PF;
-    if (nb_next < nfast && live) {
-      const uint8_t* p = src + ((blk0 + nb_next) << 6);
+      for (int q = 0; q < 4; ++q) {
+        w[4 * q + 0] = __builtin_bswap32(v[q].x);
+        w[4 * q + 1] = __builtin_bswap32(v[q].y);
+        w[4 * q + 2] = __builtin_bswap32(v[q].z);
+        w[4 * q + 3] = __builtin_bswap32(v[q].w);
+      }
+      const uint32_t nb_next = blk + PF;
+      if (nb_next < mine) {
+        const uint8_t* p = src + ((blk0 + nb_next) << 6);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+        for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const u32x4*>(p + 16 * q);
+      }
+    } else if (blk < nblk) {
+      // staged in the ring buffer this block is about to be written to (consumed at blk - 2)
+      sha_block_general(w, src, blk0 + blk, nfull, r, nb, len, slot(blk), QS);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) w[q] = 0;
     }
     sha_expand_store<QS>(w, slot(blk));
     __syncthreads();
@@ -561,18 +572,17 @@ __device__ __forceinline__ void sha_tick_produce(u32x4* __restrict__ ring, int l
   uint32_t b = 0;
   for (; b + PF <= nfast; b += PF) {
 #pragma unroll
-    for (int j = 0; j < PF; ++j) expand(nx[j], b + j);
+    for (int j = 0; j < PF; ++j) produce(nx[j], b + j);
   }
 #pragma unroll
   for (int j = 0; j < PF; ++j)
     if (b < nfast) {
-      expand(nx[j], b);
+      produce(nx[j], b);
       ++b;
     }
-  for (; b < trips; ++b) {
+  for (; b < trips; ++b) {  // past every lane's fast run
     uint32_t w[16];
     if (b < nblk) {
-      // staged in the ring buffer this block is about to be written to (consumed at b - 2)
       sha_block_general(w, src, blk0 + b, nfull, r, nb, len, slot(b), QS);
     } else {
 #pragma unroll
