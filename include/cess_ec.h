@@ -223,7 +223,7 @@ int cec_split_segment(const uint8_t* seg, size_t seg_len, int k, uint8_t* const*
  *                         other fragments' chains on the GPU queue, except for the last batches
  *                         of the run's last source, which the host hashes wholly (`tail_batches`;
  *                         -1 = auto: the batches whose GPU chains would finish after the source's
- *                         remaining batches have landed; needs the source's size).
+ *                         remaining bytes have landed; needs the source's size).
  * The pipeline is reusable: keep one for many files (its pinned ring is pinned once).
  *   read(user, dst, cap): write up to cap source bytes at dst; return the count, 0 at the end,
  *     < 0 to abort (CEC_ECALLBACK).
@@ -243,7 +243,9 @@ typedef int (*cec_record_fn)(void* user, uint64_t seg, const uint8_t* seg_hex,
                              const uint8_t* frag_hex);
 typedef struct cec_pipeline_opts {
   size_t shard_len;      /* F: a segment is k * F bytes */
-  size_t batch_segments; /* segments per batch (0: 64) */
+  size_t batch_segments; /* segments per full batch (0: 64); a run's first three batches are
+                            1/8, 1/4, 1/2 of it and the last source's last ones halve down to
+                            1/8 when its size is known (B >= 8; the records do not change) */
   int depth;             /* pinned host batches (0: 3, host / hybrid hashing 4; >= 2) */
   int hash;              /* CEC_PIPE_HASH_*: 0 none, 1 GPU, 2 host, 3 hybrid */
   int window;            /* batches hashing at once on the GPU queue (0: 32); the pipeline
