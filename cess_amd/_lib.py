@@ -77,6 +77,7 @@ SIGNATURES = {
                                 c_void_p, c_int]),
     "cec_host_sha_set_form": (c_int, [c_int]),
     "cec_host_sha_form": (c_int, []),
+    "cec_host_sha_pool_threads": (c_int, []),
     "cec_host_sha_probe": (c_double, [c_int, c_size_t, c_int]),
     "cec_split_segment": (c_int, [c_void_p, c_size_t, c_int, POINTER(c_void_p), c_size_t]),
     "cec_fill_synthetic": (c_int, [c_void_p, c_size_t, c_size_t, c_uint64, c_uint64, c_void_p]),

@@ -44,6 +44,12 @@ bool ready(const std::shared_ptr<JobState>& js);
 // Block until the job is done (the second argument is unused: the workers do all hashing).
 void wait(const std::shared_ptr<JobState>& js, bool help);
 
+// Thread reservations of long-lived users (a host-hashing pipeline reserves its host_threads at
+// creation, releases them at destruction): the pool grows to the sum of the live reservations.
+void reserve_threads(int n);
+void release_threads(int n);
+int pool_threads();
+
 // Cumulative counters of the pool's workers (diagnostics: the pipeline's CEC_PIPELINE_TRACE).
 struct PoolStats {
   double busy_s = 0;          // worker time spent hashing

@@ -86,6 +86,7 @@ struct cec_pipeline {
   int depth = 0, nd = 0, window = 0;
   int mode = CEC_PIPE_HASH_NONE;
   int host_threads = 16, tail_batches = -1;
+  bool threads_reserved = false;  // host_threads reserved in the host SHA pool
   uint64_t max_segments = 0;
   // pinned host ring
   std::vector<uint8_t*> h_in, h_par;
@@ -129,6 +130,7 @@ struct cec_pipeline {
     for (hipStream_t s : {s_h2d, s_comp, s_d2h})
       if (s) (void)hipStreamSynchronize(s);
     wait_host_jobs();
+    if (threads_reserved) hsha::release_threads(host_threads);
     if (hq) cec_hashq_destroy(hq);
     for (auto* v : {&h_in, &h_par, &h_shex, &h_fhex})
       for (uint8_t* p : *v)
@@ -162,6 +164,10 @@ struct cec_pipeline {
     window = o.window ? o.window : 32;
     if (window < 1) return cec::set_error(CEC_EINVAL, "window must be >= 1");
     host_threads = o.host_threads > 0 ? o.host_threads : 16;
+    if (host_hash()) {  // the pool holds every live pipeline's threads (one per GPU in a process)
+      hsha::reserve_threads(host_threads);
+      threads_reserved = true;
+    }
     tail_batches = o.tail_batches;
     max_segments = o.max_segments;
     PL_TRY(hipSetDevice(device));

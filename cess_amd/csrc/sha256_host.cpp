@@ -500,8 +500,10 @@ struct Pool {
     cv.notify_all();
     for (auto& t : th) t.join();
   }
+  int reserved = 0;  // threads the live pipelines asked for (reserve_threads), summed
   void grow(int n) {
     std::lock_guard<std::mutex> l(mu);
+    n = std::max(n, reserved);
     while ((int)th.size() < n) th.emplace_back([this] { loop(); });
   }
   // (under mu) chains of x16 jobs into free lanes. With enough chains for every worker to fill
@@ -682,6 +684,28 @@ PoolStats stats() {
   return s;
 }
 
+// Several pipelines in one process (one per GPU, encode_file_records_multi) each bring their own
+// thread count: the pool holds their sum, not the largest one. Threads are never ended; a
+// released reservation leaves them idle.
+void reserve_threads(int n) {
+  Pool& P = pool();
+  {
+    std::lock_guard<std::mutex> l(P.mu);
+    P.reserved += std::max(0, n);
+  }
+  P.grow(0);
+}
+void release_threads(int n) {
+  Pool& P = pool();
+  std::lock_guard<std::mutex> l(P.mu);
+  P.reserved = std::max(0, P.reserved - std::max(0, n));
+}
+int pool_threads() {
+  Pool& P = pool();
+  std::lock_guard<std::mutex> l(P.mu);
+  return (int)P.th.size();
+}
+
 void set_form(int form) { g_form.store(form); }
 int get_form() { return best_form(); }
 bool supported(int form) { return form_supported(form); }
@@ -721,6 +745,8 @@ int cec_host_sha_set_form(int form) {
 }
 
 int cec_host_sha_form(void) { return hsha::get_form(); }
+
+int cec_host_sha_pool_threads(void) { return hsha::pool_threads(); }
 
 double cec_host_sha_probe(int form, size_t bytes_per_chain, int chains) {
   if (!hsha::supported(form) || chains < 1) return -1.0;

@@ -154,6 +154,10 @@ int cec_sha256_host(const uint8_t* const* bufs, size_t n, size_t len, uint8_t* h
 #define CEC_HSHA_X16 4
 int cec_host_sha_set_form(int form);
 int cec_host_sha_form(void);
+/* Worker threads of the process-wide host SHA-256 pool: grown to the largest `threads` a call
+ * asked for, and to the sum of the host_threads of the live host / hybrid pipelines (several
+ * pipelines, one per GPU, each bring their own CPU share). */
+int cec_host_sha_pool_threads(void);
 double cec_host_sha_probe(int form, size_t bytes_per_chain, int chains);
 
 /* Hash queue: streaming SHA-256 of many long device buffers (fragment and segment hashes).

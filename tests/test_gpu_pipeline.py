@@ -303,3 +303,27 @@ def test_pipeline_random_shapes(orc, k, m, F, nseg, tail, batch, depth, window, 
     assert seen == list(range(nsegs)) and st.segments == nsegs
     if hashing:
         assert [recs[s] for s in range(nsegs)] == [(h, list(fl)) for h, fl in want]
+
+
+@pytest.mark.gpu
+def test_host_sha_pool_holds_every_pipelines_threads(orc):
+    """Several host-hashing pipelines in one process (one per GPU in encode_file_records_multi)
+    each bring their own host_threads: the process-wide host SHA-256 pool grows to their sum
+    (cec_host_sha_pool_threads), not to the largest; records stay equal to the oracle's."""
+    from cess_amd import _lib
+    from cess_amd.pipeline import RecordsSession, encode_file_records_multi
+    lib = _lib.load()
+    t0 = lib.cec_host_sha_pool_threads()
+    seg = 1 << 20
+    blob = np.random.default_rng(9).integers(0, 256, 6 * seg + 5, dtype=np.uint8).tobytes()
+    want = orc.segment_list(blob, 2, 1, seg)
+    with RecordsSession(2, 1, seg, 0, "hybrid", batch_segments=2, window=2,
+                        host_threads=t0 + 5) as a, \
+            RecordsSession(2, 1, seg, 0, "host", batch_segments=2, host_threads=7) as b:
+        assert lib.cec_host_sha_pool_threads() >= t0 + 12
+        for ses in (a, b):
+            rec, _ = ses.encode(blob)
+            assert [(x.hash, x.fragment_list) for x in rec.segments] == want
+    rec, _ = encode_file_records_multi(blob, [0, 0], 2, 1, seg, hash_on="hybrid",
+                                       hash_threads=4, window=2)
+    assert [(x.hash, x.fragment_list) for x in rec.segments] == want

@@ -103,6 +103,7 @@ extern "C" {
                            prefix_len: usize, prefix_hex: *mut u8, threads: c_int) -> c_int;
     pub fn cec_host_sha_set_form(form: c_int) -> c_int;
     pub fn cec_host_sha_form() -> c_int;
+    pub fn cec_host_sha_pool_threads() -> c_int;
     pub fn cec_host_sha_probe(form: c_int, bytes_per_chain: usize, chains: c_int) -> f64;
     pub fn cec_scale_deal_info(seg_hex: *const u8, frag_hex: *const u8, nseg: usize,
                                nfrag: usize, out: *mut u8, out_cap: usize,
