@@ -994,16 +994,31 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
            "file_bytes_per_gpu": nseg * seg_bytes, "n_gpus": world,
            "basis": "file bytes of all ranks / max over ranks of the run (barrier to barrier); "
                     "PCIe Gen5 x16 = 63 GB/s per direction per GPU; pipelines created and warmed "
-                    "up before the timed runs; seconds = the median of `runs_s`"}
-    def timed_runs(run):
+                    "up before the timed runs; seconds = the median of `runs_s`; cpu_s_runs / "
+                    "cpu_s = rank 0's process CPU seconds per run (every thread: readers, host "
+                    "SHA-256 pool)"}
+    import resource
+
+    def cpu_s() -> float:  # this process's CPU time, every thread (readers, host SHA pool)
+        r = resource.getrusage(resource.RUSAGE_SELF)
+        return r.ru_utime + r.ru_stime
+
+    cpu_runs = {}
+
+    def timed_runs(run, key=None):
         """`reps` timed runs, each barrier to barrier and max over ranks; (median s, all s,
-        last result)."""
-        ts, res = [], None
+        last result). With `key`, rank 0's CPU seconds per run go to cpu_runs[key]."""
+        ts, cs, res = [], [], None
         for _ in range(reps):
             barrier()
+            c0 = cpu_s()
             t0 = time.perf_counter()
             res = run()
-            ts.append(reduce_max(time.perf_counter() - t0))
+            dt = time.perf_counter() - t0
+            cs.append(round(cpu_s() - c0, 3))
+            ts.append(reduce_max(dt))
+        if key:
+            cpu_runs[key] = cs
         return sorted(ts)[len(ts) // 2], [round(t, 4) for t in ts], res
 
     # ranks sharing one GPU (the CESS_DEVICE rehearsal) split its HBM: the hash windows shrink
@@ -1019,9 +1034,9 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
         with Pipeline(enc, F, batch_segments=64, depth=3, hash=hashing, window=gpu_window) as p:
             p.run(buf[:64 * seg_bytes])  # warm-up: pinned ring, device slots, hash queue
             on_rec = (lambda s, sh, fl: recs.__setitem__(s, (sh, fl))) if hashing else None
-            t, runs, st = timed_runs(lambda: p.run(buf, on_record=on_rec))
+            t, runs, st = timed_runs(lambda: p.run(buf, on_record=on_rec), name)
         out[name] = {"seconds": round(t, 4), "runs_s": runs, "segments": int(st.segments),
-                     **rate(t)}
+                     "cpu_s_runs": cpu_runs[name], **rate(t)}
         if hashing:
             out[name]["hash_on"] = "gpu"
     enc.close()
@@ -1037,9 +1052,10 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
         with RecordsSession(k, m, seg_bytes, local, mode, batch_segments=64,
                             host_threads=16, window=hybrid_window) as ses:
             ses.encode(buf[:64 * seg_bytes])  # warm-up
-            t, runs, (rec, st) = timed_runs(lambda: ses.encode(buf))
+            t, runs, (rec, st) = timed_runs(lambda: ses.encode(buf), name)
             info = ses.pipe.info()
             leg = {"seconds": round(t, 4), "runs_s": runs, "segments": len(rec.segments),
+                   "cpu_s_runs": cpu_runs[name],
                    "hash_threads": 16,
                    "host_sha_form": {0: "scalar", 1: "sha-ni x1", 2: "sha-ni x2",
                                      3: "sha-ni x4", 4: "avx-512 x16"}.get(
@@ -1056,10 +1072,12 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
                     left -= take
                 done_t = []
                 barrier()
+                c1 = cpu_s()
                 t1 = time.perf_counter()
                 srecs, sst = ses.encode_many([pieces] * stream_files, on_file=lambda f, r, fs:
                                              done_t.append(time.perf_counter() - t1))
                 ts = time.perf_counter() - t1
+                cs = round(cpu_s() - c1, 3)
                 barrier()
                 sok = all(len(r.segments) == stream_segments for r in srecs)
                 for r in srecs:  # segment s of a stream file is buffer segment s % nseg
@@ -1071,7 +1089,8 @@ def host_e2e_leg(dev, local: int, world: int, rank: int, backend: str,
                 out["records_stream"] = {
                     "files": stream_files, "segments_per_file": stream_segments,
                     "file_bytes": per, "seconds": round(tsm, 4),
-                    "file_done_s": [round(x, 3) for x in done_t], **rate(tsm, stream_files * per),
+                    "file_done_s": [round(x, 3) for x in done_t], "cpu_s": cs,
+                    **rate(tsm, stream_files * per),
                     "records_per_file": True, "hash_on": "hybrid",
                     "records_equal_gpu_hashed_sampled": bool(not reduce_max(0.0 if sok else 1.0))}
         leg.update(rate(t))
