@@ -24,8 +24,10 @@ def main():
     ap.add_argument("--mib", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--probe-only", action="store_true")
+    ap.add_argument("--lib", default=os.path.join(ROOT, "cess_amd", "libcessec.so"))
+    ap.add_argument("--forms", default="1,2,3,4", help="forms timed through cec_sha256_host")
     a = ap.parse_args()
-    lib = ctypes.CDLL(os.path.join(ROOT, "cess_amd", "libcessec.so"))
+    lib = ctypes.CDLL(a.lib)
     lib.cec_host_sha_probe.restype = ctypes.c_double
     lib.cec_host_sha_probe.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int]
     lib.cec_sha256_host.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
@@ -66,7 +68,7 @@ def main():
             want = got
             print(json.dumps({"form": "hashlib", "threads": th, "chain_MiB": chain >> 20,
                               "GBps": round(total / best / 1e9, 2)}), flush=True)
-            for form in range(1, 5):
+            for form in [int(f) for f in a.forms.split(",")]:
                 if lib.cec_host_sha_set_form(form):
                     continue
                 best = 1e9
