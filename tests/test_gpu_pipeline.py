@@ -327,3 +327,49 @@ def test_host_sha_pool_holds_every_pipelines_threads(orc):
     rec, _ = encode_file_records_multi(blob, [0, 0], 2, 1, seg, hash_on="hybrid",
                                        hash_threads=4, window=2)
     assert [(x.hash, x.fragment_list) for x in rec.segments] == want
+
+
+def _sharded_rank(rank, world, port, path, seg, q):
+    import os
+    import torch.distributed as dist
+    from cess_amd.segments import encode_file_sharded
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rec = encode_file_sharded(path, rank, world, segment_size=seg, batch_segments=2, window=2)
+        q.put((rank, None if rec is None else
+               ([(s.hash, s.fragment_list) for s in rec.segments], rec.file_hash, rec.size)))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_encode_file_sharded_multi_process(orc, tmp_path, world):
+    """One process per rank (gloo group, every rank on GPU 0 here): each encodes its contiguous
+    segment range through its own RecordsSession (hybrid hashes), rank 0 gathers the SegmentLists
+    and returns the whole-file record, equal to the oracle's (segments, file hash, size)."""
+    import socket
+    import torch.multiprocessing as mp
+    seg = 1 << 20
+    blob = np.random.default_rng(31).integers(0, 256, 7 * seg + 333, dtype=np.uint8).tobytes()
+    path = tmp_path / "sharded.bin"
+    path.write_bytes(blob)
+    want = orc.segment_list(blob, 2, 1, seg)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_rank, args=(r, world, port, str(path), seg, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=150) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(res[r] is None for r in range(1, world))
+    segs, fh, size = res[0]
+    assert segs == want and fh == orc.file_hash(want) and size == len(blob)
