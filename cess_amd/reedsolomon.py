@@ -353,13 +353,15 @@ def xor_batch(d_dst, d_src, nsrc: int, src_stride: int, length: int, stream=None
                                     _stream_handle(stream)), "xor_batch")
 
 
-def sha256_hex_host(bufs, length: int, threads: int = 16) -> List[bytes]:
+def sha256_hex_host(bufs, length: int, threads: int = 16, prefix_len: int = 0):
     """SHA-256 hex of equal-length HOST buffers (numpy arrays / bytes-likes, or addresses) with
     libcessec's multi-chain host hasher (cec_sha256_host: 16 chains per core in AVX-512 lanes or
-    SHA-NI interleaved, on `threads` threads; the GIL is released during the call)."""
+    SHA-NI interleaved, on `threads` threads; the GIL is released during the call). With
+    `prefix_len` (a multiple of 64, <= length) returns (hexes, hexes of each buffer's first
+    prefix_len bytes): a segment chain yields data fragment 0's hash on the way."""
     n = len(bufs)
     if n == 0:
-        return []
+        return ([], []) if prefix_len else []
     keep = []
     ptrs = []
     for b in bufs:
@@ -374,10 +376,15 @@ def sha256_hex_host(bufs, length: int, threads: int = 16) -> List[bytes]:
         keep.append(a)
         ptrs.append(a.ctypes.data)
     out = np.zeros(n * 64, dtype=np.uint8)
+    pre = np.zeros(n * 64, dtype=np.uint8) if prefix_len else None
     arr = (c_void_p * n)(*ptrs)
-    check(_lib.load().cec_sha256_host(arr, n, length, out.ctypes.data, 0, None, threads),
+    check(_lib.load().cec_sha256_host(arr, n, length, out.ctypes.data, prefix_len,
+                                      pre.ctypes.data if prefix_len else None, threads),
           "sha256_hex_host")
-    return [out[i * 64:(i + 1) * 64].tobytes() for i in range(n)]
+    hexes = [out[i * 64:(i + 1) * 64].tobytes() for i in range(n)]
+    if prefix_len:
+        return hexes, [pre[i * 64:(i + 1) * 64].tobytes() for i in range(n)]
+    return hexes
 
 
 def sha256_hex_device(d_ptrs: Sequence[int], length: int) -> List[bytes]:

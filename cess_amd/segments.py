@@ -184,8 +184,8 @@ def encode_file_sharded(path: str, rank: int, world: int, group=None, **kw) -> O
 class SegmentEncoder:
     """Encode whole files into CESS fragments on one GPU.
 
-    hash_on = "host": SHA-256 on the host (hashlib / OpenSSL SHA-NI, `hash_threads` threads)
-    beside the GPU encode. hash_on = "gpu": every segment and fragment hash on the GPU through
+    hash_on = "host": SHA-256 on the host (libcessec's multi-chain host hasher, `hash_threads`
+    threads) beside the GPU encode. hash_on = "gpu": every segment and fragment hash on the GPU through
     the hash queue (cess_amd.hashq): each batch's chains are added after its encode and the
     queue is ticked once per batch, so `window` batches (window x batch_segments x (k+m+1)
     chains) hash together and a batch's records land `window` batches after its encode; the
@@ -214,7 +214,8 @@ class SegmentEncoder:
         self.hash_mode = hash_on
         self.wide = frags_per_batch >= 2048
         self.window = max(1, window)
-        self.pool = cf.ThreadPoolExecutor(max_workers=hash_threads)
+        self.hash_threads = hash_threads
+        self.pool = cf.ThreadPoolExecutor(max_workers=4)  # host SHA-256 jobs (their threads: C)
         self.io_threads = 8
         self.io_pool = cf.ThreadPoolExecutor(max_workers=self.io_threads)
         self.streams = [torch.cuda.Stream(self.dev) for _ in range(2)]
@@ -328,17 +329,21 @@ class SegmentEncoder:
 
     def _submit_host_hashes(self, slot: int, nseg: int):
         """Host path: segment and data-fragment hashes need only the host copy, so they start
-        as soon as the batch is read, beside the GPU work."""
+        as soon as the batch is read, beside the GPU work: one libcessec host SHA-256 job each
+        (cec_sha256_host, multi-chain) for the segment chains, which give data fragment 0's hash
+        as their prefix digest, and for the other data fragments."""
         if self.hash_on != "host":
             return None
+        from .reedsolomon import sha256_hex_host
         data = self.h_data[slot].numpy()
-        # segment hash and data fragment 0 share one stream (segment_and_first_fragment_hex)
-        seg_futs = [self.pool.submit(segment_and_first_fragment_hex,
-                                     [memoryview(data[s, i]) for i in range(self.k)])
-                    for s in range(nseg)]
-        dfuts = [[self.pool.submit(sha256_hex, memoryview(data[s, i])) for i in range(1, self.k)]
-                 for s in range(nseg)]
-        return seg_futs, dfuts
+        k, F, th = self.k, self.F, self.hash_threads
+        prefix = F if F % 64 == 0 else 0
+        seg_fut = self.pool.submit(sha256_hex_host, [data[s].reshape(-1) for s in range(nseg)],
+                                   self.seg, th, prefix)
+        d0 = 0 if prefix else 1  # without the prefix trick fragment 0 is hashed on its own
+        dfut = self.pool.submit(sha256_hex_host, [data[s, i] for s in range(nseg)
+                                                  for i in range(1 - d0, k)], F, th)
+        return seg_fut, dfut, prefix
 
     def _finish_encode(self, slot: int, nseg: int, seg_base: int, futs,
                        on_fragment: Optional[Callable]):
@@ -350,14 +355,17 @@ class SegmentEncoder:
         par = self.h_par[slot].numpy()
         recs = None
         if self.hash_on == "host":
-            seg_futs, dfuts = futs
-            pfuts = [[self.pool.submit(sha256_hex, memoryview(par[s, o])) for o in range(m)]
-                     for s in range(nseg)]
+            from .reedsolomon import sha256_hex_host
+            seg_fut, dfut, prefix = futs
+            phex = sha256_hex_host([par[s, o] for s in range(nseg) for o in range(m)], self.F,
+                                   self.hash_threads)
+            seg_res, dhex = seg_fut.result(), dfut.result()
+            shex, d0hex = seg_res if prefix else (seg_res, None)
+            nd = k - 1 if prefix else k  # data fragments hashed on their own, per segment
             recs = []
             for s in range(nseg):
-                seg_hex, d0_hex = seg_futs[s].result()
-                recs.append(SegmentList(seg_hex, [d0_hex] + [f.result() for f in dfuts[s]]
-                                        + [f.result() for f in pfuts[s]]))
+                frags = ([d0hex[s]] if prefix else []) + dhex[s * nd:(s + 1) * nd]
+                recs.append(SegmentList(shex[s], frags + phex[s * m:(s + 1) * m]))
         if on_fragment is not None:
             for s in range(nseg):
                 for i in range(k + m):

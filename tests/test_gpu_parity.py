@@ -462,6 +462,8 @@ def test_sha256_batch_matches_hashlib(torch, cess, sha_mode):
 
 @pytest.mark.parametrize("size,seg,k,m,hash_on,window", [
     (3 * (1 << 20) + 12345, 1 << 20, 2, 1, "host", 32),
+    (7 * (1 << 19) + 1, 1 << 19, 4, 2, "host", 1),
+    (11 * 3000 + 17, 3000, 3, 2, "host", 1),         # F = 1000: no prefix digest (F % 64 != 0)
     (5 * (1 << 20) + 7, 1 << 20, 2, 1, "gpu", 32),
     (9 * (1 << 20) + 7, 1 << 20, 2, 1, "gpu", 2),   # device slots reused (5 batches, window 2)
     (7 * (1 << 19) + 1, 1 << 19, 4, 2, "gpu", 1),

@@ -151,3 +151,17 @@ def test_greedy_lanes_then_tail_spill(lib):
             assert pre == [hashlib.sha256(b[:prefix]).hexdigest() for b in bufs]
     finally:
         lib.cec_host_sha_set_form(-1)
+
+
+def test_python_wrapper_prefix():
+    """cess_amd.sha256_hex_host with prefix_len: (hexes, prefix hexes), as SegmentEncoder uses it
+    for the segment chains (data fragment 0's digest on the way)."""
+    from cess_amd.reedsolomon import sha256_hex_host
+    rng = np.random.default_rng(4)
+    F = 64 * 50
+    segs = [rng.integers(0, 256, 2 * F, dtype=np.uint8) for _ in range(9)]
+    hexes, pre = sha256_hex_host(segs, 2 * F, 4, F)
+    assert hexes == [hashlib.sha256(s).hexdigest().encode() for s in segs]
+    assert pre == [hashlib.sha256(s[:F]).hexdigest().encode() for s in segs]
+    assert sha256_hex_host([], 10, 1, 64) == ([], [])
+    assert sha256_hex_host(segs[:2], 2 * F, 1) == hexes[:2]
