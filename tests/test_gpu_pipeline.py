@@ -366,10 +366,15 @@ def test_encode_file_sharded_multi_process(orc, tmp_path, world):
              for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=150) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    try:
+        res = dict(q.get(timeout=150) for _ in procs)
+    finally:  # a rank that failed leaves the others in the gather: end them (these PIDs only)
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    assert all(p.exitcode == 0 for p in procs)
     assert all(res[r] is None for r in range(1, world))
     segs, fh, size = res[0]
     assert segs == want and fh == orc.file_hash(want) and size == len(blob)
