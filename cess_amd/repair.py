@@ -66,11 +66,60 @@ def repair_fragment(enc: Encoder, survivors: Dict[int, np.ndarray], index: int,
 
 
 # Fragments to check at once from which the GPU's hash beats the host's: one SHA-256 chain per
-# fragment runs ~35 MB/s on a GPU lane (1.8 us per 64-byte block), so the GPU's time is flat up to
-# thousands of fragments (64 rebuilt 8 MiB fragments: 0.233 s), while the host's grows with the
-# count (8 threads: 0.140 s for the same 64, ~2.2 ms per fragment; the f2 row of
-# profiles/r02/aux_bench.jsonl, tools/aux_bench.py).
-AUTO_GPU_CHECK_FRAGMENTS = 128
+# fragment runs ~38 MB/s on a GPU lane (1.7 us per 64-byte block), so the GPU's time is flat up to
+# thousands of fragments (0.223-0.229 s for 64..1024 rebuilt 8 MiB fragments), while the host's
+# grows with the count: copied out in pinned chunks and hashed on 16 threads (cec_sha256_host)
+# as the chunks land, 0.020 / 0.059 / 0.105 / 0.208 s for 64 / 256 / 512 / 1024
+# (profiles/r06/repair_check_scale.jsonl, tools/repair_check_scale.py). Round 5's threshold of
+# 128 came from hashlib on 8 threads after one pageable copy-out (0.140 s for 64).
+AUTO_GPU_CHECK_FRAGMENTS = 1024
+
+
+# Host-side check staging: a ring of pinned chunk buffers kept between calls (pinning costs ~0.1 s
+# per GiB; a repair service checks batch after batch), CHECK_RING chunks of CHECK_CHUNK fragments.
+_STAGE = {}
+CHECK_CHUNK = 16
+CHECK_RING = 6
+
+
+def _host_check_hashes(frags, shard_len: int, threads: int, device) -> List[bytes]:
+    """SHA-256 hex of device fragments on host threads: copied out chunk by chunk into a ring of
+    pinned buffers on a side stream, each chunk hashed (cec_sha256_host) as soon as its copy lands
+    while the next chunks copy; the chunks' jobs share the host SHA pool's lanes. A ring buffer
+    is refilled once its previous chunk is hashed, so the pinned memory stays at CHECK_RING x
+    CHECK_CHUNK fragments whatever the batch."""
+    import concurrent.futures as cf
+    import torch
+    n = len(frags)
+    nchunks = -(-n // CHECK_CHUNK)
+    ring = min(CHECK_RING, nchunks)
+    need = ring * CHECK_CHUNK * shard_len
+    stage = _STAGE.get(device)
+    if stage is None or stage.numel() < need:
+        stage = torch.empty(need, dtype=torch.uint8, pin_memory=True)
+        _STAGE[device] = stage
+    bufs = stage[:need].view(ring, CHECK_CHUNK, shard_len)
+    st = torch.cuda.Stream(device)
+    st.wait_stream(torch.cuda.current_stream(device))
+
+    def check(c, ev):
+        ev.synchronize()
+        hv = bufs[c % ring].numpy()
+        return sha256_hex_host([hv[j] for j in range(min(CHECK_CHUNK, n - c * CHECK_CHUNK))],
+                               shard_len, threads)
+
+    futs = []
+    with cf.ThreadPoolExecutor(max_workers=ring) as ex:
+        for c in range(nchunks):
+            if c >= ring:
+                futs[c - ring].result()  # that ring buffer's chunk is hashed: reuse it
+            with torch.cuda.stream(st):
+                for j in range(c * CHECK_CHUNK, min(n, (c + 1) * CHECK_CHUNK)):
+                    bufs[c % ring][j - c * CHECK_CHUNK].copy_(frags[j], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(st)
+            futs.append(ex.submit(check, c, ev))
+        return [h for f in futs for h in f.result()]
 
 
 def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, present,
@@ -107,8 +156,7 @@ def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, pres
     elif hash_on == "gpu":
         got = sha256_hex_device([t.data_ptr() for t in frags], shard_len)
     else:
-        host = torch.stack(frags).cpu().numpy()
-        got = sha256_hex_host(list(host), shard_len, hash_threads)
+        got = _host_check_hashes(frags, shard_len, hash_threads, d_data.device)
     ok = [True] * nseg
     calls = {}
     for (s, i, h), g in zip(which, got):
