@@ -748,6 +748,27 @@ def test_repair_batch_wide(torch, cess, corc, orc):
         repair_batch(enc, dd, dp, nseg, F, present, expected, hash_on="tpu")
 
 
+def test_repair_batch_host_check_ring(torch, cess, corc, orc):
+    """The host-side check copies the rebuilt fragments out through a ring of pinned chunks
+    (repair.CHECK_RING x CHECK_CHUNK): a batch of many more fragments than the ring holds, with
+    a ragged last chunk and one wrong recorded hash deep in the batch."""
+    from cess_amd import repair
+    k, m, F, nseg = 2, 1, 4096 + 64, repair.CHECK_RING * repair.CHECK_CHUNK * 2 + 7
+    rng = np.random.default_rng(16)
+    data = rng.integers(0, 256, (nseg, k, F), dtype=np.uint8)
+    par = np.stack([np.stack(c_encode(corc, k, m, list(data[s]))) for s in range(nseg)])
+    present = np.ones((nseg, k + m), np.uint8)
+    present[np.arange(nseg), np.arange(nseg) % 3] = 0
+    expected = [{s % 3: orc.sha256_hex(data[s, s % 3] if s % 3 < k else par[s, 0])}
+                for s in range(nseg)]
+    expected[nseg - 20] = {(nseg - 20) % 3: b"f" * 64}
+    dd = to_dev(torch, data * present[:, :k, None])
+    dp = to_dev(torch, par * present[:, k:, None])
+    enc = cess.New(k, m)
+    ok = repair.repair_batch(enc, dd, dp, nseg, F, present, expected, hash_on="host")
+    assert ok == [s != nseg - 20 for s in range(nseg)]
+
+
 def test_repair_emits_completion_only_for_matching_hash(torch, cess, corc, orc):
     """The repair service reports a rebuilt fragment with restoral_order_complete(fragment_hash)
     (call 16, c-pallets/file-bank/src/lib.rs:1072-1122) only when its SHA-256 matched the
