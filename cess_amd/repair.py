@@ -167,17 +167,31 @@ def repair_batch(enc: Encoder, d_data, d_parity, nseg: int, shard_len: int, pres
 
 
 def generate_fillers(n: int, seed: int = 0xF111E5, filler_size: int = geometry.FRAGMENT_SIZE,
-                     first: int = 0, device: int = 0):
+                     first: int = 0, device: int = 0, hash_on: str = "auto",
+                     hash_threads: int = 16):
     """n idle fillers of `filler_size` bytes generated in HBM (splitmix64 counter stream,
     filler i = segment first+i of the generator) with their SHA-256 hex hashes (as
-    `upload_filler` records them), hashed on the GPU. Returns (device tensor [n][filler_size],
-    [hash])."""
+    `upload_filler` records them). Returns (device tensor [n][filler_size], [hash]). hash_on
+    "gpu": one chain per filler on the GPU (flat ~0.22 s for 8 MiB fillers up to thousands);
+    "host": copied out in pinned chunks and hashed on `hash_threads` host threads as they land
+    (the copy a miner uploading them makes anyway); "auto": the host below
+    AUTO_GPU_CHECK_FRAGMENTS fillers, as the repair check."""
     import torch
     from .reedsolomon import fill_synthetic
-    d = torch.empty((n, filler_size), dtype=torch.uint8, device=torch.device("cuda", device))
+    if hash_on not in ("gpu", "host", "auto"):
+        raise ValueError("hash_on must be 'gpu', 'host' or 'auto'")
+    dev = torch.device("cuda", device)
+    d = torch.empty((n, filler_size), dtype=torch.uint8, device=dev)
     fill_synthetic(d, filler_size, n, first, seed)
     torch.cuda.synchronize(device)
-    hashes = sha256_hex_device([d[i].data_ptr() for i in range(n)], filler_size) if n else []
+    if hash_on == "auto":
+        hash_on = "gpu" if n >= AUTO_GPU_CHECK_FRAGMENTS else "host"
+    if not n:
+        hashes = []
+    elif hash_on == "gpu":
+        hashes = sha256_hex_device([d[i].data_ptr() for i in range(n)], filler_size)
+    else:
+        hashes = _host_check_hashes([d[i] for i in range(n)], filler_size, hash_threads, dev)
     return d, hashes
 
 

@@ -831,10 +831,12 @@ def test_filler_upload_records(torch, orc):
     assert calls[1] == records.upload_filler(tee, fillers[10:])
 
 
-def test_generate_fillers(torch, orc):
+@pytest.mark.parametrize("hash_on", ["auto", "gpu", "host"])
+def test_generate_fillers(torch, orc, hash_on):
     from cess_amd.repair import generate_fillers
-    d, hashes = generate_fillers(3, filler_size=1 << 16, first=7)
-    for i in range(3):
+    n = 3 if hash_on != "host" else 40  # the host path through more than two pinned chunks
+    d, hashes = generate_fillers(n, filler_size=1 << 16, first=7, hash_on=hash_on)
+    for i in range(n):
         want = orc.synthetic_segment(0xF111E5, 7 + i, 1 << 16)
         assert np.array_equal(d[i].cpu().numpy(), want)
         assert hashes[i] == orc.sha256_hex(want)

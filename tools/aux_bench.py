@@ -96,10 +96,11 @@ def main():
                       "chunks_per_s": round(nfrag * len(idx) / t_h, 1)}), flush=True)
 
     out = {}
-    t_f = timed(lambda: out.update(r=repair.generate_fillers(nseg)))
-    print(json.dumps({"row": "f4 fillers", "fillers": nseg, "filler_bytes": F,
-                      "generate_and_hash_s": round(t_f, 4),
-                      "GBps": round(nseg * F / t_f / GB, 2)}), flush=True)
+    for on in ("gpu", "host"):
+        t_f = timed(lambda: out.update(r=repair.generate_fillers(nseg, hash_on=on)))
+        print(json.dumps({"row": "f4 fillers", "fillers": nseg, "filler_bytes": F,
+                          "hash_on": on, "generate_and_hash_s": round(t_f, 4),
+                          "GBps": round(nseg * F / t_f / GB, 2)}), flush=True)
     partial_row(args, torch, np, cess_amd, dev)
 
 
