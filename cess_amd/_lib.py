@@ -75,6 +75,8 @@ SIGNATURES = {
                                c_void_p]),
     "cec_sha256_host": (c_int, [POINTER(c_void_p), c_size_t, c_size_t, c_void_p, c_size_t,
                                 c_void_p, c_int]),
+    "cec_sha256_host_state": (c_int, [POINTER(c_void_p), c_size_t, c_size_t, c_void_p,
+                                      c_void_p, c_int]),
     "cec_host_sha_set_form": (c_int, [c_int]),
     "cec_host_sha_form": (c_int, []),
     "cec_host_sha_pool_threads": (c_int, []),
@@ -89,6 +91,9 @@ SIGNATURES = {
                               c_size_t, c_void_p, c_size_t, POINTER(c_uint64)]),
     "cec_hashq_add_prefix": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_size_t,
                                      c_size_t, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t,
+                                     POINTER(c_uint64)]),
+    "cec_hashq_add_resume": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_size_t,
+                                     c_size_t, c_size_t, c_void_p, c_void_p, c_size_t,
                                      POINTER(c_uint64)]),
     "cec_hashq_tick": (c_int, [c_void_p, c_uint32]),
     "cec_hashq_finish": (c_int, [c_void_p]),

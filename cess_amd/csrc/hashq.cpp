@@ -128,6 +128,34 @@ int cec_hashq_add_prefix(cec_hashq* q, const uint8_t* d_base, size_t n, size_t p
   return CEC_OK;
 }
 
+int cec_hashq_add_resume(cec_hashq* q, const uint8_t* d_base, size_t n, size_t per,
+                         size_t outer_stride, size_t inner_stride, size_t len, size_t start_len,
+                         const uint32_t* d_states, uint8_t* d_hex, size_t hex_outer,
+                         uint64_t* ticket) {
+  if (!q || (n && (!d_base || !d_states)) || per == 0)
+    return cec::set_error(CEC_EINVAL, "null or per == 0");
+  if (n > 0xFFFFFFFFull) return cec::set_error(CEC_EINVAL, "n too large");
+  if ((start_len & 63) || start_len > (len & ~(size_t)63))
+    return cec::set_error(CEC_EINVAL, "start_len must be a multiple of 64 within len's full blocks");
+  if (n == 0) {
+    if (ticket) *ticket = 0;
+    return CEC_OK;
+  }
+  if (q->tail + n - q->head > q->cap)
+    return cec::set_error(CEC_ENOMEM, "hash queue full: tick until chains complete");
+  HQ_TRY(hipSetDevice(q->device));
+  cec::launch_hashq_add(q->tab, q->cap - 1, q->tail, (uint32_t)n, d_base, (uint32_t)per,
+                        outer_stride, inner_stride, len, d_hex, hex_outer, 0, nullptr, 0,
+                        q->stream, d_states, start_len >> 6);
+  int rc = launched();
+  if (rc) return rc;
+  q->adds.push_back({q->tail, n, cec::sha256_blocks(len) - (start_len >> 6), 0, q->next_ticket});
+  q->tail += n;
+  if (ticket) *ticket = q->next_ticket;
+  ++q->next_ticket;
+  return CEC_OK;
+}
+
 int cec_hashq_add(cec_hashq* q, const uint8_t* d_base, size_t n, size_t per, size_t outer_stride,
                   size_t inner_stride, size_t len, uint8_t* d_hex, size_t hex_outer,
                   uint64_t* ticket) {

@@ -23,6 +23,9 @@ struct Job {
   size_t prefix_len = 0;
   uint8_t* prefix_hex = nullptr;
   size_t prefix_outer = 1;
+  // optional: the 8 state words of chain i after its full blocks (before the padding) to
+  // state_out + 8 i (a segment chain resumed elsewhere after its first len bytes)
+  uint32_t* state_out = nullptr;
 };
 
 struct JobState {

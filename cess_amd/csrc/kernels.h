@@ -158,7 +158,8 @@ __host__ __device__ inline uint64_t sha256_blocks(uint64_t len) { return (len >>
 void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
                       const uint8_t* base, uint32_t per, uint64_t outer, uint64_t inner,
                       uint64_t len, uint8_t* hex, uint64_t hex_outer, uint64_t pre_blk,
-                      uint8_t* pre_hex, uint64_t pre_hex_outer, hipStream_t st);
+                      uint8_t* pre_hex, uint64_t pre_hex_outer, hipStream_t st,
+                      const uint32_t* h0 = nullptr, uint64_t blk0 = 0);
 // Advance the n chains in slots head.. by at most max_blocks blocks each; tick_mode 0 lets `live`
 // (chains not yet complete among them) pick the kernel form, 1 or 2 = two waves with that many
 // blocks prefetched, 3 = one wave per 64 chains.

@@ -840,14 +840,16 @@ __global__ __launch_bounds__(256) void k_hashq_add(ShaChain* __restrict__ tab, u
                                                    uint64_t outer, uint64_t inner, uint64_t len,
                                                    uint8_t* hex, uint64_t hex_outer,
                                                    uint64_t pre_blk, uint8_t* pre_hex,
-                                                   uint64_t pre_hex_outer) {
+                                                   uint64_t pre_hex_outer,
+                                                   const uint32_t* __restrict__ h0,
+                                                   uint64_t blk0) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const uint32_t a = i / per, b = i % per;
   ShaChain c;
   c.src = base + a * outer + b * inner;
   c.len = len;
-  c.blk = 0;
+  c.blk = h0 ? blk0 : 0;
   c.hex = hex ? hex + (a * hex_outer + b) * 64 : nullptr;
   c.pre_blk = pre_hex ? pre_blk : 0;
   c.pre_hex = pre_hex ? pre_hex + (a * pre_hex_outer + b) * 64 : nullptr;
@@ -857,8 +859,10 @@ __global__ __launch_bounds__(256) void k_hashq_add(ShaChain* __restrict__ tab, u
   for (int q = 0; q < 2; ++q) c.pad_[q] = 0;
   const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                           0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  // resumed chains (h0): the state after the first blk0 blocks, computed elsewhere (the host
+  // hashing fragment 0 of a segment), 8 words per chain
 #pragma unroll
-  for (int q = 0; q < 8; ++q) c.h[q] = iv[q];
+  for (int q = 0; q < 8; ++q) c.h[q] = h0 ? h0[8 * (size_t)i + q] : iv[q];
   tab[(uint32_t)(slot0 + i) & mask] = c;
 }
 
@@ -885,11 +889,12 @@ void launch_sha256_hex(int sha_mode, const uint8_t* const* ptrs, const Layout* L
 void launch_hashq_add(ShaChain* tab, uint32_t mask, uint64_t slot0, uint32_t n,
                       const uint8_t* base, uint32_t per, uint64_t outer, uint64_t inner,
                       uint64_t len, uint8_t* hex, uint64_t hex_outer, uint64_t pre_blk,
-                      uint8_t* pre_hex, uint64_t pre_hex_outer, hipStream_t st) {
+                      uint8_t* pre_hex, uint64_t pre_hex_outer, hipStream_t st,
+                      const uint32_t* h0, uint64_t blk0) {
   if (n == 0) return;
   hipLaunchKernelGGL(k_hashq_add, dim3((n + 255) / 256), dim3(256), 0, st, tab, mask, slot0, n,
                      base, per, outer, inner, len, hex, hex_outer, pre_blk, pre_hex,
-                     pre_hex_outer);
+                     pre_hex_outer, h0, blk0);
 }
 
 // live chains below which the auto tick is the lane-pair form (three waves per 64 chains): at

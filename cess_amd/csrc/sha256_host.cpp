@@ -357,6 +357,8 @@ void hash_range(const Job& j, size_t c0, size_t n, int form) {
     }
     const size_t full = j.len / 64;
     blocks(f, st, p, gn, full - done);
+    if (j.state_out)
+      for (int c = 0; c < gn; ++c) std::memcpy(j.state_out + 8 * (g0 + c), state[c], 32);
     uint8_t pad[16][128];
     const uint8_t* pq[16];
     int nb = 1;
@@ -432,6 +434,7 @@ struct Lane {
   }
   void finish() {
     const Job& j = js->job;
+    if (j.state_out) std::memcpy(j.state_out + 8 * ci, st, 32);
     uint8_t pad[128];
     const int nb = pad_blocks(j.bufs[ci] + full * 64, j.len, pad);
     one_lane_blocks(st, pad, (size_t)nb);
@@ -725,6 +728,25 @@ int cec_sha256_host(const uint8_t* const* bufs, size_t n, size_t len, uint8_t* h
   j.hex = hex;
   j.prefix_len = prefix_hex ? prefix_len : 0;
   j.prefix_hex = prefix_hex;
+  if (threads <= 1) {
+    hsha::hash_range(j, 0, n, hsha::best_form());
+    return 0;
+  }
+  auto js = hsha::submit(j, threads);
+  hsha::wait(js, true);
+  return 0;
+}
+
+int cec_sha256_host_state(const uint8_t* const* bufs, size_t n, size_t len, uint8_t* hex,
+                          uint32_t* state_out, int threads) {
+  if (n && (!bufs || !hex || !state_out)) return CEC_EINVAL;
+  if (len % 64) return CEC_EINVAL;
+  hsha::Job j;
+  j.bufs = bufs;
+  j.n = n;
+  j.len = len;
+  j.hex = hex;
+  j.state_out = state_out;
   if (threads <= 1) {
     hsha::hash_range(j, 0, n, hsha::best_form());
     return 0;

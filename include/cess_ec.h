@@ -143,6 +143,11 @@ int cec_sha256_hex(const uint8_t* const* d_bufs, size_t n, size_t len, uint8_t* 
  * chain alone leaves most of a core's SHA throughput idle. Synchronous. Host only, no GPU. */
 int cec_sha256_host(const uint8_t* const* bufs, size_t n, size_t len, uint8_t* hex,
                     size_t prefix_len, uint8_t* prefix_hex, int threads);
+/* cec_sha256_host of buffers whose len is a multiple of 64 that also writes each chain's state
+ * after those len bytes (8 words, before the padding) to state_out + 8 i: fragment 0's hash and
+ * the state a segment chain resumes from on the GPU (cec_hashq_add_resume). */
+int cec_sha256_host_state(const uint8_t* const* bufs, size_t n, size_t len, uint8_t* hex,
+                          uint32_t* state_out, int threads);
 /* Forms of the host hasher: which one runs is process-wide (cec_host_sha_set_form; -1 restores
  * the default: AVX-512 x16 where the CPU has it, else SHA-NI x2 where it has SHA-NI).
  * cec_host_sha_probe times one form on the calling thread over `chains` chains of
@@ -191,6 +196,15 @@ int cec_hashq_add_prefix(cec_hashq* q, const uint8_t* d_base, size_t n, size_t p
                          size_t outer_stride, size_t inner_stride, size_t len, uint8_t* d_hex,
                          size_t hex_outer, size_t prefix_len, uint8_t* d_prefix_hex,
                          size_t prefix_hex_outer, uint64_t* ticket);
+/* cec_hashq_add of chains that resume after their first start_len bytes (a multiple of 64 within
+ * len's full blocks): chain i starts from the SHA-256 state d_states[8 i .. 8 i + 7] (device
+ * memory, the eight 32-bit words after start_len bytes, as cec_sha256_host_state gives them)
+ * and hashes bytes start_len .. len of its buffer. A segment chain continued on the GPU after
+ * the host hashed its fragment 0. */
+int cec_hashq_add_resume(cec_hashq* q, const uint8_t* d_base, size_t n, size_t per,
+                         size_t outer_stride, size_t inner_stride, size_t len, size_t start_len,
+                         const uint32_t* d_states, uint8_t* d_hex, size_t hex_outer,
+                         uint64_t* ticket);
 /* Advance every live chain by at most max_blocks 64-byte blocks (0 = to completion). */
 int cec_hashq_tick(cec_hashq* q, uint32_t max_blocks);
 /* Tick until every chain added so far is complete (enqueued; synchronise the stream to wait). */

@@ -165,3 +165,61 @@ def test_python_wrapper_prefix():
     assert pre == [hashlib.sha256(s[:F]).hexdigest().encode() for s in segs]
     assert sha256_hex_host([], 10, 1, 64) == ([], [])
     assert sha256_hex_host(segs[:2], 2 * F, 1) == hexes[:2]
+
+
+_K = [int(x, 16) for x in (
+    "428a2f98 71374491 b5c0fbcf e9b5dba5 3956c25b 59f111f1 923f82a4 ab1c5ed5 d807aa98 12835b01 "
+    "243185be 550c7dc3 72be5d74 80deb1fe 9bdc06a7 c19bf174 e49b69c1 efbe4786 0fc19dc6 240ca1cc "
+    "2de92c6f 4a7484aa 5cb0a9dc 76f988da 983e5152 a831c66d b00327c8 bf597fc7 c6e00bf3 d5a79147 "
+    "06ca6351 14292967 27b70a85 2e1b2138 4d2c6dfc 53380d13 650a7354 766a0abb 81c2c92e 92722c85 "
+    "a2bfe8a1 a81a664b c24b8b70 c76c51a3 d192e819 d6990624 f40e3585 106aa070 19a4c116 1e376c08 "
+    "2748774c 34b0bcb5 391c0cb3 4ed8aa4a 5b9cca4f 682e6ff3 748f82ee 78a5636f 84c87814 8cc70208 "
+    "90befffa a4506ceb bef9a3f7 c67178f2").split()]
+
+
+def _compress(h, block):
+    """One FIPS 180-4 compression (test checker for the states the host hasher hands out)."""
+    ror = lambda x, n: ((x >> n) | (x << (32 - n))) & 0xFFFFFFFF  # noqa: E731
+    w = [int.from_bytes(block[4 * t:4 * t + 4], "big") for t in range(16)]
+    for t in range(16, 64):
+        s0 = ror(w[t - 15], 7) ^ ror(w[t - 15], 18) ^ (w[t - 15] >> 3)
+        s1 = ror(w[t - 2], 17) ^ ror(w[t - 2], 19) ^ (w[t - 2] >> 10)
+        w.append((w[t - 16] + s0 + w[t - 7] + s1) & 0xFFFFFFFF)
+    a, b, c, d, e, f, g, hh = h
+    for t in range(64):
+        t1 = (hh + (ror(e, 6) ^ ror(e, 11) ^ ror(e, 25)) + ((e & f) ^ (~e & g)) + _K[t] + w[t])
+        t2 = (ror(a, 2) ^ ror(a, 13) ^ ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c))
+        hh, g, f, e, d, c, b, a = g, f, e, (d + t1) & 0xFFFFFFFF, c, b, a, (t1 + t2) & 0xFFFFFFFF
+    return [(x + y) & 0xFFFFFFFF for x, y in zip(h, [a, b, c, d, e, f, g, hh])]
+
+
+def test_state_after_full_blocks(lib):
+    """cec_sha256_host_state: each chain's hex and its state after len bytes (len a multiple of
+    64), in every form and lane position: the state equals a restatement's compression chain, and
+    its hex equals hashlib's."""
+    iv = [0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab,
+          0x5be0cd19]
+    rng = np.random.default_rng(12)
+    length = 64 * 5
+    bufs = [rng.integers(0, 256, length, dtype=np.uint8) for _ in range(19)]
+    want_state = []
+    for b in bufs:
+        h = list(iv)
+        for o in range(0, length, 64):
+            h = _compress(h, b[o:o + 64].tobytes())
+        want_state.append(h)
+    ptrs = (ctypes.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
+    for name in forms(lib):
+        lib.cec_host_sha_set_form(FORMS[name])
+        try:
+            for threads in (1, 4):
+                hexo = np.zeros(64 * len(bufs), np.uint8)
+                st = np.zeros(8 * len(bufs), np.uint32)
+                assert lib.cec_sha256_host_state(ptrs, len(bufs), length, hexo.ctypes.data,
+                                                 st.ctypes.data, threads) == 0
+                assert [list(st[8 * i:8 * i + 8]) for i in range(len(bufs))] == want_state, name
+                assert [bytes(hexo[64 * i:64 * i + 64]).decode() for i in range(len(bufs))] == \
+                    [hashlib.sha256(b).hexdigest() for b in bufs]
+        finally:
+            lib.cec_host_sha_set_form(-1)
+    assert lib.cec_sha256_host_state(ptrs, 1, 65, hexo.ctypes.data, st.ctypes.data, 1) == -1

@@ -101,6 +101,8 @@ extern "C" {
                                   stats: *mut cec_pipeline_stats) -> c_int;
     pub fn cec_sha256_host(bufs: *const *const u8, n: usize, len: usize, hex: *mut u8,
                            prefix_len: usize, prefix_hex: *mut u8, threads: c_int) -> c_int;
+    pub fn cec_sha256_host_state(bufs: *const *const u8, n: usize, len: usize, hex: *mut u8,
+                                 state_out: *mut u32, threads: c_int) -> c_int;
     pub fn cec_host_sha_set_form(form: c_int) -> c_int;
     pub fn cec_host_sha_form() -> c_int;
     pub fn cec_host_sha_pool_threads() -> c_int;
@@ -172,6 +174,10 @@ pub mod sys {
         pub fn cec_hashq_add(q: *mut cec_hashq, d_base: *const u8, n: usize, per: usize,
                              outer_stride: usize, inner_stride: usize, len: usize,
                              d_hex: *mut u8, hex_outer: usize, ticket: *mut u64) -> c_int;
+        pub fn cec_hashq_add_resume(q: *mut cec_hashq, d_base: *const u8, n: usize, per: usize,
+                                    outer_stride: usize, inner_stride: usize, len: usize,
+                                    start_len: usize, d_states: *const u32, d_hex: *mut u8,
+                                    hex_outer: usize, ticket: *mut u64) -> c_int;
         pub fn cec_hashq_add_prefix(q: *mut cec_hashq, d_base: *const u8, n: usize, per: usize,
                                     outer_stride: usize, inner_stride: usize, len: usize,
                                     d_hex: *mut u8, hex_outer: usize, prefix_len: usize,
