@@ -95,6 +95,12 @@ struct cec_pipeline {
   std::vector<uint8_t*> h_shex, h_fhex;  // pinned hex, per device slot
   hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr;
   std::vector<hipEvent_t> ev_h2d, ev_enc, ev_d2h, ev_hex;  // per device slot
+  // hybrid resume (per device slot): the host hashes fragment 0 of each segment and hands its
+  // chain state to the GPU queue, which continues the segment chain over fragments 1..k-1
+  std::vector<uint32_t*> h_state, d_state;
+  std::vector<hipEvent_t> ev_state;  // the states' H2D (h_state reusable once complete)
+  std::vector<bool> state_pending;
+  bool resume = false;
   cec_hashq* hq = nullptr;
   uint32_t tick_blocks = 0;
   // host hash jobs not yet known to be finished (they read the pinned ring)
@@ -115,6 +121,8 @@ struct cec_pipeline {
     bool gpu = false;         // some chains on the GPU hash queue (hex copied out of slot ds)
     bool gpu_seg = false;     // the segment chain too (GPU mode)
     bool host_frags = false;  // the host hashes every fragment chain of the batch
+    bool seg_resume = false;  // hybrid: fragment 0 on the host, the segment chain resumed on the GPU
+    bool resume_added = false;
     std::shared_ptr<hsha::JobState> j_seg, j_data, j_par;
     std::vector<const uint8_t*> p_seg, p_data, p_par;
     std::vector<uint8_t> shex, fhex;  // host-hashed records [nseg][64], [nseg][k+m][64]
@@ -135,6 +143,12 @@ struct cec_pipeline {
     for (auto* v : {&h_in, &h_par, &h_shex, &h_fhex})
       for (uint8_t* p : *v)
         if (p) (void)hipHostFree(p);
+    for (uint32_t* p : h_state)
+      if (p) (void)hipHostFree(p);
+    for (uint32_t* p : d_state)
+      if (p) (void)hipFree(p);
+    for (hipEvent_t e : ev_state)
+      if (e) (void)hipEventDestroy(e);
     for (auto* v : {&d_data, &d_par, &d_shex, &d_fhex})
       for (uint8_t* p : *v)
         if (p) (void)hipFree(p);
@@ -222,6 +236,20 @@ struct cec_pipeline {
         PL_TRY(hipHostMalloc(&h_shex[i], B * 64, hipHostMallocDefault));
         PL_TRY(hipHostMalloc(&h_fhex[i], B * (k + m) * 64, hipHostMallocDefault));
       }
+      // hybrid resume: needs fragment 0 on a block boundary (CEC_PIPELINE_NO_RESUME: off, A/B)
+      resume = mode == CEC_PIPE_HASH_HYBRID && F % 64 == 0 && k > 1 &&
+               !getenv("CEC_PIPELINE_NO_RESUME");
+      if (resume) {
+        h_state.assign(nd, nullptr);
+        d_state.assign(nd, nullptr);
+        ev_state.assign(nd, nullptr);
+        state_pending.assign(nd, false);
+        for (int i = 0; i < nd; ++i) {
+          PL_TRY(hipHostMalloc(&h_state[i], B * 32, hipHostMallocDefault));
+          PL_TRY(hipMalloc(&d_state[i], B * 32));
+          PL_TRY(hipEventCreateWithFlags(&ev_state[i], hipEventDisableTiming));
+        }
+      }
       size_t chains = (size_t)(window + 1) * B * (k + m + 1), cap = 1024;
       while (cap < chains) cap <<= 1;
       PL_RC(cec_hashq_create(device, cap, s_comp, &hq));
@@ -265,7 +293,29 @@ struct cec_pipeline {
     return cec_hashq_tick(hq, tick_blocks);
   }
 
+  // The resumed segment chains of a hybrid batch, once its fragment-0 host job is done: the
+  // states to the device, then the chains (from byte F of each segment, into the slot's segment
+  // hex), on the queue's stream. Their add is the batch's last, so its ticket.
+  int add_resume(Batch& b, bool block) {
+    if (!b.seg_resume || b.resume_added) return CEC_OK;
+    if (!hsha::ready(b.j_seg)) {
+      if (!block) return CEC_OK;
+      hsha::wait(b.j_seg, true);
+    }
+    PL_TRY(hipMemcpyAsync(d_state[b.ds], h_state[b.ds], b.nseg * 32, hipMemcpyHostToDevice,
+                          s_comp));
+    PL_TRY(hipEventRecord(ev_state[b.ds], s_comp));
+    state_pending[b.ds] = true;
+    uint64_t t = 0;
+    PL_RC(cec_hashq_add_resume(hq, d_data[b.ds], b.nseg, 1, SB, SB, SB, F, d_state[b.ds],
+                               d_shex[b.ds], 1, &t));
+    b.ticket = t;
+    b.resume_added = true;
+    return CEC_OK;
+  }
+
   bool hashed(const Batch& b) {
+    if (b.seg_resume && !b.resume_added) return false;
     int done = 0;
     (void)cec_hashq_status(hq, b.ticket, &done, nullptr, nullptr);
     return done != 0;
@@ -273,8 +323,9 @@ struct cec_pipeline {
 
   // Tick until the batch's chains are complete, then copy its hex out (on the compute stream).
   int copy_hex(Batch& b) {
+    PL_RC(add_resume(b, true));
     while (!hashed(b)) PL_RC(cec_hashq_tick(hq, tick_blocks));
-    if (b.gpu_seg)
+    if (b.gpu_seg || b.seg_resume)
       PL_TRY(hipMemcpyAsync(h_shex[b.ds], d_shex[b.ds], b.nseg * 64, hipMemcpyDeviceToHost,
                             s_comp));
     PL_TRY(hipMemcpyAsync(h_fhex[b.ds], d_fhex[b.ds], b.nseg * (k + m) * 64,
@@ -287,8 +338,9 @@ struct cec_pipeline {
   std::shared_ptr<hsha::JobState> host_job(std::vector<const uint8_t*>& ptrs, size_t len,
                                            uint8_t* hex, size_t per, size_t hex_outer,
                                            size_t prefix_len, uint8_t* prefix_hex,
-                                           size_t prefix_outer) {
+                                           size_t prefix_outer, uint32_t* state_out = nullptr) {
     hsha::Job j;
+    j.state_out = state_out;
     j.bufs = ptrs.data();
     j.n = ptrs.size();
     j.len = len;
@@ -313,8 +365,16 @@ struct cec_pipeline {
     const bool prefix = F % 64 == 0;
     b.p_seg.resize(b.nseg);
     for (size_t s = 0; s < b.nseg; ++s) b.p_seg[s] = base + s * SB;
-    b.j_seg = host_job(b.p_seg, SB, b.shex.data(), 1, 1, prefix ? F : 0,
-                       prefix ? b.fhex.data() : nullptr, n);
+    if (b.seg_resume) {
+      // fragment 0 only: its hex, and the chain state the GPU resumes the segment chain from
+      // (the slot's previous states must have been copied to the device first)
+      if (state_pending[b.ds]) (void)hipEventSynchronize(ev_state[b.ds]);
+      state_pending[b.ds] = false;
+      b.j_seg = host_job(b.p_seg, F, b.fhex.data(), 1, n, 0, nullptr, 1, h_state[b.ds]);
+    } else {
+      b.j_seg = host_job(b.p_seg, SB, b.shex.data(), 1, 1, prefix ? F : 0,
+                         prefix ? b.fhex.data() : nullptr, n);
+    }
     // data fragments the host hashes on their own chains: 1..k-1 with the prefix trick (0..k-1
     // without), for batches whose fragments are all on the host or, without the prefix trick,
     // hybrid batches too (their GPU part is the parity alone)
@@ -535,7 +595,8 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
       if (on_record && p->mode != CEC_PIPE_HASH_NONE) {
         const int g0 = b.gpu ? (b.gpu_seg ? 0 : p->hybrid_gpu_first()) : n;
         for (size_t s = 0; s < b.nseg; ++s) {
-          const uint8_t* sh = b.gpu_seg ? p->h_shex[b.ds] + s * 64 : b.shex.data() + s * 64;
+          const uint8_t* sh = b.gpu_seg || b.seg_resume ? p->h_shex[b.ds] + s * 64
+                                                        : b.shex.data() + s * 64;
           for (int f = 0; f < n; ++f) {
             const uint8_t* src = f >= g0 ? p->h_fhex[b.ds] + (s * n + f) * 64
                                          : b.fhex.data() + (s * n + f) * 64;
@@ -617,6 +678,7 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
     b.host_frags = host_frags;
     b.gpu = p->mode == CEC_PIPE_HASH_GPU || (p->mode == CEC_PIPE_HASH_HYBRID && !host_frags);
     b.gpu_seg = p->mode == CEC_PIPE_HASH_GPU;
+    b.seg_resume = p->resume && b.gpu && !b.gpu_seg;
     b.hex_copied = !b.gpu;
     fs.segments += nseg;
     fs.bytes += got;
@@ -640,6 +702,9 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
       PL_TRY(hipEventRecord(p->ev_hex[ds], p->s_comp));
       PL_RC(cec_hashq_tick(p->hq, p->tick_blocks));
     }
+    // resumed segment chains of the batches whose fragment-0 host jobs are done
+    if (p->resume)
+      for (auto& o : inflight) PL_RC(p->add_resume(o, false));
     const double tb = now_s();
     sec_per_byte = 0.5 * sec_per_byte + 0.5 * (tb - last_batch_t) / (double)got;
     last_batch_t = tb;
@@ -667,6 +732,8 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
     ++i;
   }
   // drain
+  if (p->resume)
+    for (auto& o : inflight) PL_RC(p->add_resume(o, true));
   if (p->hq) PL_RC(cec_hashq_finish(p->hq));
   if (i) PL_RC(records_through(i - 1));
   for (hipStream_t s : {p->s_h2d, p->s_comp, p->s_d2h})
