@@ -97,8 +97,8 @@ struct cec_pipeline {
   std::vector<hipEvent_t> ev_h2d, ev_enc, ev_d2h, ev_hex;  // per device slot
   // hybrid resume (per device slot): the host hashes fragment 0 of each segment and hands its
   // chain state to the GPU queue, which continues the segment chain over fragments 1..k-1
-  std::vector<uint32_t*> h_state, d_state;
-  std::vector<hipEvent_t> ev_state;  // the states' H2D (h_state reusable once complete)
+  std::vector<uint32_t*> h_state;    // pinned, read by the add kernel in place
+  std::vector<hipEvent_t> ev_state;  // after that add (h_state reusable once complete)
   std::vector<bool> state_pending;
   bool resume = false;
   cec_hashq* hq = nullptr;
@@ -145,8 +145,6 @@ struct cec_pipeline {
         if (p) (void)hipHostFree(p);
     for (uint32_t* p : h_state)
       if (p) (void)hipHostFree(p);
-    for (uint32_t* p : d_state)
-      if (p) (void)hipFree(p);
     for (hipEvent_t e : ev_state)
       if (e) (void)hipEventDestroy(e);
     for (auto* v : {&d_data, &d_par, &d_shex, &d_fhex})
@@ -236,17 +234,18 @@ struct cec_pipeline {
         PL_TRY(hipHostMalloc(&h_shex[i], B * 64, hipHostMallocDefault));
         PL_TRY(hipHostMalloc(&h_fhex[i], B * (k + m) * 64, hipHostMallocDefault));
       }
-      // hybrid resume: needs fragment 0 on a block boundary (CEC_PIPELINE_NO_RESUME: off, A/B)
+      // hybrid resume, opt-in (CEC_PIPELINE_RESUME=1): needs fragment 0 on a block boundary. It
+      // halves the host's hashing on hybrid batches, but inside the bench's process it cut the
+      // four-file stream from 36-41 to 25-26 GB/s (its GPU queue holds half again as many
+      // chains), profiles/r06/bench_resume_ab/
       resume = mode == CEC_PIPE_HASH_HYBRID && F % 64 == 0 && k > 1 &&
-               !getenv("CEC_PIPELINE_NO_RESUME");
+               getenv("CEC_PIPELINE_RESUME") != nullptr;
       if (resume) {
         h_state.assign(nd, nullptr);
-        d_state.assign(nd, nullptr);
         ev_state.assign(nd, nullptr);
         state_pending.assign(nd, false);
         for (int i = 0; i < nd; ++i) {
           PL_TRY(hipHostMalloc(&h_state[i], B * 32, hipHostMallocDefault));
-          PL_TRY(hipMalloc(&d_state[i], B * 32));
           PL_TRY(hipEventCreateWithFlags(&ev_state[i], hipEventDisableTiming));
         }
       }
@@ -302,13 +301,13 @@ struct cec_pipeline {
       if (!block) return CEC_OK;
       hsha::wait(b.j_seg, true);
     }
-    PL_TRY(hipMemcpyAsync(d_state[b.ds], h_state[b.ds], b.nseg * 32, hipMemcpyHostToDevice,
-                          s_comp));
-    PL_TRY(hipEventRecord(ev_state[b.ds], s_comp));
-    state_pending[b.ds] = true;
+    // the add kernel reads the states straight from the pinned host slot (no copy on the
+    // compute stream, where a small H2D would queue behind the batches' large copies)
     uint64_t t = 0;
-    PL_RC(cec_hashq_add_resume(hq, d_data[b.ds], b.nseg, 1, SB, SB, SB, F, d_state[b.ds],
+    PL_RC(cec_hashq_add_resume(hq, d_data[b.ds], b.nseg, 1, SB, SB, SB, F, h_state[b.ds],
                                d_shex[b.ds], 1, &t));
+    PL_TRY(hipEventRecord(ev_state[b.ds], s_comp));  // h_state[ds] reusable once read
+    state_pending[b.ds] = true;
     b.ticket = t;
     b.resume_added = true;
     return CEC_OK;

@@ -197,8 +197,9 @@ int cec_hashq_add_prefix(cec_hashq* q, const uint8_t* d_base, size_t n, size_t p
                          size_t hex_outer, size_t prefix_len, uint8_t* d_prefix_hex,
                          size_t prefix_hex_outer, uint64_t* ticket);
 /* cec_hashq_add of chains that resume after their first start_len bytes (a multiple of 64 within
- * len's full blocks): chain i starts from the SHA-256 state d_states[8 i .. 8 i + 7] (device
- * memory, the eight 32-bit words after start_len bytes, as cec_sha256_host_state gives them)
+ * len's full blocks): chain i starts from the SHA-256 state d_states[8 i .. 8 i + 7] (memory
+ * the device reads: device memory or pinned host memory, read by the add's kernel on the queue's
+ * stream; the eight 32-bit words after start_len bytes, as cec_sha256_host_state gives them)
  * and hashes bytes start_len .. len of its buffer. A segment chain continued on the GPU after
  * the host hashed its fragment 0. */
 int cec_hashq_add_resume(cec_hashq* q, const uint8_t* d_base, size_t n, size_t per,

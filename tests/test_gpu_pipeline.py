@@ -378,3 +378,24 @@ def test_encode_file_sharded_multi_process(orc, tmp_path, world):
     assert all(res[r] is None for r in range(1, world))
     segs, fh, size = res[0]
     assert segs == want and fh == orc.file_hash(want) and size == len(blob)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,seg", [(2, 1, 1 << 20), (4, 2, 4 * 4096)])
+def test_hybrid_resume_records(orc, monkeypatch, k, m, seg):
+    """The opt-in hybrid resume (CEC_PIPELINE_RESUME=1): the host hashes fragment 0 of each
+    segment and the GPU queue continues the segment chain from its state (cec_hashq_add_resume);
+    records of several ragged files in one run, and of one file with every batch on the GPU
+    (tail 0), equal the oracle's."""
+    from cess_amd.pipeline import RecordsSession
+    monkeypatch.setenv("CEC_PIPELINE_RESUME", "1")
+    sizes = [7 * seg + 5, 3 * seg, seg - 1, 11 * seg]
+    blobs = [np.random.default_rng(300 + i).integers(0, 256, n, dtype=np.uint8).tobytes()
+             for i, n in enumerate(sizes)]
+    want = [orc.segment_list(b, k, m, seg) for b in blobs]
+    for tail in (-1, 0):
+        with RecordsSession(k, m, seg, hash_on="hybrid", batch_segments=2, window=2,
+                            tail_batches=tail) as ses:
+            recs, _ = ses.encode_many(blobs)
+            for f, (r, w) in enumerate(zip(recs, want)):
+                assert [(x.hash, x.fragment_list) for x in r.segments] == w, (tail, f)
