@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Run while resume was the default and CEC_PIPELINE_NO_RESUME turned it off; it is now opt-in:
+# set CEC_PIPELINE_RESUME=1 for the "on" legs to repeat it.)
 # Hybrid resume (fragment 0 on the host, the segment chain continued on the GPU) against
 # CEC_PIPELINE_NO_RESUME=1: pipeline tests first, then the records placements, alternating.
 set -o pipefail

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Run while resume was the default and CEC_PIPELINE_NO_RESUME turned it off; it is now opt-in:
+# set CEC_PIPELINE_RESUME=1 for the "on" legs to repeat it.)
 # Hybrid resume A/B, stream only (4 x 1000-segment files), three alternating pairs.
 set -o pipefail
 OUT=gpurun_out/r06resume2; rm -rf $OUT; mkdir -p $OUT

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Run while resume was the default and CEC_PIPELINE_NO_RESUME turned it off; it is now opt-in:
+# set CEC_PIPELINE_RESUME=1 for the "on" legs to repeat it.)
 # Hybrid (with resume) stream at hash windows 32 / 48 / 64, with the wait trace.
 set -o pipefail
 OUT=gpurun_out/r06reswin; rm -rf $OUT; mkdir -p $OUT
