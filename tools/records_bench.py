@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--stream", type=int, default=0, help="files in the records_stream leg")
     ap.add_argument("--stream-segments", type=int, default=1000)
     ap.add_argument("--form", type=int, default=-1, help="cec_host_sha_set_form")
+    ap.add_argument("--pieces", action="store_true",
+                    help="stream files as in bench.py: the file buffer read as pieces")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime: torch first)
     from cess_amd import _lib
@@ -106,7 +108,15 @@ def main():
                    round(size / min(times) / 1e9, 2), "records_ok": ok, **info}
             print(json.dumps(out), flush=True)
             if a.stream and ses is not None:
-                files = [buf[:nstream]] * a.stream
+                if a.pieces:  # bench.py's host_e2e: the --gib buffer repeated up to the size
+                    pieces, left = [], nstream
+                    while left:
+                        take = min(left, size)
+                        pieces.append(buf[:take])
+                        left -= take
+                    files = [pieces] * a.stream
+                else:
+                    files = [buf[:nstream]] * a.stream
                 done_t = []
                 c0 = cpu_seconds()
                 t0 = time.perf_counter()
