@@ -254,7 +254,11 @@ struct cec_pipeline {
       PL_RC(cec_hashq_create(device, cap, s_comp, &hq));
       // GPU mode's longest chain is the segment's, hybrid's a fragment's
       const uint64_t blocks = cec::sha256_blocks(mode == CEC_PIPE_HASH_GPU ? SB : F);
-      tick_blocks = (uint32_t)((blocks + window - 1) / window);
+      // resumed segment chains join the queue when their fragment-0 host job is done, a batch
+      // or more after the batch's other chains: leave them a few ticks of slack, or the device
+      // slot's reuse (window + 3 batches later) ticks synchronously until they end
+      const uint64_t ticks = resume ? std::max(1, window - 4) : window;
+      tick_blocks = (uint32_t)((blocks + ticks - 1) / ticks);
     }
     return CEC_OK;
   }

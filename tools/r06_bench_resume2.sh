@@ -2,7 +2,8 @@
 # The bench line's host_e2e with the opt-in resume after the state ring change (4 nd state slots
 # instead of one per device slot), on and off; the pipeline tests (resume path included) first.
 # The ring variant existed for this measurement only (no change: profiles/r06/bench_resume_trace/)
-# and was reverted.
+# and was reverted. Run again with the tick slack for resumed chains (pipeline.cpp, window - 4
+# ticks per chain): profiles/r06/bench_resume_slack/.
 set -o pipefail
 OUT=gpurun_out/r06benchres2; rm -rf $OUT; mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
