@@ -235,9 +235,8 @@ struct cec_pipeline {
         PL_TRY(hipHostMalloc(&h_fhex[i], B * (k + m) * 64, hipHostMallocDefault));
       }
       // hybrid resume, opt-in (CEC_PIPELINE_RESUME=1): needs fragment 0 on a block boundary. It
-      // halves the host's hashing on hybrid batches, but inside the bench's process it cut the
-      // four-file stream from 36-41 to 25-26 GB/s (its GPU queue holds half again as many
-      // chains), profiles/r06/bench_resume_ab/
+      // halves the host's hashing on hybrid batches at the same stream rate (with the tick slack
+      // below; without it the bench's stream fell to 25-26 GB/s), profiles/r06/bench_resume_slack/
       resume = mode == CEC_PIPE_HASH_HYBRID && F % 64 == 0 && k > 1 &&
                getenv("CEC_PIPELINE_RESUME") != nullptr;
       if (resume) {
