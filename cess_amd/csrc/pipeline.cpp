@@ -234,11 +234,17 @@ struct cec_pipeline {
         PL_TRY(hipHostMalloc(&h_shex[i], B * 64, hipHostMallocDefault));
         PL_TRY(hipHostMalloc(&h_fhex[i], B * (k + m) * 64, hipHostMallocDefault));
       }
-      // hybrid resume, opt-in (CEC_PIPELINE_RESUME=1): needs fragment 0 on a block boundary. It
-      // halves the host's hashing on hybrid batches at the same stream rate (with the tick slack
-      // below; without it the bench's stream fell to 25-26 GB/s), profiles/r06/bench_resume_slack/
-      resume = mode == CEC_PIPE_HASH_HYBRID && F % 64 == 0 && k > 1 &&
-               getenv("CEC_PIPELINE_RESUME") != nullptr;
+      // hybrid resume: needs fragment 0 on a block boundary. It halves the host's hashing on
+      // hybrid batches (fragment 0 instead of the whole segment). With the host's 16 threads
+      // (~78 GB/s of hashing, ~1x the file's bytes to hash) the stream is PCIe-bound either way
+      // and resume did not pay in the bench's process; with fewer threads the host is the
+      // bound and resume lifts the stream (8 threads: 38.6 vs 35.2 GB/s, 6: 36.6 vs 28.5,
+      // profiles/r06/resume_threads/). So it is on below 12 threads: 12 hash ~59 GB/s at the
+      // ~4.9 GB/s per thread measured, above the ~50 GB/s PCIe stream. CEC_PIPELINE_RESUME=1 / 0
+      // forces it on / off.
+      const char* rv = getenv("CEC_PIPELINE_RESUME");
+      const bool want_resume = rv ? rv[0] != '0' : host_threads < 12;
+      resume = mode == CEC_PIPE_HASH_HYBRID && F % 64 == 0 && k > 1 && want_resume;
       if (resume) {
         h_state.assign(nd, nullptr);
         ev_state.assign(nd, nullptr);
@@ -747,9 +753,9 @@ int cec_pipeline_run_files(cec_pipeline* p, const cec_source* srcs, size_t nsrc,
     const double wall = now_s() - t0;
     const uint64_t xs = ps.x16_steps - ps0.x16_steps;
     fprintf(stderr, "cec_pipeline: %.4f s, read %.4f, wait %.4f (d2h %.4f, host slot %.4f, "
-            "records %.4f), mode %d, window %d, depth %d; host SHA workers busy %.3f s = %.2f of "
+            "records %.4f), mode %d, window %d, depth %d, resume %d; host SHA workers busy %.3f s = %.2f of "
             "%d threads, x16 steps %llu at %.1f lanes, SHA-NI steps %llu, spilled %llu\n", wall,
-            t_read, t_wait, w_d2h, w_slot, w_rec, p->mode, p->window, p->depth,
+            t_read, t_wait, w_d2h, w_slot, w_rec, p->mode, p->window, p->depth, (int)p->resume,
             ps.busy_s - ps0.busy_s, (ps.busy_s - ps0.busy_s) / (wall * p->host_threads),
             p->host_threads, (unsigned long long)xs,
             xs ? (double)(ps.x16_lane_steps - ps0.x16_lane_steps) / (double)xs : 0.0,

@@ -242,7 +242,10 @@ int cec_split_segment(const uint8_t* seg, size_t seg_len, int k, uint8_t* const*
  *                         other fragments' chains on the GPU queue, except for the last batches
  *                         of the run's last source, which the host hashes wholly (`tail_batches`;
  *                         -1 = auto: the batches whose GPU chains would finish after the source's
- *                         remaining bytes have landed; needs the source's size).
+ *                         remaining bytes have landed; needs the source's size). Below 12
+ *                         host_threads (or with CEC_PIPELINE_RESUME=1; =0 turns it off) the host
+ *                         hashes only fragment 0 and the GPU queue resumes the segment chain
+ *                         from its state (cec_hashq_add_resume): half the host's bytes.
  * The pipeline is reusable: keep one for many files (its pinned ring is pinned once).
  *   read(user, dst, cap): write up to cap source bytes at dst; return the count, 0 at the end,
  *     < 0 to abort (CEC_ECALLBACK).

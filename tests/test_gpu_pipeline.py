@@ -382,20 +382,27 @@ def test_encode_file_sharded_multi_process(orc, tmp_path, world):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,m,seg", [(2, 1, 1 << 20), (4, 2, 4 * 4096)])
-def test_hybrid_resume_records(orc, monkeypatch, k, m, seg):
-    """The opt-in hybrid resume (CEC_PIPELINE_RESUME=1): the host hashes fragment 0 of each
-    segment and the GPU queue continues the segment chain from its state (cec_hashq_add_resume);
-    records of several ragged files in one run, and of one file with every batch on the GPU
-    (tail 0), equal the oracle's."""
+@pytest.mark.parametrize("resume,threads", [("1", 16), (None, 4), ("0", 4)])
+def test_hybrid_resume_records(orc, monkeypatch, capfd, k, m, seg, resume, threads):
+    """The hybrid resume: the host hashes fragment 0 of each segment and the GPU queue continues
+    the segment chain from its state (cec_hashq_add_resume). Forced on (CEC_PIPELINE_RESUME=1),
+    on by itself below 12 host threads, and forced off there; records of several ragged files in
+    one run, and of one file with every batch on the GPU (tail 0), equal the oracle's."""
     from cess_amd.pipeline import RecordsSession
-    monkeypatch.setenv("CEC_PIPELINE_RESUME", "1")
+    if resume is None:
+        monkeypatch.delenv("CEC_PIPELINE_RESUME", raising=False)
+    else:
+        monkeypatch.setenv("CEC_PIPELINE_RESUME", resume)
+    monkeypatch.setenv("CEC_PIPELINE_TRACE", "1")  # its line says whether the run resumed
     sizes = [7 * seg + 5, 3 * seg, seg - 1, 11 * seg]
     blobs = [np.random.default_rng(300 + i).integers(0, 256, n, dtype=np.uint8).tobytes()
              for i, n in enumerate(sizes)]
     want = [orc.segment_list(b, k, m, seg) for b in blobs]
     for tail in (-1, 0):
         with RecordsSession(k, m, seg, hash_on="hybrid", batch_segments=2, window=2,
-                            tail_batches=tail) as ses:
+                            tail_batches=tail, host_threads=threads) as ses:
             recs, _ = ses.encode_many(blobs)
             for f, (r, w) in enumerate(zip(recs, want)):
                 assert [(x.hash, x.fragment_list) for x in r.segments] == w, (tail, f)
+        on = resume == "1" or (resume is None and threads < 12)
+        assert f"resume {int(on)};" in capfd.readouterr().err, tail
